@@ -1,0 +1,193 @@
+// bvh.cpp — binned-SAH bounding volume hierarchy over spheres.
+//
+// The reference's live path has no acceleration structure: hitWorld is a
+// linear closest-hit scan (internal/renderer/renderer.go:333-346), and its
+// only BVH (internal/optimization/spatial_acceleration.go:9-69) does not
+// compile.  This BVH is a pure accelerator introduced by the build for the
+// 10k-sphere configurations: traversal returns the
+// same closest hit as the linear scan (same Sphere.Hit arithmetic, exact-t
+// ties resolved by hittable index, as in the scan).
+//
+// Layout: nodes in depth-first order with the two children of an internal
+// node adjacent (left = i, right = i + 1), 32 B each, float bounds rounded
+// outward by one ulp so a box never excludes a point of its spheres.
+// Spheres are reordered so every leaf is a contiguous range.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "rt_internal.h"
+
+namespace rtgo {
+
+namespace {
+
+struct Box {
+  double lo[3], hi[3];
+  void reset() {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = INFINITY;
+      hi[k] = -INFINITY;
+    }
+  }
+  void grow(const Box& b) {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(lo[k], b.lo[k]);
+      hi[k] = std::max(hi[k], b.hi[k]);
+    }
+  }
+  void grow_pt(const double p[3]) {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(lo[k], p[k]);
+      hi[k] = std::max(hi[k], p[k]);
+    }
+  }
+  double area() const {
+    double e[3];
+    for (int k = 0; k < 3; ++k) e[k] = std::max(0.0, hi[k] - lo[k]);
+    return 2.0 * (e[0] * e[1] + e[1] * e[2] + e[2] * e[0]);
+  }
+};
+
+float down(double v) {
+  float f = (float)v;
+  if ((double)f > v) f = nextafterf(f, -INFINITY);
+  return nextafterf(f, -INFINITY);
+}
+float up(double v) {
+  float f = (float)v;
+  if ((double)f < v) f = nextafterf(f, INFINITY);
+  return nextafterf(f, INFINITY);
+}
+
+constexpr int kBins = 16;
+constexpr int kLeafMax = 4;
+
+}  // namespace
+
+void build_sphere_bvh(FlatScene* fs) {
+  fs->bvh.clear();
+  const int n = (int)fs->spheres.size();
+  if (n == 0) return;
+  std::vector<Box> pb(n);
+  std::vector<double> cen(3 * (size_t)n);
+  for (int i = 0; i < n; ++i) {
+    const DSphere& s = fs->spheres[i];
+    double r = fabs(s.r);
+    for (int k = 0; k < 3; ++k) {
+      pb[i].lo[k] = s.c[k] - r;
+      pb[i].hi[k] = s.c[k] + r;
+      cen[3 * (size_t)i + k] = s.c[k];
+    }
+  }
+  std::vector<int> idx(n);
+  for (int i = 0; i < n; ++i) idx[i] = i;
+
+  struct Task {
+    int node, first, count;
+  };
+  std::vector<DBVHNode> nodes;
+  nodes.reserve(2 * (size_t)n);
+  nodes.push_back(DBVHNode{});
+  std::vector<Task> stack;
+  stack.push_back({0, 0, n});
+  while (!stack.empty()) {
+    Task t = stack.back();
+    stack.pop_back();
+    Box b, cb;
+    b.reset();
+    cb.reset();
+    for (int i = t.first; i < t.first + t.count; ++i) {
+      b.grow(pb[idx[i]]);
+      cb.grow_pt(&cen[3 * (size_t)idx[i]]);
+    }
+    DBVHNode& nd = nodes[t.node];
+    for (int k = 0; k < 3; ++k) {
+      nd.lo[k] = down(b.lo[k]);
+      nd.hi[k] = up(b.hi[k]);
+    }
+    auto make_leaf = [&]() {
+      nodes[t.node].left_or_first = t.first;
+      nodes[t.node].count = t.count;
+    };
+    if (t.count <= kLeafMax) {
+      make_leaf();
+      continue;
+    }
+    // binned SAH along each axis
+    double best_cost = INFINITY;
+    int best_axis = -1, best_split = -1;
+    for (int ax = 0; ax < 3; ++ax) {
+      double ext = cb.hi[ax] - cb.lo[ax];
+      if (!(ext > 0)) continue;
+      Box bins[kBins];
+      int cnt[kBins] = {0};
+      for (int k = 0; k < kBins; ++k) bins[k].reset();
+      const double scale = kBins / ext;
+      for (int i = t.first; i < t.first + t.count; ++i) {
+        int bi = (int)((cen[3 * (size_t)idx[i] + ax] - cb.lo[ax]) * scale);
+        bi = std::min(std::max(bi, 0), kBins - 1);
+        bins[bi].grow(pb[idx[i]]);
+        cnt[bi]++;
+      }
+      double la[kBins], ra[kBins];
+      int lc[kBins], rc[kBins];
+      Box acc;
+      acc.reset();
+      int c = 0;
+      for (int k = 0; k < kBins; ++k) {
+        acc.grow(bins[k]);
+        c += cnt[k];
+        la[k] = acc.area();
+        lc[k] = c;
+      }
+      acc.reset();
+      c = 0;
+      for (int k = kBins - 1; k >= 0; --k) {
+        acc.grow(bins[k]);
+        c += cnt[k];
+        ra[k] = acc.area();
+        rc[k] = c;
+      }
+      for (int k = 0; k < kBins - 1; ++k) {
+        if (lc[k] == 0 || rc[k + 1] == 0) continue;
+        double cost = la[k] * lc[k] + ra[k + 1] * rc[k + 1];
+        if (cost < best_cost) {
+          best_cost = cost;
+          best_axis = ax;
+          best_split = k;
+        }
+      }
+    }
+    int mid;
+    if (best_axis < 0) {
+      // all centroids coincide: split by count
+      mid = t.first + t.count / 2;
+    } else {
+      const double ext = cb.hi[best_axis] - cb.lo[best_axis];
+      const double scale = kBins / ext;
+      auto it = std::partition(idx.begin() + t.first, idx.begin() + t.first + t.count, [&](int i) {
+        int bi = (int)((cen[3 * (size_t)i + best_axis] - cb.lo[best_axis]) * scale);
+        bi = std::min(std::max(bi, 0), kBins - 1);
+        return bi <= best_split;
+      });
+      mid = (int)(it - idx.begin());
+      if (mid == t.first || mid == t.first + t.count) mid = t.first + t.count / 2;
+    }
+    const int left = (int)nodes.size();
+    nodes.push_back(DBVHNode{});
+    nodes.push_back(DBVHNode{});
+    nodes[t.node].left_or_first = left;
+    nodes[t.node].count = 0;
+    stack.push_back({left + 1, mid, t.first + t.count - mid});
+    stack.push_back({left, t.first, mid - t.first});
+  }
+  std::vector<DSphere> reordered(n);
+  for (int i = 0; i < n; ++i) reordered[i] = fs->spheres[idx[i]];
+  fs->spheres.swap(reordered);
+  fs->bvh.swap(nodes);
+}
+
+}  // namespace rtgo

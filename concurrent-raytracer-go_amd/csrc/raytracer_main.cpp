@@ -1,0 +1,201 @@
+// raytracer_main.cpp — CLI mirroring cmd/raytracer/main.go:14-70.
+//
+//   raytracer <scene_file> <output_file> <width> <height>
+//             [--samples N] [--max-depth N] [--seed N] [--no-soft-shadows]
+//             [--no-recursive]
+//
+// Same positional arguments, stdout lines, ".png" default extension
+// (main.go:53-56) and benchmark_data.json next to the output
+// (main.go:64-69, renderer.go:473-485).  The render itself is rt_render()
+// on the GPU.  Deviations: ".ppm" outputs are written
+// as P3 PPM (Go writes PNG bytes whatever the extension), benchmark_data.json
+// gains the published rays_per_second / pixels_per_second fields
+// (README.md:60-61), and the optional flags above (the Go CLI never calls
+// the renderer's setters, settings.go:3-25).
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/time.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rt_api.h"
+
+static bool parse_int(const char* s, long long* out) {
+  // strconv.Atoi: optional sign, decimal digits only
+  if (!s || !*s) return false;
+  const char* p = s;
+  if (*p == '+' || *p == '-') ++p;
+  if (!*p) return false;
+  for (const char* q = p; *q; ++q)
+    if (*q < '0' || *q > '9') return false;
+  char* end = nullptr;
+  *out = strtoll(s, &end, 10);
+  return end && *end == 0;
+}
+
+static std::string dir_of(const std::string& path) {  // filepath.Dir
+  size_t s = path.find_last_of('/');
+  if (s == std::string::npos) return ".";
+  if (s == 0) return "/";
+  return path.substr(0, s);
+}
+
+static std::string ext_of(const std::string& path) {  // filepath.Ext
+  for (size_t i = path.size(); i-- > 0;) {
+    if (path[i] == '/') break;
+    if (path[i] == '.') return path.substr(i);
+  }
+  return "";
+}
+
+static std::string rfc3339nano_now() {
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  struct tm tmv;
+  localtime_r(&ts.tv_sec, &tmv);
+  char date[64];
+  strftime(date, sizeof date, "%Y-%m-%dT%H:%M:%S", &tmv);
+  char frac[16] = "";
+  if (ts.tv_nsec) {
+    snprintf(frac, sizeof frac, ".%09ld", ts.tv_nsec);
+    size_t n = strlen(frac);
+    while (n > 1 && frac[n - 1] == '0') frac[--n] = 0;
+  }
+  long off = tmv.tm_gmtoff;
+  char tz[16];
+  if (off == 0)
+    snprintf(tz, sizeof tz, "Z");
+  else
+    snprintf(tz, sizeof tz, "%c%02ld:%02ld", off < 0 ? '-' : '+', labs(off) / 3600, (labs(off) % 3600) / 60);
+  return std::string(date) + frac + tz;
+}
+
+int main(int argc, char** argv) {
+  std::vector<std::string> args;
+  rt_settings st;
+  rt_settings_default(&st);
+  st.num_workers = (int32_t)sysconf(_SC_NPROCESSORS_ONLN);  // runtime.NumCPU(), main.go:46
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    long long v;
+    auto need = [&](const char* name) -> const char* {
+      if (i + 1 >= argc) {
+        fprintf(stderr, "flag needs an argument: %s\n", name);
+        exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--samples") {
+      if (!parse_int(need("--samples"), &v) || v < 0) return 2;
+      st.samples = (int32_t)v;
+    } else if (a == "--max-depth") {
+      if (!parse_int(need("--max-depth"), &v)) return 2;
+      st.max_depth = (int32_t)v;
+    } else if (a == "--seed") {
+      if (!parse_int(need("--seed"), &v)) return 2;
+      st.seed = (uint64_t)v;
+    } else if (a == "--no-soft-shadows") {
+      st.soft_shadows = 0;
+    } else if (a == "--no-recursive") {
+      st.recursive_reflections = 0;
+    } else {
+      args.push_back(a);
+    }
+  }
+  if (args.size() < 4) {
+    printf("Usage: raytracer <scene_file> <output_file> <width> <height>\n");
+    printf("Example: raytracer scene.json output.png 800 600\n");
+    return 1;
+  }
+  const std::string scene_file = args[0];
+  const std::string output_file = args[1];
+  long long w, h;
+  if (!parse_int(args[2].c_str(), &w)) {
+    printf("Invalid width: %s\n", args[2].c_str());
+    return 1;
+  }
+  if (!parse_int(args[3].c_str(), &h)) {
+    printf("Invalid height: %s\n", args[3].c_str());
+    return 1;
+  }
+  printf("Loading scene from: %s\n", scene_file.c_str());
+  rt_scene_buf* sb = nullptr;
+  if (rt_scene_load_json(scene_file.c_str(), 0, &sb) != RT_OK) {
+    printf("Error loading scene: %s\n", rt_last_error());
+    return 1;
+  }
+  printf("Rendering at %lldx%lld resolution...\n", w, h);
+  fflush(stdout);
+  rt_scene_print_hittables(sb);
+  const rt_scene* scene = rt_scene_view(sb);
+  if (w <= 0 || h <= 0) {
+    // image.NewRGBA of an empty rectangle renders nothing; png.Encode then
+    // fails on a zero-sized image
+    printf("Error saving image: invalid image size %lldx%lld\n", w, h);
+    rt_scene_free(sb);
+    return 1;
+  }
+  const size_t npix = (size_t)w * (size_t)h;
+  std::vector<uint8_t> rgba(npix * 4);
+  rt_stats stats;
+  memset(&stats, 0, sizeof stats);
+  int rc = rt_render(scene, (int32_t)w, (int32_t)h, &st, nullptr, rgba.data(), &stats);
+  if (rc != RT_OK) {
+    fprintf(stderr, "render failed: %s\n", rt_last_error());
+    rt_scene_free(sb);
+    return 2;
+  }
+  static const char* features[] = {
+      "Improved metallic reflections with Fresnel effect",
+      "Shiny materials with configurable roughness and specular",
+      "Enhanced light source reflections",
+      "Better specular highlights for metallic surfaces",
+  };
+  printf("Rendering complete!\n");
+  printf("Enhanced materials features:\n");
+  for (const char* f : features) printf("- %s\n", f);
+
+  std::string out_path = output_file;
+  if (ext_of(out_path).empty()) out_path += ".png";
+  printf("Saving to: %s\n", out_path.c_str());
+  fflush(stdout);
+  rc = ext_of(out_path) == ".ppm" ? rt_write_ppm(out_path.c_str(), rgba.data(), (int32_t)w, (int32_t)h)
+                                  : rt_write_png(out_path.c_str(), rgba.data(), (int32_t)w, (int32_t)h);
+  if (rc != RT_OK) {
+    printf("Error saving image: %s\n", rt_last_error());
+    rt_scene_free(sb);
+    return 1;
+  }
+  // SaveBenchmarkData (renderer.go:473-485): BenchmarkData JSON, 2-space indent
+  std::string bench_path = dir_of(out_path) + "/benchmark_data.json";
+  FILE* f = fopen(bench_path.c_str(), "wb");
+  if (!f) {
+    printf("Error saving benchmark data: open %s failed\n", bench_path.c_str());
+  } else {
+    fprintf(f, "{\n");
+    fprintf(f, "  \"scene_name\": \"demo_scene\",\n");  // GetSceneName, scene.go:100-102
+    fprintf(f, "  \"resolution\": \"%lldx%lld\",\n", w, h);
+    fprintf(f, "  \"render_time_seconds\": %.17g,\n", stats.render_seconds);
+    fprintf(f, "  \"samples\": %d,\n", st.samples);
+    fprintf(f, "  \"max_depth\": %d,\n", st.max_depth);
+    fprintf(f, "  \"num_workers\": %d,\n", st.num_workers);
+    fprintf(f, "  \"objects\": %d,\n", stats.objects);
+    fprintf(f, "  \"lights\": %d,\n", stats.lights);
+    fprintf(f, "  \"timestamp\": \"%s\",\n", rfc3339nano_now().c_str());
+    fprintf(f, "  \"features\": [\n");
+    for (int i = 0; i < 4; ++i) fprintf(f, "    \"%s\"%s\n", features[i], i < 3 ? "," : "");
+    fprintf(f, "  ],\n");
+    fprintf(f, "  \"kernel_time_seconds\": %.17g,\n", stats.kernel_seconds);
+    fprintf(f, "  \"pixels_per_second\": %.17g,\n", stats.pixels_per_second);
+    fprintf(f, "  \"rays_per_second\": %.17g\n", stats.rays_per_second);
+    fprintf(f, "}");
+    fclose(f);
+    printf("Benchmark data saved\n");
+  }
+  rt_scene_free(sb);
+  return 0;
+}

@@ -1,0 +1,552 @@
+// rt_api.cpp — C ABI of librtgo.so (include/rt_api.h): scene flattening,
+// device residency, launches, blocking render.
+//
+// Replaces the Go seam *renderer.ParallelRenderer (renderer.go:54-126,
+// settings.go:3-25).  Compiled with -ffp-contract=off: the host-side
+// precomputations (cube vertices, triangle edges and normals, material
+// tables) must equal the values the reference computes per test.
+#include <hip/hip_runtime_api.h>
+#include <math.h>
+#include <string.h>
+
+#include <chrono>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_rng.h"
+#include "rt_internal.h"
+
+namespace rtgo {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      set_error(std::string(#expr) + " failed: " + hipGetErrorString(e_));             \
+      return RT_E_DEVICE;                                                               \
+    }                                                                                   \
+  } while (0)
+
+// ---------------------------------------------------------------- Go math
+static double go_min(double x, double y) {
+  if ((isinf(x) && x < 0) || (isinf(y) && y < 0)) return -INFINITY;
+  if (isnan(x) || isnan(y)) return NAN;
+  if (x == 0 && x == y) return signbit(x) ? x : y;
+  return x < y ? x : y;
+}
+
+struct v3 {
+  double x, y, z;
+};
+static v3 mk(double x, double y, double z) { return v3{x, y, z}; }
+static v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+static v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static v3 divs(v3 a, double s) { return mk(a.x / s, a.y / s, a.z / s); }
+static v3 cross(v3 a, v3 b) { return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+static v3 normalize(v3 a) {
+  double l = sqrt(a.x * a.x + a.y * a.y + a.z * a.z);
+  if (l == 0) return mk(0, 0, 0);
+  return divs(a, l);
+}
+static v3 arr(const double* p) { return mk(p[0], p[1], p[2]); }
+static void put(double* d, v3 v) {
+  d[0] = v.x;
+  d[1] = v.y;
+  d[2] = v.z;
+}
+
+// Material constructors (material.go:22-73,159-167,231-233,292-294;
+// advanced_materials.go:14-19,117-123) and the metallic tables the renderer
+// derives from GetMetallic (renderer.go:193-226,236-246,262-287).
+static DMat make_mat(const rt_material& m) {
+  DMat d;
+  memset(&d, 0, sizeof d);
+  d.kind = m.kind;
+  put(d.color, arr(m.color));
+  double metallic = 0.0;
+  switch (m.kind) {
+    case RT_MAT_METAL:
+    case RT_MAT_SHINY:
+      d.roughness = go_min(m.roughness, 1.0);
+      metallic = go_min(m.metallic, 1.0);
+      d.ior = 1.5;
+      put(d.albedo, arr(m.color));
+      if (m.kind == RT_MAT_METAL) {
+        d.rough_draw = d.roughness > 0.001;
+        d.fs = 0.6 + metallic * 0.4;
+        d.mf = 0.4 + metallic * 0.5;
+        d.blend_metal = metallic > 0.8;
+      } else {
+        d.rough_draw = d.roughness > 0;
+        d.fs = 0.4 + go_min(m.specular, 1.0) * 0.4;
+      }
+      break;
+    case RT_MAT_PERFECTMIRROR:
+      d.roughness = go_min(m.roughness, 1.0);
+      d.rough_draw = d.roughness > 0.001;
+      metallic = 1.0;
+      d.ior = 2.0;
+      put(d.albedo, arr(m.color));
+      break;
+    case RT_MAT_GLASS:
+      d.ior = m.refraction_index;
+      put(d.albedo, arr(m.color));
+      break;
+    case RT_MAT_DIELECTRIC:
+      d.ior = m.refraction_index;
+      put(d.albedo, mk(1.0, 1.0, 1.0));
+      break;
+    case RT_MAT_DIFFUSELIGHT:
+      put(d.emit, arr(m.color));
+      break;
+    default:  // lambertian
+      d.kind = RT_MAT_LAMBERTIAN;
+      put(d.albedo, arr(m.color));
+      break;
+  }
+  d.metallic = metallic;
+  {  // Schlick f0 = Pow((IOR-1)/(IOR+1), 2) — Go's Pow(x,2) rounds as x*x
+    double r = (d.ior - 1.0) / (d.ior + 1.0);
+    d.f0 = r * r;
+  }
+  d.ambient = 0.1;
+  if (metallic > 0.9)
+    d.ambient = 0.05;
+  else if (metallic > 0.7)
+    d.ambient = 0.07;
+  else if (metallic > 0.5)
+    d.ambient = 0.08;
+  d.diffuse_strength = 0.25;
+  if (metallic > 0.95)
+    d.diffuse_strength = 0.05;
+  else if (metallic > 0.9)
+    d.diffuse_strength = 0.08;
+  else if (metallic > 0.8)
+    d.diffuse_strength = 0.12;
+  else if (metallic > 0.7)
+    d.diffuse_strength = 0.15;
+  else if (metallic > 0.5)
+    d.diffuse_strength = 0.2;
+  d.spec_pow = metallic > 0.9 ? 64 : (metallic > 0.8 ? 48 : 32);
+  if (metallic > 0.95) {
+    d.rw = 0.85; d.dw = 0.15;
+  } else if (metallic > 0.9) {
+    d.rw = 0.8; d.dw = 0.2;
+  } else if (metallic > 0.8) {
+    d.rw = 0.75; d.dw = 0.25;
+  } else if (metallic > 0.7) {
+    d.rw = 0.7; d.dw = 0.3;
+  } else if (metallic > 0.5) {
+    d.rw = 0.6; d.dw = 0.4;
+  } else if (metallic > 0.2) {
+    d.rw = 0.4; d.dw = 0.6;
+  } else {
+    d.rw = 1.0; d.dw = 1.0;
+  }
+  return d;
+}
+
+static void push_tri(FlatScene* fs, v3 v0, v3 v1, v3 v2, int mat, int obj) {
+  DTri t;
+  memset(&t, 0, sizeof t);
+  v3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+  put(t.v0, v0);
+  put(t.e1, e1);
+  put(t.e2, e2);
+  put(t.n, normalize(cross(e1, e2)));  // NewTriangle, triangle.go:13-34
+  t.mat = mat;
+  t.obj = obj;
+  fs->tris.push_back(t);
+}
+
+void flatten_scene(const rt_scene& s, FlatScene* fs) {
+  *fs = FlatScene();
+  for (int i = 0; i < s.num_objects; ++i) {
+    const rt_object& o = s.objects[i];
+    const int mat = (int)fs->mats.size();
+    fs->mats.push_back(make_mat(o.material));
+    if (o.type == RT_OBJ_SPHERE) {
+      DSphere sp;
+      memset(&sp, 0, sizeof sp);
+      put(sp.c, arr(o.position));
+      sp.r = o.radius;
+      sp.mat = mat;
+      sp.obj = i;
+      fs->spheres.push_back(sp);
+    } else {  // createCube, scene.go:150-190
+      v3 pos = arr(o.position);
+      v3 h = divs(arr(o.size), 2.0);
+      v3 v[8] = {add(pos, mk(-h.x, -h.y, -h.z)), add(pos, mk(h.x, -h.y, -h.z)), add(pos, mk(h.x, h.y, -h.z)),
+                 add(pos, mk(-h.x, h.y, -h.z)),  add(pos, mk(-h.x, -h.y, h.z)), add(pos, mk(h.x, -h.y, h.z)),
+                 add(pos, mk(h.x, h.y, h.z)),    add(pos, mk(-h.x, h.y, h.z))};
+      static const int faces[6][4] = {{0, 1, 2, 3}, {1, 5, 6, 2}, {5, 4, 7, 6},
+                                      {4, 0, 3, 7}, {3, 2, 6, 7}, {4, 5, 1, 0}};
+      for (int f = 0; f < 6; ++f) {
+        push_tri(fs, v[faces[f][0]], v[faces[f][1]], v[faces[f][2]], mat, i);
+        push_tri(fs, v[faces[f][0]], v[faces[f][2]], v[faces[f][3]], mat, i);
+      }
+    }
+  }
+  for (int i = 0; i < s.num_lights; ++i) {
+    DLight l;
+    memset(&l, 0, sizeof l);
+    put(l.pos, arr(s.lights[i].position));
+    put(l.color, arr(s.lights[i].color));
+    l.intensity = s.lights[i].intensity;
+    fs->lights.push_back(l);
+  }
+  put(fs->cam_pos, arr(s.camera.position));
+  fs->aspect = s.camera.aspect_ratio;
+  fs->objects = s.num_objects;
+}
+
+static int validate_scene(const rt_scene* s) {
+  if (!s) {
+    set_error("scene is NULL");
+    return RT_E_INVALID;
+  }
+  if (s->num_objects < 0 || s->num_lights < 0 || (s->num_objects > 0 && !s->objects) ||
+      (s->num_lights > 0 && !s->lights)) {
+    set_error("scene arrays inconsistent");
+    return RT_E_INVALID;
+  }
+  for (int i = 0; i < s->num_objects; ++i) {
+    const rt_object& o = s->objects[i];
+    if (o.type != RT_OBJ_SPHERE && o.type != RT_OBJ_CUBE) {
+      set_error("object " + std::to_string(i) + ": unknown type " + std::to_string(o.type));
+      return RT_E_INVALID;
+    }
+    if (o.material.kind < RT_MAT_LAMBERTIAN || o.material.kind > RT_MAT_DIFFUSELIGHT) {
+      set_error("object " + std::to_string(i) + ": unknown material kind");
+      return RT_E_INVALID;
+    }
+  }
+  return RT_OK;
+}
+
+static int validate_settings(const rt_settings* st, int32_t w, int32_t h) {
+  if (!st) {
+    set_error("settings is NULL");
+    return RT_E_INVALID;
+  }
+  if (w <= 0 || h <= 0 || (long long)w * h > (1LL << 31) / 4) {
+    set_error("invalid image size " + std::to_string(w) + "x" + std::to_string(h));
+    return RT_E_INVALID;
+  }
+  if (st->samples < 0 || st->samples > (1 << 24)) {
+    set_error("invalid samples");
+    return RT_E_INVALID;
+  }
+  return RT_OK;
+}
+
+}  // namespace rtgo
+
+using namespace rtgo;
+
+// ======================================================================== ABI
+struct rt_context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool have_scene = false;
+  FlatScene flat;
+  void* d_scene = nullptr;  // one allocation: spheres | tris | mats | lights | bvh
+  size_t d_scene_bytes = 0;
+  const DSphere* d_spheres = nullptr;
+  const DTri* d_tris = nullptr;
+  const DMat* d_mats = nullptr;
+  const DLight* d_lights = nullptr;
+  const DBVHNode* d_bvh = nullptr;
+  unsigned long long* d_counts = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool have_timing = false;
+};
+
+extern "C" {
+
+void rt_settings_default(rt_settings* s) {
+  if (!s) return;
+  memset(s, 0, sizeof *s);
+  // NewParallelRenderer defaults, renderer.go:54-65
+  s->samples = 100;
+  s->max_depth = 50;
+  s->anti_aliasing = 1;
+  s->recursive_reflections = 1;
+  s->soft_shadows = 1;
+  s->depth_of_field = 0;
+  s->num_workers = 1;
+  s->seed = 1;
+}
+
+int32_t rt_abi_version(void) { return RT_ABI_VERSION; }
+
+const char* rt_last_error(void) { return g_last_error.c_str(); }
+
+int32_t rt_num_tiles(int32_t w, int32_t h) {
+  if (w <= 0 || h <= 0) return 0;
+  return ((w + 31) / 32) * ((h + 31) / 32);
+}
+
+int32_t rt_tiles_for_rank(int32_t w, int32_t h, int32_t rank, int32_t world) {
+  int32_t n = rt_num_tiles(w, h);
+  if (world < 1 || rank < 0 || rank >= world || rank >= n) return 0;
+  return (n - rank + world - 1) / world;
+}
+
+int rt_context_create(int32_t device, rt_context** out) {
+  if (!out) {
+    set_error("out is NULL");
+    return RT_E_INVALID;
+  }
+  *out = nullptr;
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) {
+    set_error("device " + std::to_string(device) + " out of range (" + std::to_string(n) + " devices)");
+    return RT_E_DEVICE;
+  }
+  HIP_TRY(hipSetDevice(device));
+  rt_context* c = new rt_context();
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->d_counts, 16 * sizeof(unsigned long long));
+  if (e != hipSuccess) {
+    set_error(std::string("context init failed: ") + hipGetErrorString(e));
+    rt_context_destroy(c);
+    return RT_E_DEVICE;
+  }
+  *out = c;
+  return RT_OK;
+}
+
+void rt_context_destroy(rt_context* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->d_scene) (void)hipFree(c->d_scene);
+  if (c->d_counts) (void)hipFree(c->d_counts);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
+  if (!c) {
+    set_error("context is NULL");
+    return RT_E_INVALID;
+  }
+  int rc = validate_scene(s);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  flatten_scene(*s, &c->flat);
+  const bool want_bvh = force_bvh > 0 || (force_bvh == 0 && c->flat.spheres.size() > 64);
+  if (want_bvh && !c->flat.tris.empty()) {
+    if (force_bvh > 0) {
+      set_error("BVH supports sphere-only scenes");
+      return RT_E_INVALID;
+    }
+  } else if (want_bvh) {
+    build_sphere_bvh(&c->flat);
+  }
+  const FlatScene& f = c->flat;
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  size_t off_s = 0;
+  size_t off_t = off_s + al(f.spheres.size() * sizeof(DSphere));
+  size_t off_m = off_t + al(f.tris.size() * sizeof(DTri));
+  size_t off_l = off_m + al(f.mats.size() * sizeof(DMat));
+  size_t off_b = off_l + al(f.lights.size() * sizeof(DLight));
+  size_t total = off_b + al(f.bvh.size() * sizeof(DBVHNode)) + 256;
+  if (c->stream) HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->d_scene && c->d_scene_bytes < total) {
+    HIP_TRY(hipFree(c->d_scene));
+    c->d_scene = nullptr;
+  }
+  if (!c->d_scene) {
+    HIP_TRY(hipMalloc(&c->d_scene, total));
+    c->d_scene_bytes = total;
+  }
+  char* base = (char*)c->d_scene;
+  std::vector<char> host(total, 0);
+  memcpy(host.data() + off_s, f.spheres.data(), f.spheres.size() * sizeof(DSphere));
+  memcpy(host.data() + off_t, f.tris.data(), f.tris.size() * sizeof(DTri));
+  memcpy(host.data() + off_m, f.mats.data(), f.mats.size() * sizeof(DMat));
+  memcpy(host.data() + off_l, f.lights.data(), f.lights.size() * sizeof(DLight));
+  memcpy(host.data() + off_b, f.bvh.data(), f.bvh.size() * sizeof(DBVHNode));
+  HIP_TRY(hipMemcpy(base, host.data(), total, hipMemcpyHostToDevice));
+  c->d_spheres = (const DSphere*)(base + off_s);
+  c->d_tris = (const DTri*)(base + off_t);
+  c->d_mats = (const DMat*)(base + off_m);
+  c->d_lights = (const DLight*)(base + off_l);
+  c->d_bvh = (const DBVHNode*)(base + off_b);
+  c->have_scene = true;
+  return RT_OK;
+}
+
+int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settings* st, int32_t rank,
+                            int32_t world, int32_t layout, float* d_linear, uint8_t* d_rgba, void* stream,
+                            rt_counts* counts) {
+  if (!c || !c->have_scene) {
+    set_error("context has no scene");
+    return RT_E_INVALID;
+  }
+  int rc = validate_settings(st, w, h);
+  if (rc) return rc;
+  if (world < 1 || rank < 0 || rank >= world) {
+    set_error("invalid rank/world");
+    return RT_E_INVALID;
+  }
+  if (layout != RT_LAYOUT_IMAGE && layout != RT_LAYOUT_PACKED_TILES) {
+    set_error("invalid layout");
+    return RT_E_INVALID;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  const FlatScene& f = c->flat;
+  KParams p;
+  memset(&p, 0, sizeof p);
+  p.spheres = c->d_spheres;
+  p.tris = c->d_tris;
+  p.mats = c->d_mats;
+  p.lights = c->d_lights;
+  p.bvh = c->d_bvh;
+  p.out_linear = d_linear;
+  p.out_rgba = d_rgba;
+  p.counts = counts ? c->d_counts : nullptr;
+  memcpy(p.cam, f.cam_pos, sizeof p.cam);
+  p.aspect = f.aspect;
+  p.seed_key = rt_rng_seed_key(st->seed);
+  p.ns = (int32_t)f.spheres.size();
+  p.nt = (int32_t)f.tris.size();
+  p.nl = (int32_t)f.lights.size();
+  p.use_bvh = f.bvh.empty() ? 0 : 1;
+  p.W = w;
+  p.H = h;
+  p.spp = st->samples;
+  p.max_depth = st->max_depth;
+  p.recursive = st->recursive_reflections != 0;
+  p.soft = st->soft_shadows != 0;
+  p.rank = rank;
+  p.world = world;
+  p.tiles_x = (w + 31) / 32;
+  p.ntiles = rt_num_tiles(w, h);
+  // sample slices per pixel: enough lanes per pixel to fill the chip even
+  // when only a few tiles hold geometry
+  int S = 16;
+  while (S > 1 && S > st->samples) S >>= 1;
+  p.slices = S;
+  p.pix_per_wg = 256 / S;
+  p.blk_w = p.pix_per_wg >= 32 ? 32 : p.pix_per_wg;
+  p.blk_h = p.pix_per_wg / p.blk_w;
+  p.layout = layout;
+  const int local_tiles = rt_tiles_for_rank(w, h, rank, world);
+  p.num_wgs = local_tiles * (1024 / p.pix_per_wg);
+  // the caller's stream, as given (NULL = the legacy default stream)
+  hipStream_t s = (hipStream_t)stream;
+  if (counts) HIP_TRY(hipMemsetAsync(c->d_counts, 0, 16 * sizeof(unsigned long long), s));
+  HIP_TRY(hipEventRecord(c->ev0, s));
+  int e = launch_render(p, counts != nullptr, s);
+  if (e != hipSuccess) {
+    set_error(std::string("render launch failed: ") + hipGetErrorString((hipError_t)e));
+    return RT_E_DEVICE;
+  }
+  HIP_TRY(hipEventRecord(c->ev1, s));
+  c->last_stream = s;
+  c->have_timing = true;
+  if (counts) {
+    unsigned long long h_c[16];
+    HIP_TRY(hipMemcpyAsync(h_c, c->d_counts, sizeof h_c, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    counts->camera_rays = h_c[0];
+    counts->bounce_rays = h_c[1];
+    counts->shadow_rays = h_c[2];
+    counts->sphere_tests = h_c[3];
+    counts->triangle_tests = h_c[4];
+    counts->box_tests = h_c[5];
+    counts->shade_events = h_c[6];
+    counts->light_evals = h_c[7];
+    counts->rng_draws = h_c[8];
+  }
+  return RT_OK;
+}
+
+int rt_context_last_kernel_seconds(rt_context* c, double* seconds) {
+  if (!c || !seconds || !c->have_timing) {
+    set_error("no timed launch on this context");
+    return RT_E_INVALID;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipEventSynchronize(c->ev1));
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  *seconds = ms * 1e-3;
+  return RT_OK;
+}
+
+int rt_unpack_tiles_async(int32_t w, int32_t h, int32_t world, int32_t max_local, const float* pl,
+                          const uint8_t* pr, float* ol, uint8_t* orgba, void* stream) {
+  if (w <= 0 || h <= 0 || world < 1 || max_local < 0) {
+    set_error("invalid unpack arguments");
+    return RT_E_INVALID;
+  }
+  int e = launch_unpack(w, h, world, max_local, pl, pr, ol, orgba, stream);
+  if (e != hipSuccess) {
+    set_error(std::string("unpack launch failed: ") + hipGetErrorString((hipError_t)e));
+    return RT_E_DEVICE;
+  }
+  return RT_OK;
+}
+
+int rt_render(const rt_scene* scene, int32_t w, int32_t h, const rt_settings* st, float* out_linear,
+              uint8_t* out_rgba, rt_stats* stats) {
+  int rc = validate_scene(scene);
+  if (rc) return rc;
+  rc = validate_settings(st, w, h);
+  if (rc) return rc;
+  auto t0 = std::chrono::steady_clock::now();
+  rt_context* c = nullptr;
+  rc = rt_context_create(0, &c);
+  if (rc) return rc;
+  struct Guard {
+    rt_context* c;
+    float* dl = nullptr;
+    uint8_t* dr = nullptr;
+    ~Guard() {
+      if (dl) (void)hipFree(dl);
+      if (dr) (void)hipFree(dr);
+      rt_context_destroy(c);
+    }
+  } g{c};
+  rc = rt_context_set_scene(c, scene, 0);
+  if (rc) return rc;
+  const size_t npix = (size_t)w * h;
+  HIP_TRY(hipMalloc((void**)&g.dl, npix * 3 * sizeof(float)));
+  HIP_TRY(hipMalloc((void**)&g.dr, npix * 4));
+  rc = rt_context_render_async(c, w, h, st, 0, 1, RT_LAYOUT_IMAGE, g.dl, g.dr, c->stream, nullptr);
+  if (rc) return rc;
+  if (out_linear)
+    HIP_TRY(hipMemcpyAsync(out_linear, g.dl, npix * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  if (out_rgba) HIP_TRY(hipMemcpyAsync(out_rgba, g.dr, npix * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  double ks = 0;
+  rc = rt_context_last_kernel_seconds(c, &ks);
+  if (rc) return rc;
+  double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (stats) {
+    stats->render_seconds = secs;
+    stats->kernel_seconds = ks;
+    stats->rays_per_second = (double)npix * st->samples / secs;
+    stats->pixels_per_second = (double)npix / secs;
+    stats->objects = c->flat.objects;
+    stats->lights = (int32_t)c->flat.lights.size();
+  }
+  return RT_OK;
+}
+
+}  // extern "C"

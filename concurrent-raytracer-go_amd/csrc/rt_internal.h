@@ -1,0 +1,69 @@
+// rt_internal.h — host-side interfaces between the C ABI (rt_api.cpp), the
+// kernels (rt_kernel.hip), the scene loader (scene_json.cpp), the BVH
+// builder (bvh.cpp) and the output writers (image_io.cpp).
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rt_api.h"
+#include "rt_scene_dev.h"
+
+namespace rtgo {
+
+void set_error(const std::string& msg);
+
+// ---------------------------------------------------------------- scene
+struct FlatScene {
+  std::vector<DSphere> spheres;
+  std::vector<DTri> tris;
+  std::vector<DMat> mats;
+  std::vector<DLight> lights;
+  std::vector<DBVHNode> bvh;  // empty => linear scan
+  double cam_pos[3] = {0, 0, 0};
+  double aspect = 0;
+  int32_t objects = 0;        // len(hittables)
+};
+
+// GetHittables + createCube + material constructors (scene.go:59-190).
+void flatten_scene(const rt_scene& s, FlatScene* out);
+// Binned-SAH BVH over out->spheres (reorders spheres). Requires no triangles.
+void build_sphere_bvh(FlatScene* fs);
+
+// ---------------------------------------------------------------- kernels
+struct KParams {
+  const DSphere* spheres;
+  const DTri* tris;
+  const DMat* mats;
+  const DLight* lights;
+  const DBVHNode* bvh;
+  float* out_linear;
+  uint8_t* out_rgba;
+  unsigned long long* counts;  // 9 counters (rt_counts order) or null
+  double cam[3];
+  double aspect;
+  uint64_t seed_key;
+  int32_t ns, nt, nl, use_bvh;
+  int32_t W, H;
+  int32_t spp, max_depth;
+  int32_t recursive, soft;
+  int32_t rank, world;
+  int32_t tiles_x, ntiles;
+  int32_t slices;     // S: sample slices per pixel
+  int32_t pix_per_wg; // P = 256 / S
+  int32_t blk_w, blk_h;
+  int32_t layout;     // RT_LAYOUT_*
+  int32_t num_wgs;
+};
+
+// Enqueue the render kernel; returns hipError_t as int.
+int launch_render(const KParams& p, bool count, void* stream);
+int launch_unpack(int32_t W, int32_t H, int32_t world, int32_t max_local, const float* pl, const uint8_t* pr,
+                  float* ol, uint8_t* orgba, void* stream);
+
+// ---------------------------------------------------------------- output
+double go_pow_tonemap(double x);  // Pow(x, 1/2.2) with Go's special cases
+void tonemap_to_rgba(const double c[3], uint8_t out[4]);
+
+}  // namespace rtgo

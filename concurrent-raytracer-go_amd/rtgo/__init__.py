@@ -1,0 +1,501 @@
+"""rtgo — Python mirror of the reference's renderer interface over librtgo.so.
+
+The reference's seam is the Go method set of ``*renderer.ParallelRenderer``
+(internal/renderer/renderer.go:54-126, settings.go:3-36) plus
+``scene.LoadFromFile`` (internal/scene/scene.go:45-57).  This module exposes
+the same names (snake_case) on top of the C ABI in include/rt_api.h; the
+compute path is the gfx950 kernel inside librtgo.so.  There is no CPU
+fallback: rendering without a GPU raises ``RenderError``.
+
+The library is loaded lazily.  When PyTorch is already imported its HIP
+runtime (same soname, libamdhip64.so.7) is the one librtgo binds to, so
+torch device pointers and streams can be passed to ``Context``.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import time
+from datetime import datetime, timezone
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "librtgo.so")
+
+RT_OK = 0
+RT_OBJ_SPHERE, RT_OBJ_CUBE = 0, 1
+MATERIAL_KINDS = {
+    "lambertian": 0,
+    "metal": 1,
+    "shiny": 2,
+    "perfectmirror": 3,
+    "glass": 4,
+    "dielectric": 5,
+    "diffuselight": 6,
+}
+RT_LAYOUT_IMAGE, RT_LAYOUT_PACKED_TILES = 0, 1
+
+
+class RenderError(RuntimeError):
+    """A librtgo call failed (message from rt_last_error)."""
+
+
+# --------------------------------------------------------------- C structs
+class Material(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("_pad", ctypes.c_int32),
+        ("color", ctypes.c_double * 3),
+        ("roughness", ctypes.c_double),
+        ("metallic", ctypes.c_double),
+        ("specular", ctypes.c_double),
+        ("refraction_index", ctypes.c_double),
+    ]
+
+
+class Object(ctypes.Structure):
+    _fields_ = [
+        ("type", ctypes.c_int32),
+        ("_pad", ctypes.c_int32),
+        ("position", ctypes.c_double * 3),
+        ("size", ctypes.c_double * 3),
+        ("radius", ctypes.c_double),
+        ("material", Material),
+    ]
+
+
+class Light(ctypes.Structure):
+    _fields_ = [
+        ("position", ctypes.c_double * 3),
+        ("color", ctypes.c_double * 3),
+        ("intensity", ctypes.c_double),
+    ]
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [
+        ("position", ctypes.c_double * 3),
+        ("look_at", ctypes.c_double * 3),
+        ("up", ctypes.c_double * 3),
+        ("fov", ctypes.c_double),
+        ("aspect_ratio", ctypes.c_double),
+    ]
+
+
+class SceneView(ctypes.Structure):
+    _fields_ = [
+        ("camera", Camera),
+        ("objects", ctypes.POINTER(Object)),
+        ("num_objects", ctypes.c_int32),
+        ("_pad0", ctypes.c_int32),
+        ("lights", ctypes.POINTER(Light)),
+        ("num_lights", ctypes.c_int32),
+        ("_pad1", ctypes.c_int32),
+    ]
+
+
+class Settings(ctypes.Structure):
+    _fields_ = [
+        ("samples", ctypes.c_int32),
+        ("max_depth", ctypes.c_int32),
+        ("anti_aliasing", ctypes.c_int32),
+        ("recursive_reflections", ctypes.c_int32),
+        ("soft_shadows", ctypes.c_int32),
+        ("depth_of_field", ctypes.c_int32),
+        ("num_workers", ctypes.c_int32),
+        ("_pad", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("render_seconds", ctypes.c_double),
+        ("kernel_seconds", ctypes.c_double),
+        ("rays_per_second", ctypes.c_double),
+        ("pixels_per_second", ctypes.c_double),
+        ("objects", ctypes.c_int32),
+        ("lights", ctypes.c_int32),
+    ]
+
+
+COUNT_FIELDS = [
+    "camera_rays",
+    "bounce_rays",
+    "shadow_rays",
+    "sphere_tests",
+    "triangle_tests",
+    "box_tests",
+    "shade_events",
+    "light_evals",
+    "rng_draws",
+]
+
+
+class Counts(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in COUNT_FIELDS]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n in COUNT_FIELDS}
+
+
+# the symbols include/rt_api.h declares (checked by tests/test_abi.py)
+EXPORTED_SYMBOLS = [
+    "rt_settings_default",
+    "rt_abi_version",
+    "rt_last_error",
+    "rt_scene_load_json",
+    "rt_scene_parse_json",
+    "rt_scene_view",
+    "rt_scene_warnings",
+    "rt_scene_free",
+    "rt_scene_print_hittables",
+    "rt_render",
+    "rt_context_create",
+    "rt_context_destroy",
+    "rt_context_set_scene",
+    "rt_num_tiles",
+    "rt_tiles_for_rank",
+    "rt_context_render_async",
+    "rt_unpack_tiles_async",
+    "rt_context_last_kernel_seconds",
+    "rt_tonemap_rgba",
+    "rt_write_png",
+    "rt_write_ppm",
+]
+
+_lib = None
+
+
+def lib():
+    """Load librtgo.so (once) and declare the C signatures."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RenderError(
+            f"{LIB_PATH} is missing: build it with `make -C concurrent-raytracer-go_amd` "
+            "(or __graft_entry__.build())"
+        )
+    # One HIP runtime per process: torch bundles libamdhip64.so (soname
+    # libamdhip64.so.7) and loads it by a path the dynamic loader cannot
+    # match against an already-loaded /opt/rocm copy, so torch must come
+    # first; librtgo's DT_NEEDED libamdhip64.so.7 then binds to torch's copy.
+    if os.environ.get("RTGO_NO_TORCH", "0") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_size_t
+    sig = {
+        "rt_settings_default": (None, [ctypes.POINTER(Settings)]),
+        "rt_abi_version": (i32, []),
+        "rt_last_error": (ctypes.c_char_p, []),
+        "rt_scene_load_json": (ctypes.c_int, [ctypes.c_char_p, i32, ctypes.POINTER(vp)]),
+        "rt_scene_parse_json": (ctypes.c_int, [ctypes.c_char_p, sz, i32, ctypes.POINTER(vp)]),
+        "rt_scene_view": (ctypes.POINTER(SceneView), [vp]),
+        "rt_scene_warnings": (i32, [vp]),
+        "rt_scene_free": (None, [vp]),
+        "rt_scene_print_hittables": (ctypes.c_int, [vp]),
+        "rt_render": (
+            ctypes.c_int,
+            [ctypes.POINTER(SceneView), i32, i32, ctypes.POINTER(Settings), vp, vp, ctypes.POINTER(Stats)],
+        ),
+        "rt_context_create": (ctypes.c_int, [i32, ctypes.POINTER(vp)]),
+        "rt_context_destroy": (None, [vp]),
+        "rt_context_set_scene": (ctypes.c_int, [vp, ctypes.POINTER(SceneView), i32]),
+        "rt_num_tiles": (i32, [i32, i32]),
+        "rt_tiles_for_rank": (i32, [i32, i32, i32, i32]),
+        "rt_context_render_async": (
+            ctypes.c_int,
+            [vp, i32, i32, ctypes.POINTER(Settings), i32, i32, i32, vp, vp, vp, ctypes.POINTER(Counts)],
+        ),
+        "rt_unpack_tiles_async": (ctypes.c_int, [i32, i32, i32, i32, vp, vp, vp, vp, vp]),
+        "rt_context_last_kernel_seconds": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
+        "rt_tonemap_rgba": (None, [vp, i32, vp]),
+        "rt_write_png": (ctypes.c_int, [ctypes.c_char_p, vp, i32, i32]),
+        "rt_write_ppm": (ctypes.c_int, [ctypes.c_char_p, vp, i32, i32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != RT_OK:
+        msg = lib().rt_last_error()
+        raise RenderError(f"librtgo error {rc}: {msg.decode() if msg else ''}")
+
+
+def default_settings() -> Settings:
+    s = Settings()
+    lib().rt_settings_default(ctypes.byref(s))
+    return s
+
+
+# --------------------------------------------------------------- scene
+class Scene:
+    """A loaded scene (scene.Scene, internal/scene/scene.go:12-16)."""
+
+    def __init__(self, handle=None, objects=None, lights=None, camera=None):
+        self._handle = handle
+        if handle is not None:
+            self._view = lib().rt_scene_view(handle).contents
+        else:
+            self._objects = (Object * max(1, len(objects)))(*objects)
+            self._lights = (Light * max(1, len(lights)))(*lights)
+            v = SceneView()
+            v.camera = camera
+            v.objects = ctypes.cast(self._objects, ctypes.POINTER(Object))
+            v.num_objects = len(objects)
+            v.lights = ctypes.cast(self._lights, ctypes.POINTER(Light))
+            v.num_lights = len(lights)
+            self._view = v
+
+    @classmethod
+    def load_from_file(cls, path: str) -> "Scene":
+        """scene.LoadFromFile (scene.go:45-57)."""
+        h = ctypes.c_void_p()
+        _check(lib().rt_scene_load_json(path.encode(), 0, ctypes.byref(h)))
+        return cls(handle=h)
+
+    @classmethod
+    def from_json_text(cls, text: str) -> "Scene":
+        h = ctypes.c_void_p()
+        b = text.encode()
+        _check(lib().rt_scene_parse_json(b, len(b), 0, ctypes.byref(h)))
+        return cls(handle=h)
+
+    @classmethod
+    def from_python(cls, camera: dict, objects: list, lights: list) -> "Scene":
+        """Build a scene from already-decoded values (loader defaults applied)."""
+        cam = Camera()
+        cam.position[:] = camera.get("position", (0, 0, 0))
+        cam.look_at[:] = camera.get("lookAt", (0, 0, 0))
+        cam.up[:] = camera.get("up", (0, 0, 0))
+        cam.fov = camera.get("fov", 0.0)
+        cam.aspect_ratio = camera.get("aspectRatio", 0.0)
+        objs = []
+        for o in objects:
+            ob = Object()
+            ob.type = RT_OBJ_SPHERE if o["type"] == "sphere" else RT_OBJ_CUBE
+            ob.position[:] = o.get("position", (0, 0, 0))
+            ob.size[:] = o.get("size", (0, 0, 0))
+            ob.radius = o.get("radius", 0.0)
+            m = o["material"]
+            ob.material.kind = MATERIAL_KINDS[m["type"]]
+            ob.material.color[:] = m.get("color", (0, 0, 0))
+            ob.material.roughness = m.get("roughness", 0.0)
+            ob.material.metallic = m.get("metallic", 1.0 if m["type"] == "metal" else 0.0)
+            ob.material.specular = m.get("specular", 1.0)
+            ob.material.refraction_index = m.get("refractionIndex", 1.5)
+            objs.append(ob)
+        ls = []
+        for l in lights:
+            li = Light()
+            li.position[:] = l["position"]
+            li.color[:] = l.get("color", (0, 0, 0))
+            li.intensity = l.get("intensity", 0.0)
+            ls.append(li)
+        return cls(objects=objs, lights=ls, camera=cam)
+
+    @property
+    def view(self) -> SceneView:
+        return self._view
+
+    @property
+    def num_objects(self) -> int:
+        return self._view.num_objects
+
+    @property
+    def warnings(self) -> int:
+        return lib().rt_scene_warnings(self._handle) if self._handle is not None else 0
+
+    def print_hittables(self):
+        if self._handle is not None:
+            lib().rt_scene_print_hittables(self._handle)
+
+    def __del__(self):
+        h = getattr(self, "_handle", None)
+        if h is not None and _lib is not None:
+            _lib.rt_scene_free(h)
+            self._handle = None
+
+
+# --------------------------------------------------------------- renderer
+class ParallelRenderer:
+    """renderer.ParallelRenderer (renderer.go:20-29) backed by the GPU kernel."""
+
+    FEATURES = [
+        "Improved metallic reflections with Fresnel effect",
+        "Shiny materials with configurable roughness and specular",
+        "Enhanced light source reflections",
+        "Better specular highlights for metallic surfaces",
+    ]
+
+    def __init__(self, num_workers: int = 1):
+        self.settings = default_settings()  # NewParallelRenderer defaults, renderer.go:54-65
+        self.settings.num_workers = num_workers
+        self.benchmark_data: dict = {}
+        self.last_linear = None
+        self.last_stats = None
+
+    # settings.go:3-25
+    def set_samples(self, samples: int):
+        self.settings.samples = samples
+
+    def set_max_depth(self, max_depth: int):
+        self.settings.max_depth = max_depth
+
+    def set_anti_aliasing(self, on: bool):
+        self.settings.anti_aliasing = int(on)
+
+    def set_recursive_reflections(self, on: bool):
+        self.settings.recursive_reflections = int(on)
+
+    def set_soft_shadows(self, on: bool):
+        self.settings.soft_shadows = int(on)
+
+    def set_depth_of_field(self, on: bool):
+        self.settings.depth_of_field = int(on)
+
+    def set_seed(self, seed: int):
+        self.settings.seed = seed
+
+    def get_stats(self) -> dict:  # settings.go:27-36
+        s = self.settings
+        return {
+            "workers": s.num_workers,
+            "samples": s.samples,
+            "maxDepth": s.max_depth,
+            "antiAliasing": bool(s.anti_aliasing),
+            "recursiveReflections": bool(s.recursive_reflections),
+            "softShadows": bool(s.soft_shadows),
+            "depthOfField": bool(s.depth_of_field),
+        }
+
+    def render(self, scene: Scene, width: int, height: int) -> np.ndarray:
+        """Render (renderer.go:67-126): returns an (H, W, 4) uint8 RGBA image.
+
+        The mean linear radiance (before tone mapping) is kept in
+        ``self.last_linear`` as an (H, W, 3) float32 array.
+        """
+        lin = np.zeros((height, width, 3), np.float32)
+        rgba = np.zeros((height, width, 4), np.uint8)
+        st = Stats()
+        _check(
+            lib().rt_render(
+                ctypes.byref(scene.view),
+                width,
+                height,
+                ctypes.byref(self.settings),
+                lin.ctypes.data,
+                rgba.ctypes.data,
+                ctypes.byref(st),
+            )
+        )
+        self.last_linear = lin
+        self.last_stats = st
+        self.benchmark_data = {
+            "scene_name": "demo_scene",
+            "resolution": f"{width}x{height}",
+            "render_time_seconds": st.render_seconds,
+            "samples": self.settings.samples,
+            "max_depth": self.settings.max_depth,
+            "num_workers": self.settings.num_workers,
+            "objects": st.objects,
+            "lights": st.lights,
+            "timestamp": datetime.now(timezone.utc).isoformat(),
+            "features": list(self.FEATURES),
+            "kernel_time_seconds": st.kernel_seconds,
+            "pixels_per_second": st.pixels_per_second,
+            "rays_per_second": st.rays_per_second,
+        }
+        return rgba
+
+    def save_image(self, img: np.ndarray, filename: str):
+        """SaveImage (renderer.go:438-451); '.ppm' writes a P3 PPM."""
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        h, w = img.shape[:2]
+        f = lib().rt_write_ppm if filename.endswith(".ppm") else lib().rt_write_png
+        _check(f(filename.encode(), img.ctypes.data, w, h))
+
+    def save_benchmark_data(self, path: str):
+        """SaveBenchmarkData (renderer.go:473-485)."""
+        d = os.path.dirname(path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(self.benchmark_data, f, indent=2)
+
+
+# --------------------------------------------------------------- device API
+class Context:
+    """A scene resident on one device (rt_context_*)."""
+
+    def __init__(self, device: int = 0):
+        self._h = ctypes.c_void_p()
+        _check(lib().rt_context_create(device, ctypes.byref(self._h)))
+
+    def set_scene(self, scene: Scene, force_bvh: int = 0):
+        self._scene = scene  # keep alive
+        _check(lib().rt_context_set_scene(self._h, ctypes.byref(scene.view), force_bvh))
+
+    def render_async(self, width, height, settings: Settings, d_linear: int, d_rgba: int, stream: int = 0,
+                     rank: int = 0, world: int = 1, layout: int = RT_LAYOUT_IMAGE):
+        _check(
+            lib().rt_context_render_async(
+                self._h, width, height, ctypes.byref(settings), rank, world, layout,
+                ctypes.c_void_p(d_linear), ctypes.c_void_p(d_rgba), ctypes.c_void_p(stream), None,
+            )
+        )
+
+    def count(self, width, height, settings: Settings, d_linear: int, d_rgba: int, stream: int = 0,
+              rank: int = 0, world: int = 1, layout: int = RT_LAYOUT_IMAGE) -> dict:
+        c = Counts()
+        _check(
+            lib().rt_context_render_async(
+                self._h, width, height, ctypes.byref(settings), rank, world, layout,
+                ctypes.c_void_p(d_linear), ctypes.c_void_p(d_rgba), ctypes.c_void_p(stream), ctypes.byref(c),
+            )
+        )
+        return c.as_dict()
+
+    def last_kernel_seconds(self) -> float:
+        s = ctypes.c_double()
+        _check(lib().rt_context_last_kernel_seconds(self._h, ctypes.byref(s)))
+        return s.value
+
+    def close(self):
+        if self._h:
+            lib().rt_context_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def num_tiles(width: int, height: int) -> int:
+    return lib().rt_num_tiles(width, height)
+
+
+def tiles_for_rank(width: int, height: int, rank: int, world: int) -> int:
+    return lib().rt_tiles_for_rank(width, height, rank, world)
+
+
+def unpack_tiles_async(width, height, world, max_local, d_pl, d_pr, d_ol, d_or, stream=0):
+    _check(
+        lib().rt_unpack_tiles_async(
+            width, height, world, max_local, ctypes.c_void_p(d_pl), ctypes.c_void_p(d_pr),
+            ctypes.c_void_p(d_ol), ctypes.c_void_p(d_or), ctypes.c_void_p(stream),
+        )
+    )

@@ -1,0 +1,238 @@
+/*
+ * rt_api.h — C ABI of the MI355X-native renderer core (librtgo.so).
+ *
+ * Drop-in boundary for the per-pixel ray-trace hot path of
+ * JoshElkind/concurrent-raytracer-go.  The reference has no FFI; its seam is
+ * the Go method set of *renderer.ParallelRenderer, called only from
+ * cmd/raytracer/main.go:40-69.  Each entry point below names the reference
+ * symbol (file:line, relative to the reference root) it replaces.
+ *
+ * Conventions:
+ *   - every function returns 0 (RT_OK) on success and a negative RT_E* code
+ *     on failure; rt_last_error() returns a thread-local message.  Nothing
+ *     here aborts the process (the Go loader panics on a bad material;
+ *     internal/scene/scene.go:105,109-145).
+ *   - buffers are caller-owned; no pointer is retained after a call returns,
+ *     except the scene a context uploads (copied to device memory).
+ *   - rt_render is synchronous and blocking like Go's Render
+ *     (internal/renderer/renderer.go:67-126).  A context is not safe for
+ *     concurrent use from several threads (neither is the Go renderer: it
+ *     mutates benchmarkData, renderer.go:103-112).
+ *   - all arithmetic on the path is IEEE binary64, like the Go float64 code.
+ */
+#ifndef RT_API_H
+#define RT_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* status codes */
+#define RT_OK 0
+#define RT_E_INVALID (-1)   /* bad argument */
+#define RT_E_IO (-2)        /* file read/write failed */
+#define RT_E_PARSE (-3)     /* scene JSON malformed */
+#define RT_E_DEVICE (-4)    /* HIP runtime / device error */
+#define RT_E_NOMEM (-5)
+
+/* Object kinds — internal/scene/scene.go:69-82 ("sphere", "cube"; any other
+ * type string is skipped by the loader with "Unknown object type"). */
+#define RT_OBJ_SPHERE 0
+#define RT_OBJ_CUBE 1
+
+/* Material kinds reachable from JSON — internal/scene/scene.go:104-148. */
+#define RT_MAT_LAMBERTIAN 0    /* material.go:18-55 (also the default case) */
+#define RT_MAT_METAL 1         /* material.go:57-149 */
+#define RT_MAT_SHINY 2         /* material.go:151-225 */
+#define RT_MAT_PERFECTMIRROR 3 /* advanced_materials.go:111-171 */
+#define RT_MAT_GLASS 4         /* advanced_materials.go:9-66 */
+#define RT_MAT_DIELECTRIC 5    /* material.go:227-286 */
+#define RT_MAT_DIFFUSELIGHT 6  /* material.go:288-318 */
+
+/* Material parameters exactly as the JSON loader hands them to the Go
+ * constructors (scene.go:104-148), i.e. with the loader's defaults already
+ * applied (metal: roughness 0, metallic 1, specular 1; shiny: roughness 0,
+ * metallic 0, specular 1; perfectmirror: roughness 0; glass/dielectric:
+ * refractionIndex 1.5).  The constructors' clamps (NewMetal's
+ * Min(x,1.0), material.go:65-73 etc.) are applied by the renderer, not here. */
+typedef struct {
+  int32_t kind;          /* RT_MAT_* */
+  int32_t _pad;
+  double color[3];       /* "color" (emit colour for diffuselight) */
+  double roughness;
+  double metallic;
+  double specular;
+  double refraction_index;
+} rt_material;
+
+/* One scene object — internal/scene/scene.go:26-32 (type Object). */
+typedef struct {
+  int32_t type;          /* RT_OBJ_* */
+  int32_t _pad;
+  double position[3];    /* sphere centre / cube centre */
+  double size[3];        /* cube edge lengths (unused for spheres) */
+  double radius;         /* sphere radius (unused for cubes) */
+  rt_material material;
+} rt_object;
+
+/* Point light — scene.go:34-39.  "type" is ignored by the renderer
+ * (renderer.go:248-294 treats every light as a point light). */
+typedef struct {
+  double position[3];
+  double color[3];
+  double intensity;
+} rt_light;
+
+/* Camera — scene.go:18-24.  Only position and aspect_ratio are used by the
+ * reference's getRay (renderer.go:377-390); the others are carried for
+ * fidelity. */
+typedef struct {
+  double position[3];
+  double look_at[3];
+  double up[3];
+  double fov;
+  double aspect_ratio;
+} rt_camera;
+
+/* Scene view — scene.go:12-16 (type Scene). */
+typedef struct {
+  rt_camera camera;
+  const rt_object* objects;
+  int32_t num_objects;
+  int32_t _pad0;
+  const rt_light* lights;
+  int32_t num_lights;
+  int32_t _pad1;
+} rt_scene;
+
+/* Renderer settings — the ParallelRenderer fields (renderer.go:20-29) and
+ * their setters (settings.go:3-25).  Defaults: rt_settings_default(). */
+typedef struct {
+  int32_t samples;               /* SetSamples; default 100 */
+  int32_t max_depth;             /* SetMaxDepth; default 50 */
+  int32_t anti_aliasing;         /* SetAntiAliasing; inert in the reference (jitter is unconditional, renderer.go:155-156) */
+  int32_t recursive_reflections; /* SetRecursiveReflections; default 1 */
+  int32_t soft_shadows;          /* SetSoftShadows; default 1 */
+  int32_t depth_of_field;        /* SetDepthOfField; inert (advanced.go unused) */
+  int32_t num_workers;           /* NewParallelRenderer(n); recorded in benchmark data only */
+  int32_t _pad;
+  uint64_t seed;                 /* counter-based RNG seed (include/rt_rng.h); default 1 */
+} rt_settings;
+
+typedef struct {
+  double render_seconds;    /* wall time of rt_render, upload + kernels + download (Go Render semantics) */
+  double kernel_seconds;    /* device time of the render kernels (HIP events) */
+  double rays_per_second;   /* W*H*spp / render_seconds — the published metric (README.md:61) */
+  double pixels_per_second; /* W*H / render_seconds (README.md:60) */
+  int32_t objects;          /* len(hittables): a cube counts as one (renderer.go:109) */
+  int32_t lights;
+} rt_stats;
+
+/* Per-launch operation counts (for the roofline's algorithmic FLOPs). */
+typedef struct {
+  uint64_t camera_rays;      /* primary samples traced */
+  uint64_t bounce_rays;      /* closest-hit queries (primary + scattered) */
+  uint64_t shadow_rays;      /* any-hit queries (hard + soft) */
+  uint64_t sphere_tests;     /* ray/sphere intersection tests executed */
+  uint64_t triangle_tests;   /* ray/triangle tests executed */
+  uint64_t box_tests;        /* BVH node slab tests executed */
+  uint64_t shade_events;     /* surface hits shaded (direct lighting + scatter) */
+  uint64_t light_evals;      /* per-light direct-lighting evaluations */
+  uint64_t rng_draws;        /* uniform draws */
+} rt_counts;
+
+void rt_settings_default(rt_settings* s);
+int32_t rt_abi_version(void);
+const char* rt_last_error(void);
+
+/* ---------------------------------------------------------------- scene */
+
+typedef struct rt_scene_buf rt_scene_buf; /* owns a parsed scene */
+
+/* scene.LoadFromFile — internal/scene/scene.go:45-57 (+ Vec3.UnmarshalJSON,
+ * internal/math/vector.go:176-193, and the material defaults of
+ * createMaterial, scene.go:104-148).  Unknown object types are dropped like
+ * GetHittables does (scene.go:80-82).  A material without "color" (Go
+ * panics, scene.go:113) is loaded with colour (0,0,0) and counted in
+ * rt_scene_warnings(). `verbose` != 0 prints the reference's stdout lines
+ * (scene.go:62-88). */
+int rt_scene_load_json(const char* path, int32_t verbose, rt_scene_buf** out);
+int rt_scene_parse_json(const char* text, size_t len, int32_t verbose, rt_scene_buf** out);
+const rt_scene* rt_scene_view(const rt_scene_buf* buf);
+int32_t rt_scene_warnings(const rt_scene_buf* buf);
+void rt_scene_free(rt_scene_buf* buf);
+/* Print the lines (*Scene).GetHittables prints (scene.go:62-88), in Go's
+ * fmt formatting, for a CLI that mirrors cmd/raytracer. */
+int rt_scene_print_hittables(const rt_scene_buf* buf);
+
+/* ------------------------------------------------------- blocking render */
+
+/* (*ParallelRenderer).Render — internal/renderer/renderer.go:67-126.
+ * out_linear_rgb: W*H*3 floats (may be NULL), pixel (x,y) at (y*W+x)*3, i.e.
+ *   the Go image row y (row 0 is the BOTTOM of the viewport: the image is
+ *   vertically flipped vs world up, exactly like the reference).  Value =
+ *   mean radiance over samples before tone mapping.
+ * out_rgba: W*H*4 bytes (may be NULL) — toneMap + ToRGB, alpha 255
+ *   (renderer.go:92-97,348-367; vector.go:106-109).
+ * stats may be NULL.  Uses device settings->... on device 0. */
+int rt_render(const rt_scene* scene, int32_t width, int32_t height, const rt_settings* settings,
+              float* out_linear_rgb, uint8_t* out_rgba, rt_stats* stats);
+
+/* ------------------------------------------- resident context (bench/MGPU) */
+
+typedef struct rt_context rt_context;
+
+int rt_context_create(int32_t device, rt_context** out);
+void rt_context_destroy(rt_context* ctx);
+
+/* Flatten (GetHittables, scene.go:59-90; createCube, scene.go:150-190) and
+ * upload the scene to device memory.  Builds the BVH when the scene is
+ * large (or when force_bvh > 0; force_bvh < 0 forbids it). */
+int rt_context_set_scene(rt_context* ctx, const rt_scene* scene, int32_t force_bvh);
+
+#define RT_LAYOUT_IMAGE 0        /* write pixels of this rank's tiles into a W*H image */
+#define RT_LAYOUT_PACKED_TILES 1 /* write this rank's tiles packed: [local_tile][32*32] */
+
+/* Number of 32x32 tiles of a W*H image (createRenderTasks, renderer.go:398-436). */
+int32_t rt_num_tiles(int32_t width, int32_t height);
+/* Tiles owned by `rank` of `world` under strided assignment t -> t % world. */
+int32_t rt_tiles_for_rank(int32_t width, int32_t height, int32_t rank, int32_t world);
+
+/* Enqueue a render of the tiles t with t % world == rank on `hip_stream`
+ * (a hipStream_t, NULL = default stream).  d_linear (float3 per pixel) and
+ * d_rgba (4 B per pixel, may be NULL) are DEVICE pointers sized for the
+ * layout: W*H pixels (IMAGE) or rt_tiles_for_rank()*1024 pixels (PACKED).
+ * Asynchronous: returns after the launches are queued.  If counts != NULL a
+ * counting variant runs instead and the counts are returned (synchronous). */
+int rt_context_render_async(rt_context* ctx, int32_t width, int32_t height, const rt_settings* settings,
+                            int32_t rank, int32_t world, int32_t layout, float* d_linear, uint8_t* d_rgba,
+                            void* hip_stream, rt_counts* counts);
+
+/* Scatter packed tiles gathered from all ranks, laid out
+ * [world][max_local_tiles][1024] (float3 and rgba), into W*H images. */
+int rt_unpack_tiles_async(int32_t width, int32_t height, int32_t world, int32_t max_local_tiles,
+                          const float* d_packed_linear, const uint8_t* d_packed_rgba, float* d_linear,
+                          uint8_t* d_rgba, void* hip_stream);
+
+/* Device time (seconds) of the last render launch enqueued on this context
+ * (HIP events recorded around it on its stream); waits for it. */
+int rt_context_last_kernel_seconds(rt_context* ctx, double* seconds);
+
+/* ------------------------------------------------------------ output */
+
+/* toneMap + ToRGB on host (renderer.go:348-367; vector.go:106-109). */
+void rt_tonemap_rgba(const float* linear_rgb, int32_t npix, uint8_t* out_rgba);
+/* SaveImage — renderer.go:438-451 (PNG, opaque 8-bit RGB like Go's encoder). */
+int rt_write_png(const char* path, const uint8_t* rgba, int32_t width, int32_t height);
+/* SavePPMFromVec3-style P3 writer (internal/output/ppm.go:34-59), from RGBA8. */
+int rt_write_ppm(const char* path, const uint8_t* rgba, int32_t width, int32_t height);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_API_H */

@@ -1,0 +1,89 @@
+/*
+ * rt_rng.h — the counter-keyed random stream shared (as a SPEC) by the CPU
+ * oracle (oracle/oracle.c) and the gfx950 kernel.
+ *
+ * Why a new generator: the reference draws from Go's global math/rand
+ * (internal/math/random.go:8-14), shared across goroutines and unseedable
+ * under go 1.24 (rand.Seed is a no-op), so its draw order depends on the
+ * goroutine schedule.  Bit-level parity with a Go run is
+ * impossible; parity is defined against the oracle, which consumes exactly
+ * the same draws as the kernel because both key the stream by
+ * (seed, pixel, sample) — never by tile, rank or thread.
+ *
+ * Spec:
+ *   key0   = mix64(seed)                               (once per render)
+ *   k      = mix64(key0 ^ (pixel << 32 | sample))      pixel = y*W + x
+ *   s[i]   = mix64(k + (i+1) * 0x9E3779B97F4A7C15), i = 0..3
+ *   next() = xoshiro256+ (Blackman & Vigna 2018): r = s0 + s3, then the
+ *            standard state update with rotl(s3, 45)
+ *   draw() = bits_as_double(0x3FF0000000000000 | (next() >> 12)) - 1.0
+ *            (uniform on [0,1) in steps of 2^-52; the Go equivalent is
+ *            rand.Float64(), random.go:12-14)
+ * mix64 is the SplitMix64 finaliser.
+ *
+ * The draw ORDER is the reference's call order:
+ * per sample u, v (renderer.go:155-156); per bounce, for every light whose
+ * hard shadow ray is unoccluded, 16 RandomVec3InUnitSphere
+ * (renderer.go:315-316, vector.go:132-139: 3 draws per rejection try);
+ * then the material's scatter draws.
+ */
+#ifndef RT_RNG_H
+#define RT_RNG_H
+
+#include <stdint.h>
+#include <string.h>
+
+#if defined(__HIP__) || defined(__HIPCC__)
+#define RT_RNG_FN static inline __host__ __device__
+#else
+#define RT_RNG_FN static inline
+#endif
+
+#define RT_RNG_GAMMA 0x9E3779B97F4A7C15ULL
+
+typedef struct {
+  uint64_t s0, s1, s2, s3;
+} rt_rng;
+
+RT_RNG_FN uint64_t rt_mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+RT_RNG_FN uint64_t rt_rng_seed_key(uint64_t seed) { return rt_mix64(seed); }
+
+RT_RNG_FN void rt_rng_init(rt_rng* r, uint64_t seed_key, uint32_t pixel, uint32_t sample) {
+  uint64_t k = rt_mix64(seed_key ^ (((uint64_t)pixel << 32) | (uint64_t)sample));
+  r->s0 = rt_mix64(k + 1 * RT_RNG_GAMMA);
+  r->s1 = rt_mix64(k + 2 * RT_RNG_GAMMA);
+  r->s2 = rt_mix64(k + 3 * RT_RNG_GAMMA);
+  r->s3 = rt_mix64(k + 4 * RT_RNG_GAMMA);
+}
+
+RT_RNG_FN uint64_t rt_rng_next(rt_rng* r) {
+  uint64_t result = r->s0 + r->s3;
+  uint64_t t = r->s1 << 17;
+  r->s2 ^= r->s0;
+  r->s3 ^= r->s1;
+  r->s1 ^= r->s2;
+  r->s0 ^= r->s3;
+  r->s2 ^= t;
+  r->s3 = (r->s3 << 45) | (r->s3 >> 19);
+  return result;
+}
+
+RT_RNG_FN double rt_bits_to_unit(uint64_t x) {
+  uint64_t b = 0x3FF0000000000000ULL | (x >> 12);
+  double d;
+#if defined(__HIP_DEVICE_COMPILE__)
+  d = __builtin_bit_cast(double, b);
+#else
+  memcpy(&d, &b, sizeof d);
+#endif
+  return d - 1.0;
+}
+
+RT_RNG_FN double rt_rng_draw(rt_rng* r) { return rt_bits_to_unit(rt_rng_next(r)); }
+
+#endif /* RT_RNG_H */

@@ -1,0 +1,79 @@
+"""Scenes used by the parity tests (shared by CPU and GPU tests)."""
+import json
+import os
+
+SCENES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scenes")
+
+# Every JSON-reachable material (scene.go:104-148), spheres and a cube, a
+# light behind the camera side, facing the reference's fixed -Z camera.
+ALL_MATERIALS = {
+    "camera": {"position": [0, 0.5, 6], "lookAt": [0, 0, 0], "up": [0, 1, 0], "fov": 60, "aspectRatio": 1.5},
+    "objects": [
+        {"type": "sphere", "position": [0, -1001, 0], "radius": 1000,
+         "material": {"type": "lambertian", "color": [0.5, 0.5, 0.5]}},
+        {"type": "sphere", "position": [-3.2, 0, 0], "radius": 0.8,
+         "material": {"type": "metal", "color": [0.9, 0.6, 0.3], "roughness": 0.2, "metallic": 0.85,
+                      "specular": 0.7}},
+        {"type": "sphere", "position": [-1.4, 0, 0.5], "radius": 0.7,
+         "material": {"type": "glass", "color": [0.9, 0.95, 1.0], "refractionIndex": 1.5}},
+        {"type": "sphere", "position": [0.3, 0, 0], "radius": 0.8,
+         "material": {"type": "dielectric", "refractionIndex": 1.33}},
+        {"type": "sphere", "position": [2.0, 0, -0.5], "radius": 0.8,
+         "material": {"type": "shiny", "color": [0.2, 0.8, 0.3], "roughness": 0.1, "metallic": 0.6,
+                      "specular": 0.5}},
+        {"type": "sphere", "position": [3.6, 0.2, 0], "radius": 0.7,
+         "material": {"type": "perfectmirror", "color": [0.8, 0.8, 0.8], "roughness": 0.05}},
+        {"type": "sphere", "position": [0, 2.2, -2], "radius": 0.6,
+         "material": {"type": "diffuselight", "color": [4, 4, 3.5]}},
+        {"type": "cube", "position": [1.2, -0.6, 1.6], "size": [0.8, 0.8, 0.8],
+         "material": {"type": "metal", "color": [0.7, 0.7, 0.9], "roughness": 0.0, "metallic": 1.0}},
+        {"type": "cube", "position": [-2.2, -0.7, 2.0], "size": [0.6, 0.6, 0.6],
+         "material": {"type": "lambertian", "color": [0.8, 0.1, 0.1]}},
+        {"type": "sphere", "position": [-0.5, -0.75, 2.2], "radius": 0.25,
+         "material": {"type": "metal", "color": [0.95, 0.95, 0.95], "roughness": 0.6, "metallic": 0.55}},
+        {"type": "sphere", "position": [0.9, 1.0, 1.0], "radius": 0.3,
+         "material": {"type": "unknownkind", "color": [0.3, 0.3, 0.9]}},
+    ],
+    "lights": [
+        {"type": "point", "position": [4, 6, 6], "color": [1, 1, 1], "intensity": 40.0},
+        {"type": "point", "position": [-5, 3, 4], "color": [0.8, 0.8, 1], "intensity": 20.0},
+        {"type": "point", "position": [0, 0.5, 0.3], "color": [1, 0.5, 0.5], "intensity": 0.5},
+    ],
+}
+
+
+def scene_path(name):
+    return os.path.join(SCENES, name)
+
+
+def all_materials_json():
+    return json.dumps(ALL_MATERIALS)
+
+
+# (id, loader, width, height, settings overrides)
+PARITY_CASES = [
+    ("spheres_facing", ("file", "sphere_reflections_light_facing.json"), 96, 72, {"samples": 8}),
+    ("spheres_as_committed", ("file", "sphere_reflections_light.json"), 64, 48, {"samples": 4}),
+    ("silver_facing", ("file", "final_silver_prism_purple_cube_facing.json"), 96, 72, {"samples": 6}),
+    ("all_materials", ("json", None), 96, 64, {"samples": 8}),
+    ("all_materials_hard_shadows", ("json", None), 64, 48, {"samples": 4, "soft_shadows": 0}),
+    ("all_materials_no_recursion", ("json", None), 64, 48, {"samples": 4, "recursive_reflections": 0}),
+    ("all_materials_depth3", ("json", None), 64, 48, {"samples": 4, "max_depth": 3}),
+    ("all_materials_odd_size_spp", ("json", None), 37, 29, {"samples": 3}),
+    ("all_materials_depth0", ("json", None), 20, 10, {"samples": 2, "max_depth": 0}),
+]
+
+
+def load_case(rtgo, loader):
+    kind, name = loader
+    if kind == "file":
+        return rtgo.Scene.load_from_file(scene_path(name))
+    return rtgo.Scene.from_json_text(all_materials_json())
+
+
+def make_settings(rtgo, overrides, seed=1):
+    st = rtgo.default_settings()
+    st.seed = seed
+    for k, v in overrides.items():
+        setattr(st, k, v)
+    return st
