@@ -184,6 +184,25 @@ void build_sphere_bvh(FlatScene* fs) {
     stack.push_back({left + 1, mid, t.first + t.count - mid});
     stack.push_back({left, t.first, mid - t.first});
   }
+  // depth check: traversal keeps at most depth-1 pending right children on
+  // its per-lane LDS stack (rt_kernel.hip kStack = 40)
+  {
+    std::vector<std::pair<int, int>> st = {{0, 1}};
+    int maxd = 0;
+    while (!st.empty()) {
+      auto [ni, dep] = st.back();
+      st.pop_back();
+      maxd = std::max(maxd, dep);
+      if (nodes[ni].count == 0) {
+        st.push_back({nodes[ni].left_or_first, dep + 1});
+        st.push_back({nodes[ni].left_or_first + 1, dep + 1});
+      }
+    }
+    if (maxd > 38) {
+      fs->bvh.clear();  // too deep for the stack: keep the linear scan
+      return;
+    }
+  }
   std::vector<DSphere> reordered(n);
   for (int i = 0; i < n; ++i) reordered[i] = fs->spheres[idx[i]];
   fs->spheres.swap(reordered);

@@ -7,6 +7,7 @@
 // tables) must equal the values the reference computes per test.
 #include <hip/hip_runtime_api.h>
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <chrono>
@@ -96,8 +97,9 @@ static DMat make_mat(const rt_material& m) {
       d.ior = m.refraction_index;
       put(d.albedo, arr(m.color));
       break;
-    case RT_MAT_DIELECTRIC:
+    case RT_MAT_DIELECTRIC:  // attenuation and GetAlbedo are (1,1,1), material.go:236,266-268
       d.ior = m.refraction_index;
+      put(d.color, mk(1.0, 1.0, 1.0));
       put(d.albedo, mk(1.0, 1.0, 1.0));
       break;
     case RT_MAT_DIFFUSELIGHT:
@@ -158,6 +160,16 @@ static void push_tri(FlatScene* fs, v3 v0, v3 v1, v3 v2, int mat, int obj) {
   put(t.e1, e1);
   put(t.e2, e2);
   put(t.n, normalize(cross(e1, e2)));  // NewTriangle, triangle.go:13-34
+  // bounding sphere for the shadow-cone culling (rt_kernel.hip); any
+  // rounding here is covered by the kernel's inflation margins
+  const v3 bc = divs(add(add(v0, v1), v2), 3.0);
+  double br = 0;
+  for (v3 v : {v0, v1, v2}) {
+    v3 dv = sub(v, bc);
+    br = fmax(br, sqrt(dv.x * dv.x + dv.y * dv.y + dv.z * dv.z));
+  }
+  put(t.bc, bc);
+  t.br = br;
   t.mat = mat;
   t.obj = obj;
   fs->tris.push_back(t);
@@ -174,6 +186,7 @@ void flatten_scene(const rt_scene& s, FlatScene* fs) {
       memset(&sp, 0, sizeof sp);
       put(sp.c, arr(o.position));
       sp.r = o.radius;
+      sp.r2 = o.radius * o.radius;
       sp.mat = mat;
       sp.obj = i;
       fs->spheres.push_back(sp);
@@ -202,6 +215,19 @@ void flatten_scene(const rt_scene& s, FlatScene* fs) {
   put(fs->cam_pos, arr(s.camera.position));
   fs->aspect = s.camera.aspect_ratio;
   fs->objects = s.num_objects;
+}
+
+// Sample slices per pixel (S): a workgroup's 256 lanes are P = 256/S pixels
+// x S slices; lane (p, q) traces samples q, q+S, ... of pixel p, so a wave
+// holds the samples of one or two pixels (coherent rays) and even a frame
+// whose geometry covers a few tiles fills the chip.  S divides spp when a
+// divisor in [32, 64] exists, so every lane traces the same sample count.
+static int choose_slices(int spp) {
+  if (spp <= 1) return 1;
+  if (spp <= 64) return spp;
+  for (int d = 64; d >= 32; --d)
+    if (spp % d == 0) return d;
+  return 64;
 }
 
 static int validate_scene(const rt_scene* s) {
@@ -265,6 +291,17 @@ struct rt_context {
   unsigned long long* d_counts = nullptr;
   hipStream_t last_stream = nullptr;
   bool have_timing = false;
+  unsigned long long* dbg = nullptr;
+  // tile dispatch order (schedule.cpp), cached per (scene, W, H, rank, world)
+  uint64_t scene_gen = 0;
+  int64_t order_key[5] = {-1, -1, -1, -1, -1};
+  std::vector<int32_t> order_host;
+  int32_t* d_order = nullptr;
+  size_t d_order_cap = 0;
+  std::vector<unsigned long long> masks_host;  // per local tile primary-ray masks
+  unsigned long long* d_masks = nullptr;
+  size_t d_masks_cap = 0;
+  int32_t stage_bytes = 0;  // scene prefix staged into LDS per workgroup (0 = none)
 };
 
 extern "C" {
@@ -332,6 +369,8 @@ void rt_context_destroy(rt_context* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->d_scene) (void)hipFree(c->d_scene);
   if (c->d_counts) (void)hipFree(c->d_counts);
+  if (c->d_order) (void)hipFree(c->d_order);
+  if (c->d_masks) (void)hipFree(c->d_masks);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -386,7 +425,10 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   c->d_mats = (const DMat*)(base + off_m);
   c->d_lights = (const DLight*)(base + off_l);
   c->d_bvh = (const DBVHNode*)(base + off_b);
+  // small linear-scan scenes are staged into LDS by every workgroup
+  c->stage_bytes = (f.bvh.empty() && off_b <= 48 * 1024) ? (int32_t)off_b : 0;
   c->have_scene = true;
+  c->scene_gen += 1;
   return RT_OK;
 }
 
@@ -419,6 +461,7 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   p.out_linear = d_linear;
   p.out_rgba = d_rgba;
   p.counts = counts ? c->d_counts : nullptr;
+  p.dbg = c->dbg;
   memcpy(p.cam, f.cam_pos, sizeof p.cam);
   p.aspect = f.aspect;
   p.seed_key = rt_rng_seed_key(st->seed);
@@ -438,15 +481,53 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   p.ntiles = rt_num_tiles(w, h);
   // sample slices per pixel: enough lanes per pixel to fill the chip even
   // when only a few tiles hold geometry
-  int S = 16;
-  while (S > 1 && S > st->samples) S >>= 1;
-  p.slices = S;
-  p.pix_per_wg = 256 / S;
-  p.blk_w = p.pix_per_wg >= 32 ? 32 : p.pix_per_wg;
-  p.blk_h = p.pix_per_wg / p.blk_w;
+  p.slices = choose_slices(st->samples);
+  if (const char* e = getenv("RTGO_SLICES")) {  // experiments only
+    const int v = atoi(e);
+    if (v >= 1 && v <= 256) p.slices = v;
+  }
+  p.pix_per_wg = 256 / p.slices;
+  p.blocks_per_tile = (1024 + p.pix_per_wg - 1) / p.pix_per_wg;
   p.layout = layout;
   const int local_tiles = rt_tiles_for_rank(w, h, rank, world);
-  p.num_wgs = local_tiles * (1024 / p.pix_per_wg);
+  p.num_wgs = local_tiles * p.blocks_per_tile;
+  {  // tile dispatch order (expensive tiles first), uploaded when it changes
+    const int64_t key[5] = {(int64_t)c->scene_gen, w, h, rank, world};
+    if (memcmp(key, c->order_key, sizeof key) != 0) {
+      tile_dispatch_order(f, w, h, rank, world, &c->order_host);
+      if (f.bvh.empty() && f.spheres.size() <= 64 && f.tris.size() <= 64) {
+        tile_primary_masks(f, w, h, rank, world, &c->masks_host);
+        if (c->masks_host.size() > c->d_masks_cap) {
+          if (c->d_masks) HIP_TRY(hipFree(c->d_masks));
+          c->d_masks = nullptr;
+          HIP_TRY(hipMalloc((void**)&c->d_masks, c->masks_host.size() * sizeof(unsigned long long)));
+          c->d_masks_cap = c->masks_host.size();
+        }
+        if (!c->masks_host.empty())
+          HIP_TRY(hipMemcpy(c->d_masks, c->masks_host.data(), c->masks_host.size() * sizeof(unsigned long long),
+                            hipMemcpyHostToDevice));
+      } else {
+        c->masks_host.clear();
+      }
+      if (c->order_host.size() > c->d_order_cap) {
+        if (c->d_order) HIP_TRY(hipFree(c->d_order));
+        c->d_order = nullptr;
+        HIP_TRY(hipMalloc((void**)&c->d_order, c->order_host.size() * sizeof(int32_t)));
+        c->d_order_cap = c->order_host.size();
+      }
+      if (!c->order_host.empty())
+        HIP_TRY(hipMemcpy(c->d_order, c->order_host.data(), c->order_host.size() * sizeof(int32_t),
+                          hipMemcpyHostToDevice));
+      memcpy(c->order_key, key, sizeof key);
+    }
+    p.tile_order = getenv("RTGO_NO_TILE_ORDER") ? nullptr : c->d_order;
+    p.tile_masks = (c->masks_host.empty() || getenv("RTGO_NO_FRUSTUM")) ? nullptr : c->d_masks;
+  }
+  {  // LDS staging of the scene prefix + BVH stack placement
+    p.stage_src = c->d_scene;
+    p.stage_bytes = getenv("RTGO_NO_STAGE") ? 0 : c->stage_bytes;
+    p.stack_off = (p.stage_bytes + 15) & ~15;
+  }
   // the caller's stream, as given (NULL = the legacy default stream)
   hipStream_t s = (hipStream_t)stream;
   if (counts) HIP_TRY(hipMemsetAsync(c->d_counts, 0, 16 * sizeof(unsigned long long), s));
@@ -473,6 +554,15 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
     counts->light_evals = h_c[7];
     counts->rng_draws = h_c[8];
   }
+  return RT_OK;
+}
+
+int rt_context_set_debug_buffer(rt_context* c, void* d_buf) {
+  if (!c) {
+    set_error("context is NULL");
+    return RT_E_INVALID;
+  }
+  c->dbg = (unsigned long long*)d_buf;
   return RT_OK;
 }
 

@@ -30,6 +30,15 @@ struct FlatScene {
 void flatten_scene(const rt_scene& s, FlatScene* out);
 // Binned-SAH BVH over out->spheres (reorders spheres). Requires no triangles.
 void build_sphere_bvh(FlatScene* fs);
+// Dispatch order of the local tiles of (rank, world): descending estimated
+// cost (primitives whose projected bounds overlap the tile), ties by index.
+void tile_dispatch_order(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
+                         std::vector<int32_t>* order);
+// Primary-ray candidate masks per local tile (2 x u64: spheres, triangles;
+// scenes with <= 64 of each): bit i set unless primitive i's bounding sphere
+// provably misses the cone of the tile's camera rays.
+void tile_primary_masks(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
+                        std::vector<unsigned long long>* masks);
 
 // ---------------------------------------------------------------- kernels
 struct KParams {
@@ -41,6 +50,12 @@ struct KParams {
   float* out_linear;
   uint8_t* out_rgba;
   unsigned long long* counts;  // 9 counters (rt_counts order) or null
+  unsigned long long* dbg;     // per-WG timing records (RT_WG_TIMING builds only) or null
+  const int32_t* tile_order;   // local tile indices in dispatch order, or null (identity)
+  const unsigned long long* tile_masks;  // per local tile: primary-ray candidate masks (spheres, tris) or null
+  const void* stage_src;       // start of the scene prefix staged into LDS (spheres..lights)
+  int32_t stage_bytes;         // bytes to stage (multiple of 16); 0 = read the scene from global memory
+  int32_t stack_off;           // byte offset of the BVH stacks in dynamic LDS
   double cam[3];
   double aspect;
   uint64_t seed_key;
@@ -50,9 +65,9 @@ struct KParams {
   int32_t recursive, soft;
   int32_t rank, world;
   int32_t tiles_x, ntiles;
-  int32_t slices;     // S: sample slices per pixel
-  int32_t pix_per_wg; // P = 256 / S
-  int32_t blk_w, blk_h;
+  int32_t slices;          // S: sample slices per pixel
+  int32_t pix_per_wg;      // P = 256 / S (consecutive row-major pixels of a tile)
+  int32_t blocks_per_tile; // ceil(1024 / P)
   int32_t layout;     // RT_LAYOUT_*
   int32_t num_wgs;
 };

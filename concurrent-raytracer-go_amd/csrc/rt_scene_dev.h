@@ -20,16 +20,18 @@ namespace rtgo {
 struct alignas(16) DSphere {  // 48 B
   double c[3];
   double r;
+  double r2;    // r*r, the value Sphere.Hit computes per test (sphere.go:26)
   int32_t mat;
   int32_t obj;  // hittable index (tie order)
-  int32_t pad[2];
 };
 
-struct alignas(16) DTri {  // 112 B
+struct alignas(16) DTri {  // 144 B
   double v0[3];
   double e1[3];  // v1 - v0
   double e2[3];  // v2 - v0
   double n[3];   // face normal = Normals[0..2]
+  double bc[3];  // bounding sphere (culling only): centroid ...
+  double br;     // ... and the largest vertex distance
   int32_t mat;
   int32_t obj;
   int32_t pad[2];

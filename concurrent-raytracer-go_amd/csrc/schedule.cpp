@@ -1,0 +1,112 @@
+// schedule.cpp — dispatch order of a rank's 32x32 tiles.
+//
+// The reference hands tiles to goroutines in row-major order through a
+// channel (createRenderTasks, internal/renderer/renderer.go:398-436); a
+// goroutine that draws a slow tile just keeps it while the others continue.
+// On the GPU a workgroup is dispatched once and runs to completion, so a
+// slow tile dispatched late (long multi-bounce paths between mirrors) runs
+// alone at the end of the launch.  Tiles are therefore dispatched in order
+// of an estimated cost: the number of primitives whose projected bounding
+// sphere overlaps the tile (cheap, host-side, camera model of getRay,
+// renderer.go:377-390).  This only permutes work: every tile is rendered by
+// exactly the same code, so the image does not depend on the order.
+#include <math.h>
+
+#include <algorithm>
+#include <numeric>
+#include <vector>
+
+#include "rt_internal.h"
+
+namespace rtgo {
+
+void tile_dispatch_order(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
+                         std::vector<int32_t>* order) {
+  const int tiles_x = (W + 31) / 32, tiles_y = (H + 31) / 32, ntiles = tiles_x * tiles_y;
+  std::vector<float> cost(ntiles, 0.0f);
+  const double vw = 2.0 * fs.aspect;
+  auto add_sphere = [&](const double* c, double r) {
+    const double R = fabs(r);
+    const double cx = c[0] - fs.cam_pos[0], cy = c[1] - fs.cam_pos[1], cz = c[2] - fs.cam_pos[2];
+    if (cz - R >= 0) return;  // entirely behind the camera: no camera ray reaches it
+    if (cz + R > -1e-9 || !(fabs(vw) > 0)) {  // straddles the camera plane: everywhere
+      for (auto& v : cost) v += 1.0f;
+      return;
+    }
+    // image bounds of the bounding box corners (perspective keeps convexity)
+    double u0 = INFINITY, u1 = -INFINITY, v0 = INFINITY, v1 = -INFINITY;
+    for (int k = 0; k < 8; ++k) {
+      const double qx = cx + ((k & 1) ? R : -R), qy = cy + ((k & 2) ? R : -R), qz = cz + ((k & 4) ? R : -R);
+      const double u = 0.5 + qx / (-qz * vw), v = 0.5 + qy / (-qz * 2.0);
+      u0 = fmin(u0, u);
+      u1 = fmax(u1, u);
+      v0 = fmin(v0, v);
+      v1 = fmax(v1, v);
+    }
+    const double px0 = u0 * W, px1 = u1 * W, py0 = v0 * H, py1 = v1 * H;
+    if (px1 < 0 || py1 < 0 || px0 >= W || py0 >= H) return;
+    const int tx0 = std::max(0, (int)floor(px0) / 32), tx1 = std::min(tiles_x - 1, (int)floor(fmin(px1, W - 1)) / 32);
+    const int ty0 = std::max(0, (int)floor(py0) / 32), ty1 = std::min(tiles_y - 1, (int)floor(fmin(py1, H - 1)) / 32);
+    for (int ty = ty0; ty <= ty1; ++ty)
+      for (int tx = tx0; tx <= tx1; ++tx) cost[ty * tiles_x + tx] += 1.0f;
+  };
+  for (const DSphere& s : fs.spheres) add_sphere(s.c, s.r);
+  for (const DTri& t : fs.tris) add_sphere(t.bc, t.br);
+
+  order->clear();
+  for (int t = rank, lt = 0; t < ntiles; t += world, ++lt) order->push_back(lt);
+  std::stable_sort(order->begin(), order->end(), [&](int32_t a, int32_t b) {
+    return cost[rank + a * world] > cost[rank + b * world];
+  });
+}
+
+// Does the cone (apex, unit axis, cos/sin of its half-angle) meet the sphere
+// (c, r)?  Same conservative test as the kernel's cone_meets_sphere: radius
+// inflated by ~1e-7, far above binary64 rounding of the ray directions.
+static bool cone_meets_sphere(const double c[3], double r, const double apex[3], const double axis[3], double cos_t,
+                              double sin_t) {
+  const double v[3] = {c[0] - apex[0], c[1] - apex[1], c[2] - apex[2]};
+  const double dc2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+  const double dc = sqrt(dc2);
+  const double ra = fabs(r) * (1.0 + 1e-7) + 1e-7 * dc + 1e-12;
+  if (dc <= ra) return true;
+  const double tl = sqrt(fmax(dc2 - ra * ra, 0.0));
+  const double vd = v[0] * axis[0] + v[1] * axis[1] + v[2] * axis[2];
+  return vd >= cos_t * (1.0 - 1e-9) * tl - (sin_t + 1e-9) * ra - 1e-7 * dc;
+}
+
+void tile_primary_masks(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
+                        std::vector<unsigned long long>* masks) {
+  masks->clear();
+  const int tiles_x = (W + 31) / 32, tiles_y = (H + 31) / 32, ntiles = tiles_x * tiles_y;
+  const int ns = (int)fs.spheres.size(), nt = (int)fs.tris.size();
+  const double vw = 2.0 * fs.aspect;
+  for (int t = rank; t < ntiles; t += world) {
+    const int tx = t % tiles_x, ty = t / tiles_x;
+    // camera rays of the tile: getRay direction (vw*(u-1/2), 2*(v-1/2), -1)
+    // with u in [x0/W, x1/W], v in [y0/H, y1/H] (renderer.go:155-156,377-390)
+    const int x0 = tx * 32, x1 = std::min(tx * 32 + 32, (int)W);
+    const int y0 = ty * 32, y1 = std::min(ty * 32 + 32, (int)H);
+    const double dx0 = vw * ((double)x0 / W - 0.5), dx1 = vw * ((double)x1 / W - 0.5);
+    const double dy0 = 2.0 * ((double)y0 / H - 0.5), dy1 = 2.0 * ((double)y1 / H - 0.5);
+    double axis[3] = {0.5 * (dx0 + dx1), 0.5 * (dy0 + dy1), -1.0};
+    const double al = sqrt(axis[0] * axis[0] + axis[1] * axis[1] + axis[2] * axis[2]);
+    for (double& a : axis) a /= al;
+    double cmin = 1.0;  // the widest corner: the angle is quasiconvex on the image plane
+    for (int k = 0; k < 4; ++k) {
+      const double cx = (k & 1) ? dx1 : dx0, cy = (k & 2) ? dy1 : dy0;
+      const double cl = sqrt(cx * cx + cy * cy + 1.0);
+      cmin = fmin(cmin, (axis[0] * cx + axis[1] * cy - axis[2]) / cl);
+    }
+    const double smax = sqrt(fmax(0.0, 1.0 - cmin * cmin));
+    unsigned long long ms = 0, mt = 0;
+    for (int i = 0; i < ns && i < 64; ++i)
+      if (cone_meets_sphere(fs.spheres[i].c, fs.spheres[i].r, fs.cam_pos, axis, cmin, smax)) ms |= 1ull << i;
+    for (int i = 0; i < nt && i < 64; ++i)
+      if (cone_meets_sphere(fs.tris[i].bc, fs.tris[i].br, fs.cam_pos, axis, cmin, smax)) mt |= 1ull << i;
+    masks->push_back(ms);
+    masks->push_back(mt);
+  }
+}
+
+}  // namespace rtgo

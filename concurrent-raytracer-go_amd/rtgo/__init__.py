@@ -22,7 +22,8 @@ from datetime import datetime, timezone
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "librtgo.so")
+# RTGO_LIB selects an alternative build of the same library (A/B variants)
+LIB_PATH = os.environ.get("RTGO_LIB") or os.path.join(os.path.dirname(_HERE), "build", "librtgo.so")
 
 RT_OK = 0
 RT_OBJ_SPHERE, RT_OBJ_CUBE = 0, 1
@@ -161,6 +162,7 @@ EXPORTED_SYMBOLS = [
     "rt_context_render_async",
     "rt_unpack_tiles_async",
     "rt_context_last_kernel_seconds",
+    "rt_context_set_debug_buffer",
     "rt_tonemap_rgba",
     "rt_write_png",
     "rt_write_ppm",
@@ -215,6 +217,7 @@ def lib():
         ),
         "rt_unpack_tiles_async": (ctypes.c_int, [i32, i32, i32, i32, vp, vp, vp, vp, vp]),
         "rt_context_last_kernel_seconds": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
+        "rt_context_set_debug_buffer": (ctypes.c_int, [vp, vp]),
         "rt_tonemap_rgba": (None, [vp, i32, vp]),
         "rt_write_png": (ctypes.c_int, [ctypes.c_char_p, vp, i32, i32]),
         "rt_write_ppm": (ctypes.c_int, [ctypes.c_char_p, vp, i32, i32]),
@@ -466,6 +469,9 @@ class Context:
             )
         )
         return c.as_dict()
+
+    def set_debug_buffer(self, d_buf: int):
+        _check(lib().rt_context_set_debug_buffer(self._h, ctypes.c_void_p(d_buf)))
 
     def last_kernel_seconds(self) -> float:
         s = ctypes.c_double()

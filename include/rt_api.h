@@ -219,6 +219,11 @@ int rt_unpack_tiles_async(int32_t width, int32_t height, int32_t world, int32_t 
                           const float* d_packed_linear, const uint8_t* d_packed_rgba, float* d_linear,
                           uint8_t* d_rgba, void* hip_stream);
 
+/* Debug hook: a device buffer of 16 u64 per workgroup that RT_WG_TIMING
+ * builds of the kernel fill with per-wave s_memrealtime stamps
+ * (start, loop end, end, XCC/HW id).  Product builds ignore it. */
+int rt_context_set_debug_buffer(rt_context* ctx, void* d_buf);
+
 /* Device time (seconds) of the last render launch enqueued on this context
  * (HIP events recorded around it on its stream); waits for it. */
 int rt_context_last_kernel_seconds(rt_context* ctx, double* seconds);

@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Per-workgroup timing of an RT_WG_TIMING build (dev tool).
+
+usage: RTGO_LIB=.../librtgo_timing.so wg_timing.py [scene.json] [W H SPP]
+Prints the kernel span, wave duration percentiles, how many waves are in
+flight over time (occupancy profile) and the slowest workgroups' tiles.
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "concurrent-raytracer-go_amd"))
+import torch  # noqa: E402
+
+import rtgo  # noqa: E402
+
+scene = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "scenes", "sphere_reflections_light_facing.json")
+W, H, SPP = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (800, 600, 100)
+ctx = rtgo.Context(0)
+ctx.set_scene(rtgo.Scene.load_from_file(scene))
+st = rtgo.default_settings()
+st.samples = SPP
+lin = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
+rgba = torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda")
+nwg_max = 2_000_000
+dbg = torch.zeros(nwg_max * 32, dtype=torch.int64, device="cuda")
+ctx.set_debug_buffer(dbg.data_ptr())
+RANK, WORLD = int(os.environ.get("WG_RANK", "0")), int(os.environ.get("WG_WORLD", "1"))
+if os.environ.get("WG_DEPTH"):
+    st.max_depth = int(os.environ["WG_DEPTH"])
+for _ in range(2):
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    ctx.render_async(W, H, st, lin.data_ptr(), rgba.data_ptr(), 0, RANK, WORLD, rtgo.RT_LAYOUT_PACKED_TILES)
+    e1.record()
+    torch.cuda.synchronize()
+print(f"kernel {e0.elapsed_time(e1):.3f} ms (rank {RANK}/{WORLD}, depth {st.max_depth})")
+d = dbg.cpu().numpy().reshape(-1, 4, 8)
+used = d[:, 0, 0] != 0
+d = d[used]
+nwg = d.shape[0]
+t0 = d[:, :, 0].min()
+start = (d[:, :, 0] - t0) / 100.0  # s_memrealtime: 100 MHz -> microseconds
+loop = (d[:, :, 1] - t0) / 100.0
+end = (d[:, :, 2] - t0) / 100.0
+span = end.max()
+dur = (end - start).ravel()
+print(f"{scene} {W}x{H}x{SPP}: {nwg} WGs, span {span:.1f} us")
+for q in (50, 90, 99, 99.9, 100):
+    print(f"  wave duration p{q}: {np.percentile(dur, q):.1f} us")
+epi = (end - loop).ravel()
+print(f"  epilogue (reduce+write) p50 {np.percentile(epi, 50):.2f} us  p99 {np.percentile(epi, 99):.2f} us")
+# waves in flight over time
+grid = np.linspace(0, span, 41)
+inflight = [int(((start <= t) & (end > t)).sum()) for t in grid]
+print("  waves in flight at 2.5% steps:", inflight)
+wgdur = end.max(axis=1) - start.min(axis=1)
+order = np.argsort(-wgdur)[:10]
+print("  slowest WGs (index, us, start us):", [(int(i), round(float(wgdur[i]), 1), round(float(start[i].min()), 1))
+                                              for i in order])
+for i in order[:5]:
+    for w in range(4):
+        h, l, sct, it = d[i, w, 4:8]
+        if it:
+            print(f"    WG {int(i)} wave {w}: iters {it}, cycles cand {h} light {l} soft {sct} "
+                  f"(per iter: {h / it:.0f} / {l / it:.0f} / {sct / it:.0f}); wave us {end[i, w] - start[i, w]:.0f}")
+busy = dur.sum()
+print(f"  mean waves in flight {busy / span:.1f}")
