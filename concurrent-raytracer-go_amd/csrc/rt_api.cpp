@@ -281,13 +281,14 @@ struct rt_context {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool have_scene = false;
   FlatScene flat;
-  void* d_scene = nullptr;  // one allocation: spheres | tris | mats | lights | bvh
+  void* d_scene = nullptr;  // one allocation: spheres | tris | mats | lights | jump table | bvh
   size_t d_scene_bytes = 0;
   const DSphere* d_spheres = nullptr;
   const DTri* d_tris = nullptr;
   const DMat* d_mats = nullptr;
   const DLight* d_lights = nullptr;
   const DBVHNode* d_bvh = nullptr;
+  const uint64_t* d_jump = nullptr;
   unsigned long long* d_counts = nullptr;
   hipStream_t last_stream = nullptr;
   bool have_timing = false;
@@ -401,7 +402,8 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   size_t off_t = off_s + al(f.spheres.size() * sizeof(DSphere));
   size_t off_m = off_t + al(f.tris.size() * sizeof(DTri));
   size_t off_l = off_m + al(f.mats.size() * sizeof(DMat));
-  size_t off_b = off_l + al(f.lights.size() * sizeof(DLight));
+  size_t off_j = off_l + al(f.lights.size() * sizeof(DLight));
+  size_t off_b = off_j + al(kJump * 2 * sizeof(uint64_t));
   size_t total = off_b + al(f.bvh.size() * sizeof(DBVHNode)) + 256;
   if (c->stream) HIP_TRY(hipStreamSynchronize(c->stream));
   if (c->d_scene && c->d_scene_bytes < total) {
@@ -418,6 +420,16 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   memcpy(host.data() + off_t, f.tris.data(), f.tris.size() * sizeof(DTri));
   memcpy(host.data() + off_m, f.mats.data(), f.mats.size() * sizeof(DMat));
   memcpy(host.data() + off_l, f.lights.data(), f.lights.size() * sizeof(DLight));
+  {
+    uint64_t* jt = reinterpret_cast<uint64_t*>(host.data() + off_j);
+    uint64_t a = 1, cc = 0;  // x_{i+j} = A_j x_i + C_j, built incrementally (rt_pcg_jump_coeffs)
+    for (int j = 0; j < kJump; ++j) {
+      jt[2 * j] = a;
+      jt[2 * j + 1] = cc;
+      cc = cc * RT_PCG_MULT + RT_PCG_INC;
+      a = a * RT_PCG_MULT;
+    }
+  }
   memcpy(host.data() + off_b, f.bvh.data(), f.bvh.size() * sizeof(DBVHNode));
   HIP_TRY(hipMemcpy(base, host.data(), total, hipMemcpyHostToDevice));
   c->d_spheres = (const DSphere*)(base + off_s);
@@ -425,6 +437,7 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   c->d_mats = (const DMat*)(base + off_m);
   c->d_lights = (const DLight*)(base + off_l);
   c->d_bvh = (const DBVHNode*)(base + off_b);
+  c->d_jump = (const uint64_t*)(base + off_j);
   // small linear-scan scenes are staged into LDS by every workgroup
   c->stage_bytes = (f.bvh.empty() && off_b <= 48 * 1024) ? (int32_t)off_b : 0;
   c->have_scene = true;
@@ -458,6 +471,7 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   p.mats = c->d_mats;
   p.lights = c->d_lights;
   p.bvh = c->d_bvh;
+  p.jump = c->d_jump;
   p.out_linear = d_linear;
   p.out_rgba = d_rgba;
   p.counts = counts ? c->d_counts : nullptr;

@@ -41,12 +41,17 @@ void tile_primary_masks(const FlatScene& fs, int32_t W, int32_t H, int32_t rank,
                         std::vector<unsigned long long>* masks);
 
 // ---------------------------------------------------------------- kernels
+// PCG jump-ahead entries: cooperative soft shadows evaluate up to 64
+// rejection tries (3 draws each) per round and then advance by 3*64 draws.
+constexpr int kJump = 3 * 64 + 1;
+
 struct KParams {
   const DSphere* spheres;
   const DTri* tris;
   const DMat* mats;
   const DLight* lights;
   const DBVHNode* bvh;
+  const uint64_t* jump;        // PCG jump table: (A_j, C_j) for j = 0..kJump-1 (rt_rng.h)
   float* out_linear;
   uint8_t* out_rgba;
   unsigned long long* counts;  // 9 counters (rt_counts order) or null

@@ -1,28 +1,34 @@
 // rt_kernel.hip — gfx950 (CDNA4) kernels of the renderer core.
 //
 // One launch renders every 32x32 tile (createRenderTasks,
-// internal/renderer/renderer.go:398-436) that this rank owns.  Mapping
+// internal/renderer/renderer.go:398-436) that this rank owns.  Design
 // (DESIGN.md §Kernels):
 //   workgroup (256 lanes = 4 wave64) = P consecutive row-major pixels of a
 //     tile x S sample slices (P = 256/S, S chosen by the host, ~spp/2);
-//   lane (p, q) traces samples q, q+S, q+2S, ... of pixel p with a
-//     persistent, iterative bounce loop (traceRay, renderer.go:165-227,
-//     unrolled): a lane whose path ends immediately regenerates its next
-//     camera sample, so paths of different length keep the lanes busy;
-//   a wave therefore holds the samples of one or two pixels — near-identical
-//     rays, so the branchy shading code stays coherent;
-//   the S slice sums of a pixel are reduced in LDS in slice order, divided by
-//     spp, tone-mapped (toneMap, renderer.go:348-367) and written once:
-//     float3 linear radiance + RGBA8.
-// Scene data for linear-scan scenes is read with wave-uniform addresses, so
-// it lives in SGPRs via the scalar cache (zero LDS bank cycles, no VGPRs).
-// Large sphere scenes use a BVH (bvh.cpp) traversed with a per-lane stack in
-// LDS.  All arithmetic is binary64 in the reference's order, compiled with
+//   lane (p, q) traces samples q, q+S, ... of pixel p with a persistent,
+//     iterative bounce loop (traceRay, renderer.go:165-227, unrolled); a lane
+//     whose path ends regenerates its next camera sample at once, and a lane
+//     with no samples left stays in the loop as a HELPER;
+//   per bounce and light, the 16 jittered shadow rays (calculateSmartShadow,
+//     renderer.go:299-331) are produced in a wave-converged section: when
+//     only a few lanes of the wave still need them (the long multi-bounce
+//     paths that otherwise run alone at the end of the launch), all 64 lanes
+//     evaluate one owner's rejection tries in parallel (PCG jump-ahead, see
+//     include/rt_rng.h) and trace the accepted rays in parallel — same draws,
+//     same rays, same result as the sequential loop;
+//   the S slice sums of a pixel are tree-reduced in LDS in a fixed order,
+//     divided by spp, tone-mapped (toneMap, renderer.go:348-367) and written
+//     once: float3 linear radiance + RGBA8.
+// Small linear-scan scenes are staged into LDS by every workgroup; large
+// sphere scenes use a BVH (bvh.cpp) with per-lane LDS stacks.  Primitives
+// that provably cannot be hit (tile frustum / shadow cone tests with wide
+// margins) are skipped; everything else gets the reference's exact test.
+// All path arithmetic is binary64 in the reference's order, compiled with
 // -ffp-contract=off, so every decision (hit / miss, root choice, rejection
 // test, reflect vs refract) is bit-identical to the oracle's.  Divisions that
 // only feed range tests are filtered by a reciprocal multiply with a 2^-40
-// relative error margin; the exact IEEE division runs whenever the filter
-// cannot decide, so the filtered decision always equals Go's.
+// relative margin; the exact IEEE division runs whenever the filter cannot
+// decide.
 #include <hip/hip_runtime.h>
 
 #include "../../include/rt_rng.h"
@@ -30,6 +36,9 @@
 
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 3  // measured best of 2/3/4 (4 spills the FP64 path state)
+#endif
+#ifndef RT_COOP_MAX
+#define RT_COOP_MAX 8  // cooperative soft shadows when at most this many lanes need them
 #endif
 
 namespace rtgo {
@@ -106,20 +115,58 @@ __device__ __forceinline__ double pow_gamma(double x, double y) {
   return exp(y * log(x));
 }
 
+// A binary64 constant materialised at its use (two s_mov_b32) rather than
+// hoisted into an SGPR pair for the whole kernel: the bounce loop is
+// SGPR-bound, and hoisted constants push loop state into VGPR-lane spills.
+constexpr uint64_t bits(double v) { return __builtin_bit_cast(uint64_t, v); }
+template <uint64_t B>
+__device__ __forceinline__ double kconst() {
+  uint32_t lo, hi;
+  asm volatile("s_mov_b32 %0, %2\n\ts_mov_b32 %1, %3"
+               : "=s"(lo), "=s"(hi)
+               : "i"((uint32_t)B), "i"((uint32_t)(B >> 32)));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+#define KC(v) kconst<bits(v)>()
+
+// ------------------------------------------------------------ lane helpers
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int lane) {
+  return ((uint64_t)rl32((uint32_t)(v >> 32), lane) << 32) | rl32((uint32_t)v, lane);
+}
+__device__ __forceinline__ double rld(double v, int lane) {
+  return __builtin_bit_cast(double, rl64(__builtin_bit_cast(uint64_t, v), lane));
+}
+__device__ __forceinline__ d3 rl3(d3 v, int lane) { return mk(rld(v.x, lane), rld(v.y, lane), rld(v.z, lane)); }
+// keep a (uniform) value in VGPRs: the SGPR file is the scarce one in the bounce loop
+__device__ __forceinline__ double inv(double v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ d3 inv3(d3 v) { return mk(inv(v.x), inv(v.y), inv(v.z)); }
+
 struct Counters {
   unsigned long long v[9];
 };
 enum { C_CAM = 0, C_BOUNCE, C_SHADOW, C_SPH, C_TRI, C_BOX, C_SHADE, C_LIGHT, C_RNG };
 
 template <bool kCount>
-__device__ __forceinline__ void cnt(Counters& c, int i) {
-  if constexpr (kCount) c.v[i] += 1;
+__device__ __forceinline__ void cnt(Counters& c, int i, unsigned long long n = 1) {
+  if constexpr (kCount) c.v[i] += n;
 }
 
 template <bool kCount>
 __device__ __forceinline__ double draw(rt_rng& r, Counters& c) {
   cnt<kCount>(c, C_RNG);
   return rt_rng_draw(&r);
+}
+
+// draw i of a stream whose state is x: x_i = A_i x + C_i (jump table in LDS)
+__device__ __forceinline__ double draw_at(uint64_t x, const uint64_t* jump, int i) {
+  const uint64_t xi = jump[2 * i] * x + jump[2 * i + 1];
+  return rt_bits_to_unit(rt_pcg_out(xi));
 }
 
 // RandomVec3InUnitSphere, vector.go:132-139.
@@ -201,9 +248,9 @@ __device__ __forceinline__ bool tri_test(const DTri& T, d3 o, d3 d, double tmin,
 }
 
 // ------------------------------------------------------------ BVH traversal
-constexpr int kStack = 40;  // per-lane LDS stack depth (binned SAH over 10k spheres: depth ~ 20-30)
+constexpr int kStack = 40;  // per-lane LDS stack depth (bvh.cpp refuses deeper trees)
 
-// Conservative slab test of a float box against [tmin, tnear_max].
+// Conservative slab test of a float box against [tmin, tmax].
 __device__ __forceinline__ bool box_hit(const DBVHNode& n, d3 o, d3 id, double tmin, double tmax) {
   double tx0 = ((double)n.lo[0] - o.x) * id.x, tx1 = ((double)n.hi[0] - o.x) * id.x;
   double ty0 = ((double)n.lo[1] - o.y) * id.y, ty1 = ((double)n.hi[1] - o.y) * id.y;
@@ -211,13 +258,21 @@ __device__ __forceinline__ bool box_hit(const DBVHNode& n, d3 o, d3 id, double t
   double tn = fmax(fmax(fmin(tx0, tx1), fmin(ty0, ty1)), fmax(fmin(tz0, tz1), tmin));
   double tf = fmin(fmin(fmax(tx0, tx1), fmax(ty0, ty1)), fmin(fmax(tz0, tz1), tmax));
   // margins: the box is padded by >= 1 float ulp; allow 1e-9 relative slack
-  return tn <= tf + fabs(tf) * 1e-9 + 1e-12;
+  return tn <= tf + fabs(tf) * KC(1e-9) + KC(1e-12);
 }
 
 __device__ __forceinline__ d3 inv_dir(d3 d) {
   // zero components get a huge finite inverse: no 0*inf NaN in the slabs
   return mk(1.0 / (d.x != 0 ? d.x : 1e-300), 1.0 / (d.y != 0 ? d.y : 1e-300), 1.0 / (d.z != 0 ? d.z : 1e-300));
 }
+
+// The geometry an occlusion query needs (a small by-value subset of KParams).
+struct Geo {
+  const DSphere* spheres;
+  const DTri* tris;
+  const DBVHNode* bvh;
+  int32_t ns, nt, use_bvh;
+};
 
 struct Cand {
   unsigned long long s, t;  // bit i: sphere i / triangle i may be hit (linear scenes, <= 64 each)
@@ -234,7 +289,7 @@ struct HitSel {
 // (spheres before triangles; an exact-t tie is resolved by hittable index so
 // the later hittable wins, as in Go), or BVH traversal with the same rule.
 template <bool kCount>
-__device__ __forceinline__ bool closest_hit(const KParams& p, d3 o, d3 d, HitSel& hs, int* stack, Cand m,
+__device__ __forceinline__ bool closest_hit(const Geo& p, d3 o, d3 d, HitSel& hs, int* stack, Cand m,
                                             Counters& c) {
   const double tmin = 0.001;
   double closest = __builtin_inf();
@@ -278,7 +333,7 @@ __device__ __forceinline__ bool closest_hit(const KParams& p, d3 o, d3 d, HitSel
     }
     return found;
   }
-  // candidate masks (primary rays: the workgroup's frustum culling; all ones
+  // candidate masks (primary rays: the tile's frustum culling; all ones
   // otherwise) are wave-uniform, so the skips are scalar branches
   const bool use_m = p.ns <= 64 && p.nt <= 64;
   for (int i = 0; i < p.ns; ++i) {
@@ -317,10 +372,11 @@ __device__ __forceinline__ bool closest_hit(const KParams& p, d3 o, d3 d, HitSel
   return found;
 }
 
-// hitWorld used as an occlusion query (calculateSmartShadow only asks
-// whether any hittable is hit in [tmin, tmax], renderer.go:305,320).
+// hitWorld used as an occlusion query over everything (BVH or large linear
+// scenes): calculateSmartShadow only asks whether any hittable is hit in
+// [tmin, tmax] (renderer.go:305,320).
 template <bool kCount>
-__device__ __forceinline__ bool any_hit(const KParams& p, d3 o, d3 d, double tmax, int* stack, Counters& c) {
+__device__ __forceinline__ bool any_hit(const Geo& p, d3 o, d3 d, double tmax, int* stack, Counters& c) {
   const double tmin = 0.001;
   const double a = len2(d);
   const double inv_a = approx_rcp(a);
@@ -363,7 +419,7 @@ __device__ __forceinline__ bool any_hit(const KParams& p, d3 o, d3 d, double tma
   return false;
 }
 
-// ------------------------------------------------------------ shading
+// ------------------------------------------------------------ culling
 // Shadow-cone culling (linear-scan scenes with <= 64 spheres and <= 64
 // triangles).  calculateSmartShadow's rays all leave the hit point P inside
 // the cone around ldir of half-angle asin(0.1) (|RandomVec3InUnitSphere *
@@ -373,40 +429,26 @@ __device__ __forceinline__ bool any_hit(const KParams& p, d3 o, d3 d, double tma
 // their tests; everything else gets the exact Sphere.Hit / Triangle.Hit
 // test, so occlusion results are unchanged.  Margins (~1e-7 relative) are
 // eight orders of magnitude above binary64 rounding.
-// Does the cone (apex, unit axis, half-angle with cosine cos_t / sine sin_t)
-// meet the sphere (cc, r)?  Conservative: the radius is inflated by ~1e-7.
-__device__ __forceinline__ bool cone_meets_sphere(const double* cc, double r, d3 apex, d3 axis, double cos_t,
-                                                  double sin_t) {
-  const d3 v = ld3(cc) - apex;
-  const double dc2 = len2(v);
-  const double dc = sqrt(dc2);
-  const double ra = fabs(r) * (1.0 + 1e-7) + 1e-7 * dc + 1e-12;
-  if (dc <= ra) return true;
-  const double tl = sqrt(fmax(dc2 - ra * ra, 0.0));
-  // angle(v, axis) <= theta + beta  <=>  v.axis >= cos_t*tl - sin_t*ra
-  return dot(v, axis) >= cos_t * (1.0 - 1e-9) * tl - (sin_t + 1e-9) * ra - 1e-7 * dc;
-}
-
 __device__ __forceinline__ bool in_cone(const double* cc, double r, d3 P, d3 ldir, double ldist) {
   const d3 v = ld3(cc) - P;
   const double dc2 = len2(v);
   const double dc = sqrt(dc2);
-  const double ra = fabs(r) * (1.0 + 1e-7) + 1e-7 * dc + 1e-12;  // inflated radius
+  const double ra = fabs(r) * KC(1.0 + 1e-7) + KC(1e-7) * dc + KC(1e-12);  // inflated radius
   if (dc <= ra) return true;                                       // P inside / on it
-  if (dc - ra > ldist * (1.0 + 1e-7) + 1e-9) return false;         // beyond the light
+  if (dc - ra > ldist * KC(1.0 + 1e-7) + KC(1e-9)) return false;         // beyond the light
   // angle(v, ldir) <= alpha + beta, sin(alpha) = 0.1, sin(beta) = ra/dc:
   // v.ldir >= dc*cos(alpha+beta) = cos(alpha)*sqrt(dc^2-ra^2) - 0.1*ra
   const double tl = sqrt(fmax(dc2 - ra * ra, 0.0));
-  return dot(v, ldir) >= 0.99498 * tl - 0.1 * ra - 1e-7 * dc;
+  return dot(v, ldir) >= KC(0.99498) * tl - KC(0.1) * ra - KC(1e-7) * dc;
 }
 
 // `self` is the hittable that was hit.  When the hit is on its outside
 // (front face) and every cone direction leaves the surface by a clear angle
 // (N.ldir >= 0.1015 > sin(alpha)), a convex hittable (sphere of positive
 // radius, or createCube's box) cannot be hit again at t >= 0.001.
-__device__ __forceinline__ Cand cone_candidates(const KParams& p, d3 P, d3 N, bool front, int self, d3 ldir,
+__device__ __forceinline__ Cand cone_candidates(const Geo& p, d3 P, d3 N, bool front, int self, d3 ldir,
                                                 double ldist) {
-  const bool self_out = front && dot(N, ldir) >= 0.1015;
+  const bool self_out = front && dot(N, ldir) >= KC(0.1015);
   Cand m{0ull, 0ull};
   for (int i = 0; i < p.ns; ++i) {
     const DSphere& S = p.spheres[i];
@@ -423,7 +465,7 @@ __device__ __forceinline__ Cand cone_candidates(const KParams& p, d3 P, d3 N, bo
 
 // hitWorld(shadowRay, 0.001, dist) restricted to the candidates.
 template <bool kCount>
-__device__ __forceinline__ bool any_hit_masked(const KParams& p, d3 o, d3 d, double tmax, Cand m, Counters& c) {
+__device__ __forceinline__ bool any_hit_masked(const Geo& p, d3 o, d3 d, double tmax, Cand m, Counters& c) {
   const double a = len2(d);
   const double inv_a = approx_rcp(a);
   for (unsigned long long b = m.s; b; b &= b - 1) {
@@ -441,96 +483,85 @@ __device__ __forceinline__ bool any_hit_masked(const KParams& p, d3 o, d3 d, dou
   return false;
 }
 
-// calculateDirectLighting (renderer.go:229-297) with calculateSmartShadow
-// (renderer.go:299-331) inlined.  The 16 soft rays of a light are produced
-// by ONE loop over rejection tries (3 draws each, the same draws in the same
-// order as 16 calls of RandomVec3InUnitSphere): a wave then runs ~max over
-// lanes of the total tries (~43) instead of 16 x the max tries per point
-// (~7), and the ray of an accepted point is traced right away.
+// Occlusion of one shadow ray: candidates when culling is on, else all.
 template <bool kCount>
-__device__ __forceinline__ d3 direct_lighting(const KParams& p, const DMat* __restrict__ m, d3 P, d3 N, bool front,
-                                              int self, rt_rng& rng, int* stack, Counters& c,
-                                              unsigned long long (&dt)[3]) {
-  const double amb = m->ambient;
-  d3 total = mk(amb, amb, amb);
-  const bool masks = !p.use_bvh && p.ns <= 64 && p.nt <= 64;
-  for (int li = 0; li < p.nl; ++li) {
-    const DLight& L = p.lights[li];
-    d3 lv = ld3(L.pos) - P;
-    double ldist = sqrt(lv.x * lv.x + lv.y * lv.y + lv.z * lv.z);
-    d3 ldir = ldist == 0 ? mk(0, 0, 0) : divs(lv, ldist);
-    if (ldist < 0.001) continue;
-    cnt<kCount>(c, C_LIGHT);
-    cnt<kCount>(c, C_SHADOW);
-    Cand cm{~0ull, ~0ull};
-    bool occluded;
-    if (masks) {
-#ifdef RT_WG_TIMING
-      const unsigned long long u0 = __builtin_amdgcn_s_memtime();
-#endif
-      cm = cone_candidates(p, P, N, front, self, ldir, ldist);
-#ifdef RT_WG_TIMING
-      const unsigned long long u1 = __builtin_amdgcn_s_memtime();
-      dt[0] += u1 - u0;
-#endif
-      occluded = (cm.s | cm.t) != 0 && any_hit_masked<kCount>(p, P, ldir, ldist, cm, c);
-#ifdef RT_WG_TIMING
-      dt[1] += __builtin_amdgcn_s_memtime() - u1;
-#endif
-    } else {
-      occluded = any_hit<kCount>(p, P, ldir, ldist, stack, c);
-    }
-    double sf;
-    if (occluded) {
-      sf = 0.0;
-    } else if (p.soft) {
-#ifdef RT_WG_TIMING
-      const unsigned long long u2 = __builtin_amdgcn_s_memtime();
-#endif
-      const bool trace = !masks || (cm.s | cm.t) != 0;
-      int need = 16, unocc = 0;
-      while (need > 0) {
-        const double x = draw<kCount>(rng, c);
-        const double y = draw<kCount>(rng, c);
-        const double z = draw<kCount>(rng, c);
-        const d3 pt = mk(x * 2 - 1, y * 2 - 1, z * 2 - 1);
-        if (len2(pt) < 1) {
-          --need;
-          cnt<kCount>(c, C_SHADOW);
-          bool occ = false;
-          if (trace) {
-            const d3 sdir = normalize(ldir + muls(pt, 0.1));
-            occ = masks ? any_hit_masked<kCount>(p, P, sdir, ldist, cm, c)
-                        : any_hit<kCount>(p, P, sdir, ldist, stack, c);
-          }
-          unocc += occ ? 0 : 1;
-        }
-      }
-      sf = (double)unocc / 16.0;  // shadowSum (a count of 1.0s) / 16
-#ifdef RT_WG_TIMING
-      dt[2] += __builtin_amdgcn_s_memtime() - u2;
-#endif
-    } else {
-      sf = 1.0;
-    }
-    if (sf > 0.0) {
-      const double metallic = m->metallic;
-      double cos_t = gmax0(dot(N, ldir));
-      double intensity = cos_t * L.intensity / (ldist * ldist);
-      total = total + muls(ld3(m->albedo), m->diffuse_strength * intensity * sf);
-      if (metallic > 0.5) {
-        d3 view = normalize(neg(P));
-        d3 half = normalize(ldir + view);
-        double hc = gmax0(dot(N, half));
-        const int sp = m->spec_pow;
-        double si = sp == 64 ? pow_n<64>(hc) : (sp == 48 ? pow_n<48>(hc) : pow_n<32>(hc));
-        total = total + muls(ld3(L.color), si * intensity * sf * metallic * 3.0);
-      }
-    }
-  }
-  return total;
+__device__ __forceinline__ bool shadow_blocked(const Geo& p, bool masks, d3 o, d3 d, double tmax, Cand m,
+                                               int* stack, Counters& c) {
+  if (masks) return (m.s | m.t) != 0 && any_hit_masked<kCount>(p, o, d, tmax, m, c);
+  return any_hit<kCount>(p, o, d, tmax, stack, c);
 }
 
+// ------------------------------------------------------------ soft shadows
+// Sequential form (every lane its own): ONE loop over rejection tries (3
+// draws each — the same draws, in the same order, as 16 calls of
+// RandomVec3InUnitSphere); the ray of an accepted point is traced at once.
+// A wave runs ~max over lanes of the total tries (~43) instead of 16 x the
+// max tries per point (~7).  Returns the number of unoccluded rays.
+template <bool kCount>
+__device__ __forceinline__ int soft_seq(const Geo& p, bool masks, bool trace, d3 P, d3 ldir, double ldist,
+                                        Cand cm, rt_rng& rng, int* stack, Counters& c) {
+  int need = 16, unocc = 0;
+  while (need > 0) {
+    const double x = draw<kCount>(rng, c);
+    const double y = draw<kCount>(rng, c);
+    const double z = draw<kCount>(rng, c);
+    const d3 pt = mk(x * 2 - 1, y * 2 - 1, z * 2 - 1);
+    if (len2(pt) < 1) {
+      --need;
+      cnt<kCount>(c, C_SHADOW);
+      bool occ = false;
+      if (trace) occ = shadow_blocked<kCount>(p, masks, P, normalize(ldir + muls(pt, 0.1)), ldist, cm, stack, c);
+      unocc += occ ? 0 : 1;
+    }
+  }
+  return unocc;
+}
+
+// Cooperative form for ONE owner lane, executed by the whole (converged)
+// wave: lane h evaluates rejection try h of the owner's stream (draws
+// 3h..3h+2 via the PCG jump table), a ballot picks the first `need`
+// accepted tries in order, those lanes trace their rays, and the owner's
+// stream advances by exactly the draws the sequential loop would consume.
+// All arguments are wave-uniform (the owner's values, read from its lane).
+struct CoopOut {
+  uint64_t x;  // the owner's stream state after its 16 points
+  int unocc;   // unoccluded rays
+  int tries;   // rejection tries consumed
+};
+#ifdef RT_COOP_NOINLINE
+#define RT_COOP_FN __device__ __noinline__
+#else
+#define RT_COOP_FN __device__ __forceinline__
+#endif
+template <bool kCount>
+RT_COOP_FN CoopOut soft_coop(const Geo p, bool masks, bool trace, d3 P, d3 ldir, double ldist, Cand cm, uint64_t x,
+                             const uint64_t* jump, int* stack, Counters& c) {
+  const int lane = (int)(threadIdx.x & 63);
+  int need = 16, unocc = 0, tries = 0;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  while (need > 0) {
+    const double dx = draw_at(x, jump, 3 * lane), dy = draw_at(x, jump, 3 * lane + 1),
+                 dz = draw_at(x, jump, 3 * lane + 2);
+    const d3 pt = mk(dx * 2 - 1, dy * 2 - 1, dz * 2 - 1);
+    const bool acc = len2(pt) < 1;
+    const unsigned long long am = __ballot(acc);
+    const int rank = __popcll(am & below);
+    const bool chosen = acc && rank < need;
+    const unsigned long long chm = __ballot(chosen);
+    const int nch = __popcll(chm);
+    // tries consumed: up to and including the last chosen one
+    const int used = nch == need ? 64 - __clzll(chm) : 64;
+    bool occ = false;
+    if (chosen && trace) occ = shadow_blocked<kCount>(p, masks, P, normalize(ldir + muls(pt, 0.1)), ldist, cm, stack, c);
+    unocc += nch - __popcll(__ballot(chosen && occ));
+    need -= nch;
+    tries += used;
+    x = jump[2 * (3 * used)] * x + jump[2 * (3 * used) + 1];
+  }
+  return CoopOut{x, unocc, tries};
+}
+
+// ------------------------------------------------------------ scatter
 // Material.Scatter for the 7 JSON-reachable materials.  Single exit, result
 // by value (out-parameters on divergent paths were demoted to scratch).
 struct Scat {
@@ -596,47 +627,105 @@ __device__ __forceinline__ Scat scatter(const DMat* __restrict__ m, d3 d, d3 N, 
 }
 
 // ------------------------------------------------------------ kernel
+// Kernel parameters that only the sample set-up and the epilogue need are
+// re-read from the kernarg segment through a laundered pointer at each use
+// (scalar-cache loads) instead of being held in SGPRs across the bounce
+// loop: the loop's SGPR pressure otherwise spills uniform values into VGPR
+// lanes and reloads them inside the intersection loops.
+typedef const __attribute__((address_space(4))) KParams* KArg;  // constant (kernarg) address space
+__device__ __forceinline__ KArg fresh() {
+  // KParams is the kernel's only argument: it sits at offset 0 of the kernarg segment
+  KArg k = (KArg)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(k));
+  return k;
+}
+
+// Where workgroup wg works: which local tile (dispatch order) and which
+// block of P pixels inside it.
+struct TileLoc {
+  int blk, lt, tile, tx, ty;
+};
+__device__ __forceinline__ TileLoc tile_loc(KArg k, int wg) {
+  TileLoc t;
+  // dispatch order: the host sorts this rank's tiles by estimated cost, so
+  // long multi-bounce paths start first instead of trailing the launch
+  const int slot = wg / k->blocks_per_tile;
+  t.blk = wg - slot * k->blocks_per_tile;
+  t.lt = k->tile_order ? k->tile_order[slot] : slot;  // local tile index
+  t.tile = k->rank + t.lt * k->world;
+  t.tx = t.tile % k->tiles_x;
+  t.ty = t.tile / k->tiles_x;
+  return t;
+}
+
+// The scene view and switches of one phase of the bounce loop, re-read
+// per phase (see fresh()).  Staged scenes address the LDS copy.
+struct Hot {
+  Geo g;
+  const DMat* mats;
+  const DLight* lights;
+  const uint64_t* jump;
+  int nl, max_depth;
+  bool recursive, soft, masks;
+};
+extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
+template <bool kStage>
+__device__ __forceinline__ Hot hot() {
+  KArg k = fresh();
+  Hot h;
+  h.g = Geo{k->spheres, k->tris, k->bvh, k->ns, k->nt, k->use_bvh};
+  h.mats = k->mats;
+  h.lights = k->lights;
+  h.jump = k->jump;
+  if constexpr (kStage) {
+    const unsigned char* base = reinterpret_cast<const unsigned char*>(k->stage_src);
+    h.g.spheres = reinterpret_cast<const DSphere*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->spheres) - base));
+    h.g.tris = reinterpret_cast<const DTri*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->tris) - base));
+    h.mats = reinterpret_cast<const DMat*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->mats) - base));
+    h.lights = reinterpret_cast<const DLight*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->lights) - base));
+    h.jump = reinterpret_cast<const uint64_t*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->jump) - base));
+  }
+  h.nl = k->nl;
+  h.max_depth = k->max_depth;
+  h.recursive = k->recursive != 0;
+  h.soft = k->soft != 0;
+  h.masks = !h.g.use_bvh && h.g.ns <= 64 && h.g.nt <= 64;  // shadow-cone culling available
+  return h;
+}
+
 template <bool kCount, bool kStage>
 __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel(const KParams pk) {
   __shared__ double red[3][256];
   __shared__ unsigned long long cred[9];
-  // dynamic LDS: [staged scene (kStage)][BVH stacks (kStack x 256 ints, lane-interleaved)]
-  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
+  // dynamic LDS (dyn_lds): [staged scene + PCG jump table (kStage)][BVH stacks (kStack x 256 ints)]
 
   const int tid = threadIdx.x;
-  KParams p = pk;
+  const int lane = tid & 63;
   if constexpr (kStage) {
-    // LDS-staged scene primitives: spheres | triangles | materials | lights
-    // (one contiguous prefix of the device scene buffer), so the divergent
-    // per-lane primitive reads of the shadow and scatter code hit LDS
-    // (~64 cycles) instead of L1/L2 (measured: 55% of wave time in waits)
+    // LDS-staged scene primitives: spheres | triangles | materials | lights |
+    // jump table (one contiguous prefix of the device scene buffer), so the
+    // divergent per-lane reads of the shadow / scatter code hit LDS instead
+    // of L1/L2 (measured: 55% of wave time in memory waits without it)
     const uint4* __restrict__ src = reinterpret_cast<const uint4*>(pk.stage_src);
     uint4* dst = reinterpret_cast<uint4*>(dyn_lds);
     for (int i = tid; i < pk.stage_bytes / 16; i += 256) dst[i] = src[i];
-    const unsigned char* base = reinterpret_cast<const unsigned char*>(pk.stage_src);
-    p.spheres = reinterpret_cast<const DSphere*>(dyn_lds + (reinterpret_cast<const unsigned char*>(pk.spheres) - base));
-    p.tris = reinterpret_cast<const DTri*>(dyn_lds + (reinterpret_cast<const unsigned char*>(pk.tris) - base));
-    p.mats = reinterpret_cast<const DMat*>(dyn_lds + (reinterpret_cast<const unsigned char*>(pk.mats) - base));
-    p.lights = reinterpret_cast<const DLight*>(dyn_lds + (reinterpret_cast<const unsigned char*>(pk.lights) - base));
     __syncthreads();
   }
-  const int S = p.slices;
-  const int P = p.pix_per_wg;
   const int wg = blockIdx.x;
-  // dispatch order: the host sorts this rank's tiles by estimated cost, so
-  // long multi-bounce paths start first instead of trailing the launch
-  const int slot = wg / p.blocks_per_tile;
-  const int blk = wg - slot * p.blocks_per_tile;
-  const int lt = p.tile_order ? p.tile_order[slot] : slot;  // local tile index
-  const int tile = p.rank + lt * p.world;
-  const int tx = tile % p.tiles_x, ty = tile / p.tiles_x;
-  const int pix = tid / S;  // pixel within the block
-  const int q = tid - pix * S;  // sample slice
-  const int tp = blk * P + pix;  // row-major pixel index within the 32x32 tile
-  const int lx = tp & 31, ly = tp >> 5;
-  const int x = tx * 32 + lx, y = ty * 32 + ly;
-  const bool valid = pix < P && tp < 1024 && tile < p.ntiles && x < p.W && y < p.H;
-  int* stack = reinterpret_cast<int*>(dyn_lds + p.stack_off) + (tid >> 6) * (kStack * 64) + (tid & 63);
+  int x, y, q;
+  bool valid;
+  {
+    KArg k = fresh();
+    const int S = k->slices, Pw = k->pix_per_wg;
+    const TileLoc tl = tile_loc(k, wg);
+    const int pix = tid / S;           // pixel within the block
+    q = tid - pix * S;                 // sample slice
+    const int tp = tl.blk * Pw + pix;  // row-major pixel index within the 32x32 tile
+    x = tl.tx * 32 + (tp & 31);
+    y = tl.ty * 32 + (tp >> 5);
+    valid = pix < Pw && tp < 1024 && tl.tile < k->ntiles && x < k->W && y < k->H;
+  }
+  int* stack = reinterpret_cast<int*>(dyn_lds + pk.stack_off) + (tid >> 6) * (kStack * 64) + lane;
 
   Counters c;
   if constexpr (kCount) {
@@ -645,16 +734,12 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel(const KP
   }
 #ifdef RT_WG_TIMING
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-  unsigned long long dbg_hit = 0, dbg_light = 0, dbg_scat = 0, dbg_iter = 0;
+  unsigned long long dbg_iter = 0;
+  // wave-uniform section clocks (s_memtime): hit, lighting, soft; coop / seq invocations
+  unsigned long long dbg_hit = 0, dbg_light = 0, dbg_soft = 0, dbg_ncoop = 0, dbg_nseq = 0;
 #endif
-  unsigned long long dbg_t[3] = {0, 0, 0};  // timing builds: candidates / hard shadow / soft loop
 
-  const uint32_t pixel = (uint32_t)y * (uint32_t)p.W + (uint32_t)x;
-  const double W = (double)p.W, H = (double)p.H;
-  // getRay constants (renderer.go:377-390): lowerLeftCorner = origin -
-  // horizontal/2 - vertical/2 - (0,0,focal)
-  const double vw = 2.0 * p.aspect;
-  const double llcx = p.cam[0] - vw / 2, llcy = p.cam[1] - 1.0, llcz = p.cam[2] - 1.0;
+  const uint32_t pixel = (uint32_t)y * (uint32_t)pk.W + (uint32_t)x;
 
   // primary-ray frustum culling (host-computed per tile, schedule.cpp): only
   // primitives whose bounding sphere meets the cone of the tile's camera
@@ -662,132 +747,226 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel(const KP
   // traces its ray; provably-missed primitives are skipped, like a BVH.
   const Cand all{~0ull, ~0ull};
   Cand prim = all;
-  if (p.tile_masks) {
-    prim.s = p.tile_masks[2 * lt];
-    prim.t = p.tile_masks[2 * lt + 1];
+  if (pk.tile_masks) {
+    const int lt = tile_loc(fresh(), wg).lt;
+    prim.s = pk.tile_masks[2 * lt];
+    prim.t = pk.tile_masks[2 * lt + 1];
   }
 
-  double sx = 0, sy = 0, sz = 0;  // this lane's sample sum
+  // this lane's sample sum lives in LDS (frees 6 VGPRs of the bounce loop;
+  // same additions in the same order as a register sum)
+  red[0][tid] = 0;
+  red[1][tid] = 0;
+  red[2][tid] = 0;
   d3 o = mk(0, 0, 0), d = mk(0, 0, 0), T = mk(1, 1, 1), L = mk(0, 0, 0);
-  rt_rng rng{0, 0, 0, 0};
+  rt_rng rng{0};
   int depth = 0;
   int s = q;
   bool alive = false;
 
   for (;;) {
-    if (!alive) {
-      if (!valid || s >= p.spp) break;
-      rt_rng_init(&rng, p.seed_key, pixel, (uint32_t)s);
-      s += S;
+    // ---- (1) a lane without a path starts its next camera sample
+    KArg k = fresh();
+    if (!alive && valid && s < k->spp) {
+      rt_rng_init(&rng, k->seed_key, pixel, (uint32_t)s);
+      s += k->slices;
       cnt<kCount>(c, C_CAM);
-      double u = ((double)x + draw<kCount>(rng, c)) / W;
-      double v = ((double)y + draw<kCount>(rng, c)) / H;
-      o = mk(p.cam[0], p.cam[1], p.cam[2]);
+      int xi = x, yi = y;
+      asm volatile("" : "+v"(xi), "+v"(yi));  // recompute (double)x, (double)y here rather than keep them live
+      double u = ((double)xi + draw<kCount>(rng, c)) / (double)k->W;
+      double v = ((double)yi + draw<kCount>(rng, c)) / (double)k->H;
+      // getRay (renderer.go:377-390): lowerLeftCorner = origin -
+      // horizontal/2 - vertical/2 - (0,0,focal)
+      const double vw = 2.0 * k->aspect;
+      const double llcx = k->cam[0] - vw / 2, llcy = k->cam[1] - 1.0, llcz = k->cam[2] - 1.0;
+      o = mk(k->cam[0], k->cam[1], k->cam[2]);
       d = mk(((llcx + vw * u) + 0.0) - o.x, ((llcy + 0.0) + 2.0 * v) - o.y, ((llcz + 0.0) + 0.0) - o.z);
       T = mk(1, 1, 1);
       L = mk(0, 0, 0);
       depth = 0;
       alive = true;
     }
-    bool done = depth >= p.max_depth;  // traceRay depth cut-off: contributes 0
-    HitSel hs;
+    if (__ballot(alive) == 0) break;  // wave-uniform: nothing left anywhere in the wave
 #ifdef RT_WG_TIMING
-    const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
     ++dbg_iter;
+    const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
 #endif
-    if (!done) {
-      cnt<kCount>(c, C_BOUNCE);
-      done = !closest_hit<kCount>(p, o, d, hs, stack, depth == 0 ? prim : all, c);  // miss -> black
+
+    // ---- (2) closest hit (hitWorld, renderer.go:170)
+    bool shade = false, front = false;
+    d3 P = mk(0, 0, 0), N = mk(0, 0, 0);
+    int mi = 0, self = -1;
+    if (alive) {
+      const Hot h = hot<kStage>();
+      const Geo& g = h.g;
+      bool done = depth >= h.max_depth;  // traceRay depth cut-off: contributes 0
+      HitSel hs;
+      if (!done) {
+        cnt<kCount>(c, C_BOUNCE);
+        done = !closest_hit<kCount>(g, o, d, hs, stack, depth == 0 ? prim : all, c);  // miss -> black
+      }
+      if (done) {
+        red[0][tid] += L.x;
+        red[1][tid] += L.y;
+        red[2][tid] += L.z;
+        alive = false;
+      } else {
+        shade = true;
+        cnt<kCount>(c, C_SHADE);
+        // HitRecord of the closest primitive (sphere.go:42-58, triangle.go:68-81)
+        if (!hs.is_tri) {
+          const DSphere& S0 = g.spheres[hs.idx];
+          const double t = hs.num / len2(d);
+          P = o + muls(d, t);
+          d3 outward = divs(P - ld3(S0.c), S0.r);
+          front = dot(d, outward) < 0;
+          N = front ? outward : neg(outward);
+          mi = S0.mat;
+          self = S0.obj;
+        } else {
+          const DTri& T0 = g.tris[hs.idx];
+          P = o + muls(d, hs.num);
+          double w = 1.0 - hs.u - hs.v;
+          d3 n = ld3(T0.n);
+          N = normalize((muls(n, w) + muls(n, hs.u)) + muls(n, hs.v));
+          front = dot(d, N) < 0;
+          if (!front) N = neg(N);
+          mi = T0.mat;
+          self = T0.obj;
+        }
+      }
     }
+
 #ifdef RT_WG_TIMING
     const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
     dbg_hit += ts1 - ts0;
 #endif
-    if (done) {
-      sx += L.x;
-      sy += L.y;
-      sz += L.z;
-      alive = false;
-      continue;
-    }
-    cnt<kCount>(c, C_SHADE);
-    // HitRecord of the closest primitive (sphere.go:42-58, triangle.go:68-81)
-    d3 P, N;
-    bool front;
-    int mi, self;
-    if (!hs.is_tri) {
-      const DSphere& S0 = p.spheres[hs.idx];
-      const double t = hs.num / len2(d);
-      P = o + muls(d, t);
-      d3 outward = divs(P - ld3(S0.c), S0.r);
-      front = dot(d, outward) < 0;
-      N = front ? outward : neg(outward);
-      mi = S0.mat;
-      self = S0.obj;
-    } else {
-      const DTri& T0 = p.tris[hs.idx];
-      P = o + muls(d, hs.num);
-      double w = 1.0 - hs.u - hs.v;
-      d3 n = ld3(T0.n);
-      N = normalize((muls(n, w) + muls(n, hs.u)) + muls(n, hs.v));
-      front = dot(d, N) < 0;
-      if (!front) N = neg(N);
-      mi = T0.mat;
-      self = T0.obj;
-    }
-    const DMat* __restrict__ m = p.mats + mi;
+    if (__ballot(shade) == 0) continue;  // wave-uniform: every path of the wave missed or ended
+
+    // ---- (3) calculateDirectLighting (renderer.go:229-297), light by light
+    const Hot h = hot<kStage>();
+    const Geo& g = h.g;
+    const bool masks = h.masks, soft = h.soft;
+    const DMat* __restrict__ m = h.mats + mi;
+    d3 D = mk(0, 0, 0);
+    if (shade) D = mk(m->ambient, m->ambient, m->ambient);
+    for (int li = 0; li < h.nl; ++li) {
+      const DLight& Lt = h.lights[li];
+      d3 ldir = mk(0, 0, 0);
+      double ldist = 0;
+      Cand cm{0ull, 0ull};
+      bool lit = false, occl = false;
+      if (shade) {
+        d3 lv = ld3(Lt.pos) - P;
+        ldist = sqrt(lv.x * lv.x + lv.y * lv.y + lv.z * lv.z);
+        ldir = ldist == 0 ? mk(0, 0, 0) : divs(lv, ldist);
+        lit = !(ldist < 0.001);
+        if (lit) {
+          cnt<kCount>(c, C_LIGHT);
+          cnt<kCount>(c, C_SHADOW);
+          if (masks) cm = cone_candidates(g, P, N, front, self, ldir, ldist);
+          occl = shadow_blocked<kCount>(g, masks, P, ldir, ldist, cm, stack, c);  // hard shadow ray
+        }
+      }
+      const bool need_soft = lit && !occl && soft;
+      const bool trace = !masks || (cm.s | cm.t) != 0;
+      int unocc = 0;
+      // soft shadows: wave-converged decision between the two forms
+      const unsigned long long owners = __ballot(need_soft);
 #ifdef RT_WG_TIMING
-    const unsigned long long ts2 = __builtin_amdgcn_s_memtime();
+      const unsigned long long ts2 = __builtin_amdgcn_s_memtime();
 #endif
-    d3 D = direct_lighting<kCount>(p, m, P, N, front, self, rng, stack, c, dbg_t);
+      if (owners != 0) {
 #ifdef RT_WG_TIMING
-    const unsigned long long ts3 = __builtin_amdgcn_s_memtime();
-    dbg_light += ts3 - ts2;
+        if (__popcll(owners) <= RT_COOP_MAX)
+          dbg_ncoop += __popcll(owners);
+        else
+          dbg_nseq += 1;
 #endif
-    d3 E = ld3(m->emit);
-    const Scat sc = scatter<kCount>(m, d, N, front, rng, c);
+        if (__popcll(owners) <= RT_COOP_MAX) {
+          for (unsigned long long b = owners; b; b &= b - 1) {
+            const int ow = __builtin_ctzll(b);
+            const CoopOut r = soft_coop<kCount>(
+                g, masks, rl32(trace ? 1u : 0u, ow) != 0, inv3(rl3(P, ow)), inv3(rl3(ldir, ow)), inv(rld(ldist, ow)),
+                Cand{rl64(cm.s, ow), rl64(cm.t, ow)}, rl64(rng.x, ow), h.jump, stack, c);
+            if (lane == ow) {
+              unocc = r.unocc;
+              rng.x = r.x;
+              cnt<kCount>(c, C_SHADOW, 16);
+              cnt<kCount>(c, C_RNG, 3ull * r.tries);
+            }
+          }
+        } else if (need_soft) {
+          unocc = soft_seq<kCount>(g, masks, trace, P, ldir, ldist, cm, rng, stack, c);
+        }
+      }
 #ifdef RT_WG_TIMING
-    dbg_scat += __builtin_amdgcn_s_memtime() - ts3;
+      dbg_soft += __builtin_amdgcn_s_memtime() - ts2;
 #endif
-    if (!sc.ok) {
-      L = L + mul(T, E + D);
-      sx += L.x;
-      sy += L.y;
-      sz += L.z;
-      alive = false;
-      continue;
+      if (lit) {
+        const double sf = occl ? 0.0 : (soft ? (double)unocc / 16.0 : 1.0);  // shadowSum / 16
+        if (sf > 0.0) {
+          const double metallic = m->metallic;
+          double cos_t = gmax0(dot(N, ldir));
+          double intensity = cos_t * Lt.intensity / (ldist * ldist);
+          D = D + muls(ld3(m->albedo), m->diffuse_strength * intensity * sf);
+          if (metallic > 0.5) {
+            d3 view = normalize(neg(P));
+            d3 half = normalize(ldir + view);
+            double hc = gmax0(dot(N, half));
+            const int sp = m->spec_pow;
+            double si = sp == 64 ? pow_n<64>(hc) : (sp == 48 ? pow_n<48>(hc) : pow_n<32>(hc));
+            D = D + muls(ld3(Lt.color), si * intensity * sf * metallic * 3.0);
+          }
+        }
+      }
     }
-    L = L + mul(T, E + muls(D, m->dw));
-    if (!p.recursive || depth + 1 >= p.max_depth) {
-      sx += L.x;
-      sy += L.y;
-      sz += L.z;
-      alive = false;
-      continue;
+
+#ifdef RT_WG_TIMING
+    dbg_light += __builtin_amdgcn_s_memtime() - ts1;
+#endif
+    // ---- (4) Material.Scatter and the traceRay combination (renderer.go:181-226)
+    if (shade) {
+      d3 E = ld3(m->emit);
+      const Scat sc = scatter<kCount>(m, d, N, front, rng, c);
+      bool fin;
+      if (!sc.ok) {
+        L = L + mul(T, E + D);
+        fin = true;
+      } else {
+        L = L + mul(T, E + muls(D, m->dw));
+        const Hot h2 = hot<kStage>();
+        fin = !h2.recursive || depth + 1 >= h2.max_depth;
+        if (!fin) {
+          T = mul(T, muls(sc.A, m->rw));
+          o = P;
+          d = sc.nd;
+          depth += 1;
+        }
+      }
+      if (fin) {
+        red[0][tid] += L.x;
+        red[1][tid] += L.y;
+        red[2][tid] += L.z;
+        alive = false;
+      }
     }
-    T = mul(T, muls(sc.A, m->rw));
-    o = P;
-    d = sc.nd;
-    depth += 1;
   }
 
 #ifdef RT_WG_TIMING
   const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
 #endif
-  // ---- reduce the S slices of each pixel in slice order
-  red[0][tid] = sx;
-  red[1][tid] = sy;
-  red[2][tid] = sz;
+  // ---- reduce the S slices of each pixel in a fixed pairwise order
   if constexpr (kCount) {
     __syncthreads();
     for (int i = 0; i < 9; ++i) atomicAdd(&cred[i], c.v[i]);
   }
-  // pairwise tree over the S slices of each pixel (fixed order: the result
-  // depends only on the samples, never on timing or the GPU count)
+  KArg k = fresh();
+  const int S = k->slices, Pw = k->pix_per_wg;
   for (int n = S; n > 1;) {
     const int h = (n + 1) >> 1;
     __syncthreads();
-    if (pix < P && q < n - h) {
+    if (tid < Pw * S && q < n - h) {
       red[0][tid] += red[0][tid + h];
       red[1][tid] += red[1][tid + h];
       red[2][tid] += red[2][tid + h];
@@ -795,26 +974,26 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel(const KP
     n = h;
   }
   __syncthreads();
-  if (tid < P) {
-    const int tp2 = blk * P + tid;
-    const int lx2 = tp2 & 31, ly2 = tp2 >> 5;
-    const int x2 = tx * 32 + lx2, y2 = ty * 32 + ly2;
-    if (tp2 < 1024 && tile < p.ntiles && x2 < p.W && y2 < p.H) {
+  if (tid < Pw) {
+    const TileLoc tl = tile_loc(k, wg);
+    const int tp2 = tl.blk * Pw + tid;
+    const int x2 = tl.tx * 32 + (tp2 & 31), y2 = tl.ty * 32 + (tp2 >> 5);
+    if (tp2 < 1024 && tl.tile < k->ntiles && x2 < k->W && y2 < k->H) {
       const int base = tid * S;
       const double ax = red[0][base], ay = red[1][base], az = red[2][base];
-      const double n = (double)p.spp;
+      const double n = (double)k->spp;
       const double mx = ax / n, my = ay / n, mz = az / n;  // DivScalar(float64(samples))
       size_t oi;
-      if (p.layout == RT_LAYOUT_IMAGE)
-        oi = (size_t)y2 * p.W + x2;
+      if (k->layout == RT_LAYOUT_IMAGE)
+        oi = (size_t)y2 * k->W + x2;
       else
-        oi = (size_t)lt * 1024 + (size_t)tp2;
-      if (p.out_linear) {
-        p.out_linear[oi * 3 + 0] = (float)mx;
-        p.out_linear[oi * 3 + 1] = (float)my;
-        p.out_linear[oi * 3 + 2] = (float)mz;
+        oi = (size_t)tl.lt * 1024 + (size_t)tp2;
+      if (k->out_linear) {
+        k->out_linear[oi * 3 + 0] = (float)mx;
+        k->out_linear[oi * 3 + 1] = (float)my;
+        k->out_linear[oi * 3 + 2] = (float)mz;
       }
-      if (p.out_rgba) {
+      if (k->out_rgba) {
         // toneMap (renderer.go:348-367) then Vec3.ToRGB (vector.go:106-109)
         const double g = 1.0 / 2.2;
         const double tx_ = clamp01(pow_gamma(1.0 - exp(-(mx * 1.0)), g));
@@ -822,39 +1001,25 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel(const KP
         const double tz_ = clamp01(pow_gamma(1.0 - exp(-(mz * 1.0)), g));
         const uint32_t px4 = go_u8(clamp01(tx_) * 255) | (go_u8(clamp01(ty_) * 255) << 8) |
                              (go_u8(clamp01(tz_) * 255) << 16) | (255u << 24);
-        *reinterpret_cast<uint32_t*>(p.out_rgba + oi * 4) = px4;
+        *reinterpret_cast<uint32_t*>(k->out_rgba + oi * 4) = px4;
       }
     }
   }
   if constexpr (kCount) {
     __syncthreads();
-    if (tid < 9) atomicAdd(&p.counts[tid], cred[tid]);
+    if (tid < 9) atomicAdd(&k->counts[tid], cred[tid]);
   }
 #ifdef RT_WG_TIMING
-  for (int off = 32; off > 0; off >>= 1) {  // wave max of the per-lane section times
-    dbg_hit = max(dbg_hit, (unsigned long long)__shfl_xor(dbg_hit, off));
-    dbg_light = max(dbg_light, (unsigned long long)__shfl_xor(dbg_light, off));
-    dbg_scat = max(dbg_scat, (unsigned long long)__shfl_xor(dbg_scat, off));
-    dbg_iter = max(dbg_iter, (unsigned long long)__shfl_xor(dbg_iter, off));
-    for (int k = 0; k < 3; ++k) dbg_t[k] = max(dbg_t[k], (unsigned long long)__shfl_xor(dbg_t[k], off));
-  }
-  if (p.dbg && (tid & 63) == 0) {
-    unsigned hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    unsigned long long* r = p.dbg + ((size_t)wg * 4 + (tid >> 6)) * 8;
+  if (k->dbg && lane == 0) {
+    unsigned long long* r = k->dbg + ((size_t)wg * 4 + (tid >> 6)) * 8;
     r[0] = t_start;
     r[1] = t_loop;
     r[2] = __builtin_amdgcn_s_memrealtime();
-    r[3] = ((unsigned long long)xcc << 32) | hw;
-    r[4] = dbg_hit;
-    r[5] = dbg_light;
-    r[6] = dbg_scat;
+    r[3] = dbg_hit;
+    r[4] = dbg_light;
+    r[5] = dbg_soft;
+    r[6] = (dbg_ncoop << 32) | dbg_nseq;
     r[7] = dbg_iter;
-    r[4] = dbg_t[0];  // repurposed: candidates
-    r[6] = dbg_t[2];  // soft loop (hard shadow = light - both)
-    r[5] = dbg_light;
   }
 #endif
 }

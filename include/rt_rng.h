@@ -10,18 +10,17 @@
  * the same draws as the kernel because both key the stream by
  * (seed, pixel, sample) — never by tile, rank or thread.
  *
- * Spec (v2):
- *   key0   = mix64(seed)                                (once per render)
- *   k      = mix64(key0 ^ (pixel << 32 | sample))       pixel = y*W + x
- *   b      = mix64(k + G)                               G = 0x9E3779B97F4A7C15
- *   state  = (lo32(k), hi32(k), lo32(b), hi32(b)); an all-zero state gets s0 = 1
- *   next() = xoshiro128** (Blackman & Vigna 2018): out = rotl(s1*5, 7)*9,
- *            then the standard update with t = s1 << 9 and rotl(s3, 11)
- *   draw() = next() * 2^-32   (uniform on [0,1), 32 random bits; exact in
- *            binary64; the Go equivalent is rand.Float64(), random.go:12-14)
- * mix64 is the SplitMix64 finaliser.  Every operation of next() is a 32-bit
- * integer op (full-rate VALU on CDNA4), which is why this generator was
- * chosen over 64-bit-state ones.
+ * Spec (v3): one PCG32 stream (O'Neill 2014, PCG-XSH-RR 64/32) per sample.
+ *   key0    = mix64(seed)                               (once per render)
+ *   x_0     = mix64(key0 ^ (pixel << 32 | sample))      pixel = y*W + x
+ *   x_{i+1} = x_i * 6364136223846793005 + 1442695040888963407   (mod 2^64)
+ *   out_i   = rotr32((uint32)(((x_i >> 18) ^ x_i) >> 27), x_i >> 59)
+ *   draw_i  = out_i * 2^-32   (uniform on [0,1), 32 random bits, exact in
+ *             binary64; the Go equivalent is rand.Float64(), random.go:12-14)
+ * mix64 is the SplitMix64 finaliser.  Why PCG: the LCG state jumps ahead in
+ * O(1) — x_{i+j} = A_j x_i + C_j — so the kernel can evaluate later draws
+ * of a stream on other lanes (cooperative rejection sampling, DESIGN.md
+ * §Kernels) and still consume exactly this sequence.
  *
  * The draw ORDER is the reference's call order:
  * per sample u, v (renderer.go:155-156); per bounce, for every light whose
@@ -41,10 +40,11 @@
 #define RT_RNG_FN static inline
 #endif
 
-#define RT_RNG_GAMMA 0x9E3779B97F4A7C15ULL
+#define RT_PCG_MULT 6364136223846793005ULL
+#define RT_PCG_INC 1442695040888963407ULL
 
 typedef struct {
-  uint32_t s0, s1, s2, s3;
+  uint64_t x;
 } rt_rng;
 
 RT_RNG_FN uint64_t rt_mix64(uint64_t z) {
@@ -56,27 +56,20 @@ RT_RNG_FN uint64_t rt_mix64(uint64_t z) {
 RT_RNG_FN uint64_t rt_rng_seed_key(uint64_t seed) { return rt_mix64(seed); }
 
 RT_RNG_FN void rt_rng_init(rt_rng* r, uint64_t seed_key, uint32_t pixel, uint32_t sample) {
-  const uint64_t k = rt_mix64(seed_key ^ (((uint64_t)pixel << 32) | (uint64_t)sample));
-  const uint64_t b = rt_mix64(k + RT_RNG_GAMMA);
-  r->s0 = (uint32_t)k;
-  r->s1 = (uint32_t)(k >> 32);
-  r->s2 = (uint32_t)b;
-  r->s3 = (uint32_t)(b >> 32);
-  r->s0 |= (uint32_t)((r->s0 | r->s1 | r->s2 | r->s3) == 0);
+  r->x = rt_mix64(seed_key ^ (((uint64_t)pixel << 32) | (uint64_t)sample));
 }
 
-RT_RNG_FN uint32_t rt_rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+/* PCG-XSH-RR output of a state value */
+RT_RNG_FN uint32_t rt_pcg_out(uint64_t x) {
+  const uint32_t xs = (uint32_t)(((x >> 18) ^ x) >> 27);
+  const uint32_t rot = (uint32_t)(x >> 59);
+  return (xs >> rot) | (xs << ((32u - rot) & 31u));
+}
 
 RT_RNG_FN uint32_t rt_rng_next(rt_rng* r) {
-  const uint32_t result = rt_rotl32(r->s1 * 5u, 7) * 9u;
-  const uint32_t t = r->s1 << 9;
-  r->s2 ^= r->s0;
-  r->s3 ^= r->s1;
-  r->s1 ^= r->s2;
-  r->s0 ^= r->s3;
-  r->s2 ^= t;
-  r->s3 = rt_rotl32(r->s3, 11);
-  return result;
+  const uint64_t old = r->x;
+  r->x = old * RT_PCG_MULT + RT_PCG_INC;
+  return rt_pcg_out(old);
 }
 
 /* x * 2^-32, built from the bits: 1.x (x in the top 32 mantissa bits) - 1 */
@@ -92,5 +85,16 @@ RT_RNG_FN double rt_bits_to_unit(uint32_t x) {
 }
 
 RT_RNG_FN double rt_rng_draw(rt_rng* r) { return rt_bits_to_unit(rt_rng_next(r)); }
+
+/* Jump coefficients: x_{i+j} = A_j * x_i + C_j (mod 2^64). */
+RT_RNG_FN void rt_pcg_jump_coeffs(uint32_t j, uint64_t* A, uint64_t* C) {
+  uint64_t a = 1, c = 0;
+  for (uint32_t k = 0; k < j; ++k) {
+    c = c * RT_PCG_MULT + RT_PCG_INC;
+    a = a * RT_PCG_MULT;
+  }
+  *A = a;
+  *C = c;
+}
 
 #endif /* RT_RNG_H */

@@ -61,11 +61,17 @@ wgdur = end.max(axis=1) - start.min(axis=1)
 order = np.argsort(-wgdur)[:10]
 print("  slowest WGs (index, us, start us):", [(int(i), round(float(wgdur[i]), 1), round(float(start[i].min()), 1))
                                               for i in order])
-for i in order[:5]:
+hit, light, soft, it = (d[:, :, k].astype(np.float64) for k in (3, 4, 5, 7))
+ncoop = (d[:, :, 6].astype(np.uint64) >> np.uint64(32)).astype(np.float64)
+nseq = (d[:, :, 6].astype(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.float64)
+tot = hit.sum() + light.sum()
+print(f"  section clocks: hit {hit.sum() / tot:.1%}  lighting {light.sum() / tot:.1%} "
+      f"(soft part {soft.sum() / tot:.1%});  per iteration hit {hit.sum() / it.sum():.0f} light {light.sum() / it.sum():.0f}")
+print(f"  soft sections: coop owners {ncoop.sum():.0f}, seq waves {nseq.sum():.0f}, iterations {it.sum():.0f}")
+for i in order[:3]:
     for w in range(4):
-        h, l, sct, it = d[i, w, 4:8]
-        if it:
-            print(f"    WG {int(i)} wave {w}: iters {it}, cycles cand {h} light {l} soft {sct} "
-                  f"(per iter: {h / it:.0f} / {l / it:.0f} / {sct / it:.0f}); wave us {end[i, w] - start[i, w]:.0f}")
+        if it[i, w]:
+            print(f"    WG {int(i)} wave {w}: iters {int(it[i, w])}, clocks hit {int(hit[i, w])} light {int(light[i, w])} "
+                  f"soft {int(soft[i, w])}, coop owners {int(ncoop[i, w])} seq {int(nseq[i, w])}; wave us {end[i, w] - start[i, w]:.0f}")
 busy = dur.sum()
 print(f"  mean waves in flight {busy / span:.1f}")
