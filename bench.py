@@ -1,25 +1,29 @@
 #!/usr/bin/env python3
 """Benchmark: Mrays/s of the gfx950 renderer on BASELINE.json's config.
 
-metric  : Mrays/s = W*H*spp / render time (primary samples per second — the
+metric  : Mrays/s = W*H*spp / render time (primary samples per second, the
           reference's published rays_per_second semantics, README.md:61,
-          demo-assets/sphere_reflections_light_benchmark.json:12)
-workload: configs[1] — sphere_reflections_light, 800x600, 100 spp, depth 50,
+          demo-assets/sphere_reflections_light_benchmark.json:12).
+workload: configs[1]: sphere_reflections_light, 800x600, 100 spp, depth 50,
           soft shadows + recursive reflections, 1 GPU.  The committed scene
-          places every object behind the reference's fixed -Z camera
-          (renderer.go:377-390), so its faithful render is black; the
+          puts every object behind the reference's fixed -Z camera
+          (renderer.go:377-390), so its faithful render is black.  The
           headline `value` is therefore the "facing" variant (camera z=+8,
-          scenes/sphere_reflections_light_facing.json: same objects, lights,
-          materials), which is MORE work.  The as-committed scene is timed too
-          and reported under "as_committed".
-step    : one full render of the frame (all ranks' tiles) with the scene and
-          output buffers resident in HBM; for N>1 also the RCCL gather of the
-          packed tiles to rank 0 and the unpack there.  Strong scaling: the
-          frame is fixed, tiles are dealt t -> t % N.
+          scenes/sphere_reflections_light_facing.json: same objects, lights and
+          materials), which is MORE work.  --with-as-committed also times
+          the as-committed scene ("as_committed" in the output).
+step    : one render of the frame with the scene and output buffers resident
+          in HBM.  For N>1 a step also includes the RCCL gather of the packed
+          tiles to rank 0 and the unpack kernel there.
+scaling : weak.  At N GPUs the frame is 800 x (600*N): the same viewport at
+          N-fold vertical sample density.  Its 32x32 tiles are dealt
+          t -> t % N, so every GPU traces about one
+          800x600x100 frame of primary samples.  value = all ranks' samples /
+          max-over-ranks time.
 
 usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scene PATH]
                        [--width 800 --height 600 --spp 100 --depth 50]
-                       [--no-cpu-baseline]
+                       [--no-cpu-baseline] [--strong]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 import argparse
@@ -34,7 +38,7 @@ for p in (ROOT, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-# FP64 operations per counted event: adds, muls,
+# FP64 operations per counted event: the adds, muls,
 # divides and square roots of the reference's formulas, 1 each.
 FLOPS_PER_EVENT = {
     "camera_rays": 12,     # u, v (2 add + 2 div) + getRay (8)
@@ -46,8 +50,9 @@ FLOPS_PER_EVENT = {
     "shadow_rays": 15,     # soft direction: scale, add, normalize
     "rng_draws": 5,        # unit conversion + rejection arithmetic
 }
-PEAK_FP64_TFLOPS = 78.6   # 256 CU x 2.4 GHz x 128 FP64 FLOP/clk/CU (MI355X spec)
+PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) peak: 256 CU x 2.4 GHz x 128 FLOP/clk
 PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
 
 
 def parse():
@@ -62,13 +67,17 @@ def parse():
     ap.add_argument("--spp", type=int, default=100)
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--strong", action="store_true", help="fixed 800x600 frame for every N (strong scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--with-as-committed", action="store_true",
+                    help="also time the as-committed (black) scene; off by default so the profiled command's "
+                         "render_kernel launches are all of the headline workload")
     ap.add_argument("--cpu-threads", type=int, default=0)
     return ap.parse_args()
 
 
 class Frame:
-    """Device buffers + one render step for this rank."""
+    """Device buffers and one render step of this rank."""
 
     def __init__(self, rtgo, torch, dist, ctx, w, h, st, rank, world, device):
         self.rtgo, self.torch, self.dist = rtgo, torch, dist
@@ -79,44 +88,47 @@ class Frame:
             self.layout = rtgo.RT_LAYOUT_IMAGE
             n = w * h
         else:
+            from rtgo import shard
+
             self.layout = rtgo.RT_LAYOUT_PACKED_TILES
-            self.max_local = rtgo.tiles_for_rank(w, h, 0, world)  # rank 0 owns the most tiles
+            self.max_local = shard.max_local_tiles(w, h, world)  # rank 0 owns the most tiles
             n = self.max_local * 1024
             if rank == 0:
                 self.g_lin = torch.empty(world * n * 3, dtype=torch.float32, device=dev)
                 self.g_rgba = torch.empty(world * n * 4, dtype=torch.uint8, device=dev)
+                self.img_lin = torch.zeros(w * h * 3, dtype=torch.float32, device=dev)
+                self.img_rgba = torch.zeros(w * h * 4, dtype=torch.uint8, device=dev)
         self.lin = torch.zeros(n * 3, dtype=torch.float32, device=dev)
         self.rgba = torch.zeros(n * 4, dtype=torch.uint8, device=dev)
-        if world > 1 and rank == 0:
-            self.img_lin = torch.zeros(w * h * 3, dtype=torch.float32, device=dev)
-            self.img_rgba = torch.zeros(w * h * 4, dtype=torch.uint8, device=dev)
 
     def render(self, stream):
         self.ctx.render_async(self.w, self.h, self.st, self.lin.data_ptr(), self.rgba.data_ptr(), stream,
                               self.rank, self.world, self.layout)
 
     def gather(self, stream):
+        """The one collective (rtgo.shard.gather_packed: an equal-size
+        gather of the packed tiles to rank 0 over RCCL), then the unpack
+        kernel on rank 0."""
         if self.world == 1:
             return
-        dist, torch = self.dist, self.torch
+        from rtgo import shard
+
+        shard.gather_packed(self.dist, self.lin, self.world, self.rank, getattr(self, "g_lin", None))
+        shard.gather_packed(self.dist, self.rgba, self.world, self.rank, getattr(self, "g_rgba", None))
         if self.rank == 0:
-            gl = list(self.g_lin.chunk(self.world))
-            gr = list(self.g_rgba.chunk(self.world))
-            dist.gather(self.lin, gl, dst=0)
-            dist.gather(self.rgba, gr, dst=0)
             self.rtgo.unpack_tiles_async(self.w, self.h, self.world, self.max_local, self.g_lin.data_ptr(),
                                          self.g_rgba.data_ptr(), self.img_lin.data_ptr(),
                                          self.img_rgba.data_ptr(), stream)
-        else:
-            dist.gather(self.lin, None, dst=0)
-            dist.gather(self.rgba, None, dst=0)
 
     def counts(self, stream):
         return self.ctx.count(self.w, self.h, self.st, self.lin.data_ptr(), self.rgba.data_ptr(), stream,
                               self.rank, self.world, self.layout)
 
 
-def time_steps(frame, torch, dist, world, steps, warmup, stream_ptr, kernel_events):
+def time_steps(frame, torch, dist, world, steps, warmup, stream_ptr):
+    """W untimed steps, then K timed steps between barrier + synchronize on
+    both sides; returns (max-over-ranks seconds, per-launch kernel ms).
+    Kernel durations come from HIP events recorded on the render stream."""
     for _ in range(warmup):
         frame.render(stream_ptr)
         frame.gather(stream_ptr)
@@ -127,15 +139,12 @@ def time_steps(frame, torch, dist, world, steps, warmup, stream_ptr, kernel_even
     evs = []
     t0 = time.perf_counter()
     for _ in range(steps):
-        if kernel_events:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record()
-            frame.render(stream_ptr)
-            e1.record()
-            evs.append((e0, e1))
-        else:
-            frame.render(stream_ptr)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()  # current stream = the render stream (set in main)
+        frame.render(stream_ptr)
+        e1.record()
+        evs.append((e0, e1))
         frame.gather(stream_ptr)
     torch.cuda.synchronize()
     if world > 1:
@@ -145,8 +154,7 @@ def time_steps(frame, torch, dist, world, steps, warmup, stream_ptr, kernel_even
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kms = [a.elapsed_time(b) for a, b in evs]
-    return elapsed, kms
+    return elapsed, [a.elapsed_time(b) for a, b in evs]
 
 
 def flops_of(counts):
@@ -154,8 +162,9 @@ def flops_of(counts):
 
 
 def cpu_baseline(args, rtgo, st):
-    import numpy as np  # noqa: F401
-
+    """The oracle (C restatement of the Go goroutine path) on the host cores.
+    Bounded sample: the full 800x600x100 frame when it is cheap (the facing
+    scene is mostly sky: ~1.5 s on 8 cores), median of 3 after a warm-up."""
     import oracle
 
     scene = rtgo.Scene.load_from_file(args.scene)
@@ -164,7 +173,6 @@ def cpu_baseline(args, rtgo, st):
     except AttributeError:
         cores = os.cpu_count() or 1
     threads = args.cpu_threads or min(16, cores)
-    # bounded sample: the full frame when it is cheap, else the first tiles
     oracle.render(scene, args.width, args.height, st, nthreads=threads, max_tiles=16)  # warm-up
     times = []
     for _ in range(3):
@@ -175,15 +183,28 @@ def cpu_baseline(args, rtgo, st):
     secs = times[1]
     rays = args.width * args.height * args.spp
     return {
-        "value": rays / secs / 1e6,
+        "value": round(rays / secs / 1e6, 3),
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"full {args.width}x{args.height}x{args.spp}spp frame of the facing scene, median of 3 "
-                  f"after 1 warm-up, oracle/oracle.c (C restatement of the Go goroutine path) on {threads} "
-                  f"threads",
-        "seconds": secs,
+        "sample": f"full {args.width}x{args.height}x{args.spp}spp frame of the facing scene, median of 3 runs "
+                  f"({secs:.2f} s) after 1 warm-up; oracle/oracle.c on {threads} threads (tile queue of "
+                  f"renderer.go:67-148; the Go toolchain is absent, SURVEY.md §8c)",
     }
+
+
+def pmc_traffic(workload):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes
+    (profiles/r01_pmc_traffic.json, made by scripts/pmc_traffic.py with the
+    gfx950 corrections of MI355X_MICROARCH.md §HBM), if they match."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != workload:
+        return None
+    return d.get("hbm_bytes_per_launch")
 
 
 def main():
@@ -196,48 +217,56 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        if world == 1:
-            print(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes", file=sys.stderr)
-            sys.exit(2)
+    if world != args.gpus:
+        print(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes (WORLD_SIZE={world})",
+              file=sys.stderr)
+        sys.exit(2)
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    W = args.width
+    H = args.height if args.strong else args.height * world  # weak scaling: N-fold vertical sample density
     st = rtgo.default_settings()
     st.samples, st.max_depth, st.seed = args.spp, args.depth, args.seed
     st.num_workers = world
-    # a dedicated stream: the render kernel, its timing events and the
-    # gather all run on it (torch.cuda.Event records on the current stream)
+    # a dedicated stream: render kernel, timing events and gather all run on
+    # it (torch.cuda.Event records on the current stream)
     bench_stream = torch.cuda.Stream()
     torch.cuda.set_stream(bench_stream)
     stream_ptr = bench_stream.cuda_stream
 
     ctx = rtgo.Context(local)
     ctx.set_scene(rtgo.Scene.load_from_file(args.scene))
-    frame = Frame(rtgo, torch, dist, ctx, args.width, args.height, st, rank, world, local)
-
-    # algorithmic FP64 work of this rank's launch (counting variant, untimed)
-    counts = frame.counts(stream_ptr)
+    frame = Frame(rtgo, torch, dist, ctx, W, H, st, rank, world, local)
+    counts = frame.counts(stream_ptr)  # algorithmic work of this rank's launch (counting variant, untimed)
     torch.cuda.synchronize()
-    elapsed, kms = time_steps(frame, torch, dist, world, args.steps, args.warmup, stream_ptr, True)
+    elapsed, kms = time_steps(frame, torch, dist, world, args.steps, args.warmup, stream_ptr)
 
-    # the as-committed scene (renders black: every object behind the camera)
-    ctx2 = rtgo.Context(local)
-    ctx2.set_scene(rtgo.Scene.load_from_file(args.as_committed))
-    frame2 = Frame(rtgo, torch, dist, ctx2, args.width, args.height, st, rank, world, local)
-    elapsed2, kms2 = time_steps(frame2, torch, dist, world, args.steps, args.warmup, stream_ptr, True)
+    as_committed = None
+    if args.with_as_committed:
+        ctx2 = rtgo.Context(local)
+        ctx2.set_scene(rtgo.Scene.load_from_file(args.as_committed))
+        frame2 = Frame(rtgo, torch, dist, ctx2, W, H, st, rank, world, local)
+        elapsed2, kms2 = time_steps(frame2, torch, dist, world, args.steps, args.warmup, stream_ptr)
+        as_committed = {
+            "scene": "sphere_reflections_light.json as committed (renders black: objects behind the camera)",
+            "value": round(W * H * args.spp * args.steps / elapsed2 / 1e6, 3),
+            "ms_per_step": round(elapsed2 / args.steps * 1e3, 4),
+            "kernel_ms": round(sum(kms2) / len(kms2), 4),
+        }
 
-    rays = args.width * args.height * args.spp
+    rays = W * H * args.spp  # all ranks together
     value = rays * args.steps / elapsed / 1e6
-    value2 = rays * args.steps / elapsed2 / 1e6
-    kernel_s = sum(kms) / len(kms) / 1e3
+    kernel_s = sum(kms) / len(kms) / 1e3  # this rank's average launch
     flops = flops_of(counts)
     achieved_tf = flops / kernel_s / 1e12
-    npix_local = rtgo.tiles_for_rank(args.width, args.height, rank, world) * 1024 if world > 1 else \
-        args.width * args.height
-    hbm_bytes = npix_local * 16 + ctx_scene_bytes(ctx)
+    npix_local = rtgo.tiles_for_rank(W, H, rank, world) * 1024 if world > 1 else W * H
+    # algorithmic HBM bytes: framebuffer write (float3 + RGBA8 = 16 B/pixel)
+    # + the flattened scene read once per workgroup-resident copy (<= 4 KB)
+    hbm_bytes = npix_local * 16 + 4096
     achieved_gbs = hbm_bytes / kernel_s / 1e9
+    workload = "sphere_reflections_light_facing %dx%d %dspp depth %d" % (W, H, args.spp, args.depth)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -253,15 +282,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": round(value / 19.78676836885329, 2),
+            "scaling": "strong" if args.strong else "weak",
+            "vs_baseline": None,  # BASELINE.md has no published number on this hardware/config
             "dtype": "f64",
-            "data": "synthetic: reference scene JSON, seeded counter-based RNG (seed %d)" % args.seed,
+            "data": "synthetic: the reference's scene JSON (camera facing the objects), seeded counter-keyed "
+                    "RNG (seed %d)" % args.seed,
             "config": {
-                "workload": "sphere_reflections_light_facing (camera z=+8) %dx%d %dspp depth %d, soft shadows, "
-                            "recursive reflections" % (args.width, args.height, args.spp, args.depth),
-                "width": args.width, "height": args.height, "spp": args.spp, "max_depth": args.depth,
-                "parallelism": "tiles t%%%d" % world if world > 1 else "1 GPU",
+                "workload": workload + ", soft shadows, recursive reflections",
+                "width": W, "height": H, "spp": args.spp, "max_depth": args.depth,
+                "parallelism": "tiles t%%%d + RCCL gather" % world if world > 1 else "1 GPU",
             },
             "roofline": {
                 "bound": "valu",
@@ -269,12 +298,14 @@ def main():
                 "peak": PEAK_FP64_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved_tf / PEAK_FP64_TFLOPS, 5),
-                "traffic": None,
-                "kernel": "render_kernel<false>",
+                "traffic": pmc_traffic(workload),
+                "kernel": "rtgo::render_kernel<false,true>",
                 "kernel_ms": round(kernel_s * 1e3, 4),
                 "flops_per_launch": flops,
-                "note": "FP64 VALU-bound path (binary64 like the Go reference; no MFMA shape). "
-                        "Algorithmic FP64 ops from the kernel's own event counts x DESIGN.md costs.",
+                "note": "FP64 VALU-bound branchy path (binary64 like the Go reference; no matrix shape, no MFMA). "
+                        "achieved = algorithmic FP64 ops of one launch (the kernel's own event counts x "
+                        "DESIGN.md per-event costs) / average launch time (HIP events on the render stream). "
+                        "traffic = HBM bytes per launch from rocprofv3 FETCH_SIZE+WRITE_SIZE passes.",
             },
             "roofline_hbm": {
                 "bound": "hbm",
@@ -282,28 +313,18 @@ def main():
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / PEAK_HBM_GBS, 7),
-                "bytes_per_launch": hbm_bytes,
+                "algorithmic_bytes_per_launch": hbm_bytes,
             },
-            "counts": counts,
-            "as_committed": {
-                "scene": "sphere_reflections_light.json as committed (black image)",
-                "value": round(value2, 3),
-                "ms_per_step": round(elapsed2 / args.steps * 1e3, 4),
-                "kernel_ms": round(sum(kms2) / len(kms2), 4),
-            },
+            "counts_rank0": counts,
+            "as_committed": as_committed,
             "cpu_baseline": cpu,
         }
         if cpu:
             out["gpu_over_cpu"] = round(value / cpu["value"], 1)
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-
-
-def ctx_scene_bytes(ctx):
-    # flattened scene read once per launch (spheres/tris/materials/lights)
-    return 4096
 
 
 if __name__ == "__main__":

@@ -651,6 +651,7 @@ int rt_scene_print_hittables(const rt_scene_buf* b) {
     }
   }
   printf("Created %d hittables total\n", created);
+  fflush(stdout);  // interleave correctly with the caller's own stdout writes
   return RT_OK;
 }
 

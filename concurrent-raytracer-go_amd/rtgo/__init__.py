@@ -291,13 +291,19 @@ class Scene:
             ob.position[:] = o.get("position", (0, 0, 0))
             ob.size[:] = o.get("size", (0, 0, 0))
             ob.radius = o.get("radius", 0.0)
+            # the fields each material kind reads, with scene.go:104-148's defaults
             m = o["material"]
-            ob.material.kind = MATERIAL_KINDS[m["type"]]
-            ob.material.color[:] = m.get("color", (0, 0, 0))
-            ob.material.roughness = m.get("roughness", 0.0)
-            ob.material.metallic = m.get("metallic", 1.0 if m["type"] == "metal" else 0.0)
-            ob.material.specular = m.get("specular", 1.0)
-            ob.material.refraction_index = m.get("refractionIndex", 1.5)
+            t = m["type"] if m["type"] in MATERIAL_KINDS else "lambertian"
+            ob.material.kind = MATERIAL_KINDS[t]
+            if t != "dielectric":
+                ob.material.color[:] = m.get("color", (0, 0, 0))
+            if t in ("metal", "shiny", "perfectmirror"):
+                ob.material.roughness = m.get("roughness", 0.0)
+            if t in ("metal", "shiny"):
+                ob.material.metallic = m.get("metallic", 1.0 if t == "metal" else 0.0)
+                ob.material.specular = m.get("specular", 1.0)
+            if t in ("glass", "dielectric"):
+                ob.material.refraction_index = m.get("refractionIndex", 1.5)
             objs.append(ob)
         ls = []
         for l in lights:

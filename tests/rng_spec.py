@@ -1,0 +1,49 @@
+"""Pure-Python statement of the random stream spec v3 (include/rt_rng.h).
+
+Independent of the C code: used to check the oracle's stream and to make
+the committed known-answer vectors (tests/golden/make_rng_vectors.py).
+"""
+M64 = (1 << 64) - 1
+MULT = 6364136223846793005
+INC = 1442695040888963407
+
+
+def mix64(z):  # SplitMix64 finaliser
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+    return z ^ (z >> 31)
+
+
+def init(seed, pixel, sample):
+    return mix64(mix64(seed & M64) ^ (((pixel & 0xFFFFFFFF) << 32) | (sample & 0xFFFFFFFF)))
+
+
+def out(x):  # PCG-XSH-RR output of a state
+    xs = (((x >> 18) ^ x) >> 27) & 0xFFFFFFFF
+    rot = x >> 59
+    return ((xs >> rot) | (xs << ((32 - rot) & 31))) & 0xFFFFFFFF
+
+
+def step(x):
+    return (x * MULT + INC) & M64
+
+
+def draws(seed, pixel, sample, n):
+    """(raw 32-bit outputs, doubles out * 2^-32) of the first n draws."""
+    x = init(seed, pixel, sample)
+    raw, vals = [], []
+    for _ in range(n):
+        r = out(x)
+        x = step(x)
+        raw.append(r)
+        vals.append(r * 2.0**-32)
+    return raw, vals
+
+
+def jump(j):
+    """(A_j, C_j) with x_{i+j} = A_j x_i + C_j mod 2^64."""
+    a, c = 1, 0
+    for _ in range(j):
+        c = (c * MULT + INC) & M64
+        a = (a * MULT) & M64
+    return a, c

@@ -77,3 +77,12 @@ def make_settings(rtgo, overrides, seed=1):
     for k, v in overrides.items():
         setattr(st, k, v)
     return st
+
+
+# Committed oracle fixtures (tests/golden/make_golden.py): (id, loader, w, h, overrides, seed)
+GOLDEN_CASES = [
+    ("spheres_facing", ("file", "sphere_reflections_light_facing.json"), 64, 48, {"samples": 4}, 1),
+    ("silver_facing", ("file", "final_silver_prism_purple_cube_facing.json"), 64, 48, {"samples": 3}, 1),
+    ("all_materials", ("json", None), 48, 32, {"samples": 4}, 7),
+    ("all_materials_hard_depth4", ("json", None), 40, 24, {"samples": 2, "soft_shadows": 0, "max_depth": 4}, 2),
+]
