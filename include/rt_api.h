@@ -179,7 +179,8 @@ int rt_scene_print_hittables(const rt_scene_buf* buf);
  *   mean radiance over samples before tone mapping.
  * out_rgba: W*H*4 bytes (may be NULL) — toneMap + ToRGB, alpha 255
  *   (renderer.go:92-97,348-367; vector.go:106-109).
- * stats may be NULL.  Uses device settings->... on device 0. */
+ * stats may be NULL.  Renders on HIP device 0; returns RT_E_DEVICE (and a
+ * message) when no device is present — there is no CPU fallback. */
 int rt_render(const rt_scene* scene, int32_t width, int32_t height, const rt_settings* settings,
               float* out_linear_rgb, uint8_t* out_rgba, rt_stats* stats);
 
@@ -219,9 +220,11 @@ int rt_unpack_tiles_async(int32_t width, int32_t height, int32_t world, int32_t 
                           const float* d_packed_linear, const uint8_t* d_packed_rgba, float* d_linear,
                           uint8_t* d_rgba, void* hip_stream);
 
-/* Debug hook: a device buffer of 16 u64 per workgroup that RT_WG_TIMING
- * builds of the kernel fill with per-wave s_memrealtime stamps
- * (start, loop end, end, XCC/HW id).  Product builds ignore it. */
+/* Debug hook: a device buffer of 32 u64 per workgroup (8 per wave) that
+ * RT_WG_TIMING builds of the kernel fill: s_memrealtime at start / loop end
+ * / end, then s_memtime clocks spent in closest hit, lighting and soft
+ * shadows, coop/sequential soft-shadow counts and loop iterations
+ * (scripts/wg_timing.py).  Product builds ignore it. */
 int rt_context_set_debug_buffer(rt_context* ctx, void* d_buf);
 
 /* Device time (seconds) of the last render launch enqueued on this context
