@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <mutex>
 #include <string>
@@ -217,17 +218,17 @@ void flatten_scene(const rt_scene& s, FlatScene* fs) {
   fs->objects = s.num_objects;
 }
 
-// Sample slices per pixel (S): a workgroup's 256 lanes are P = 256/S pixels
-// x S slices; lane (p, q) traces samples q, q+S, ... of pixel p, so a wave
-// holds the samples of one or two pixels (coherent rays) and even a frame
-// whose geometry covers a few tiles fills the chip.  S divides spp when a
-// divisor in [32, 64] exists, so every lane traces the same sample count.
-static int choose_slices(int spp) {
-  if (spp <= 1) return 1;
-  if (spp <= 64) return spp;
-  for (int d = 64; d >= 32; --d)
-    if (spp % d == 0) return d;
-  return 64;
+// Pixels per work block.  Tiles without geometry: up to
+// kMaxBlockSamples sample ids (the block's hit list lives in LDS), at most
+// 64 pixels.  Tiles with geometry: about 256 samples, so the long paths of
+// one region spread over many workgroups.
+static int big_block_pixels(int spp) {
+  if (spp <= 0) return 64;
+  return std::max(1, std::min(64, kMaxBlockSamples / spp));
+}
+static int small_block_pixels(int spp) {
+  if (spp <= 0) return 64;
+  return std::max(1, std::min(big_block_pixels(spp), 256 / spp));
 }
 
 static int validate_scene(const rt_scene* s) {
@@ -263,8 +264,8 @@ static int validate_settings(const rt_settings* st, int32_t w, int32_t h) {
     set_error("invalid image size " + std::to_string(w) + "x" + std::to_string(h));
     return RT_E_INVALID;
   }
-  if (st->samples < 0 || st->samples > (1 << 24)) {
-    set_error("invalid samples");
+  if (st->samples < 0 || st->samples > kMaxBlockSamples) {
+    set_error("samples must be in [0, " + std::to_string(kMaxBlockSamples) + "]");
     return RT_E_INVALID;
   }
   return RT_OK;
@@ -295,10 +296,12 @@ struct rt_context {
   unsigned long long* dbg = nullptr;
   // tile dispatch order (schedule.cpp), cached per (scene, W, H, rank, world)
   uint64_t scene_gen = 0;
-  int64_t order_key[5] = {-1, -1, -1, -1, -1};
-  std::vector<int32_t> order_host;
-  int32_t* d_order = nullptr;
-  size_t d_order_cap = 0;
+  int64_t order_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+  std::vector<int32_t> order_host;   // local tiles in dispatch order
+  std::vector<int32_t> blocks_host;  // work blocks, 4 ints each (schedule.cpp build_blocks)
+  int32_t* d_blocks = nullptr;
+  size_t d_blocks_cap = 0;
+  int32_t max_block_pixels = 1;
   std::vector<unsigned long long> masks_host;  // per local tile primary-ray masks
   unsigned long long* d_masks = nullptr;
   size_t d_masks_cap = 0;
@@ -355,6 +358,7 @@ int rt_context_create(int32_t device, rt_context** out) {
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_counts, 16 * sizeof(unsigned long long));
+
   if (e != hipSuccess) {
     set_error(std::string("context init failed: ") + hipGetErrorString(e));
     rt_context_destroy(c);
@@ -370,7 +374,8 @@ void rt_context_destroy(rt_context* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->d_scene) (void)hipFree(c->d_scene);
   if (c->d_counts) (void)hipFree(c->d_counts);
-  if (c->d_order) (void)hipFree(c->d_order);
+
+  if (c->d_blocks) (void)hipFree(c->d_blocks);
   if (c->d_masks) (void)hipFree(c->d_masks);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -493,22 +498,23 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   p.world = world;
   p.tiles_x = (w + 31) / 32;
   p.ntiles = rt_num_tiles(w, h);
-  // sample slices per pixel: enough lanes per pixel to fill the chip even
-  // when only a few tiles hold geometry
-  p.slices = choose_slices(st->samples);
-  if (const char* e = getenv("RTGO_SLICES")) {  // experiments only
-    const int v = atoi(e);
-    if (v >= 1 && v <= 256) p.slices = v;
-  }
-  p.pix_per_wg = 256 / p.slices;
-  p.blocks_per_tile = (1024 + p.pix_per_wg - 1) / p.pix_per_wg;
   p.layout = layout;
-  const int local_tiles = rt_tiles_for_rank(w, h, rank, world);
-  p.num_wgs = local_tiles * p.blocks_per_tile;
-  {  // tile dispatch order (expensive tiles first), uploaded when it changes
-    const int64_t key[5] = {(int64_t)c->scene_gen, w, h, rank, world};
+  {  // tile dispatch order (expensive tiles first) and work blocks, uploaded when they change
+    int bigP = big_block_pixels(st->samples), smallP = small_block_pixels(st->samples);
+    if (const char* e = getenv("RTGO_BLOCK_PIXELS")) {  // experiments only: "BIGxSMALL"
+      int b1 = 0, b2 = 0;
+      if (sscanf(e, "%dx%d", &b1, &b2) == 2 && b1 >= 1 && b2 >= 1 && b1 <= 64 && b2 <= 64 &&
+          std::max(b1, b2) * std::max(1, st->samples) <= kMaxBlockSamples) {
+        bigP = b1;
+        smallP = b2;
+      }
+    }
+    const int64_t key[8] = {(int64_t)c->scene_gen, w, h, rank, world, st->samples, bigP, smallP};
     if (memcmp(key, c->order_key, sizeof key) != 0) {
-      tile_dispatch_order(f, w, h, rank, world, &c->order_host);
+      std::vector<float> cost;
+      tile_dispatch_order(f, w, h, rank, world, &c->order_host, &cost);
+      if (getenv("RTGO_NO_TILE_ORDER")) std::sort(c->order_host.begin(), c->order_host.end());
+      build_blocks(c->order_host, cost, st->samples, bigP, smallP, &c->blocks_host);
       if (f.bvh.empty() && f.spheres.size() <= 64 && f.tris.size() <= 64) {
         tile_primary_masks(f, w, h, rank, world, &c->masks_host);
         if (c->masks_host.size() > c->d_masks_cap) {
@@ -523,18 +529,21 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
       } else {
         c->masks_host.clear();
       }
-      if (c->order_host.size() > c->d_order_cap) {
-        if (c->d_order) HIP_TRY(hipFree(c->d_order));
-        c->d_order = nullptr;
-        HIP_TRY(hipMalloc((void**)&c->d_order, c->order_host.size() * sizeof(int32_t)));
-        c->d_order_cap = c->order_host.size();
+      if (c->blocks_host.size() > c->d_blocks_cap) {
+        if (c->d_blocks) HIP_TRY(hipFree(c->d_blocks));
+        c->d_blocks = nullptr;
+        HIP_TRY(hipMalloc((void**)&c->d_blocks, c->blocks_host.size() * sizeof(int32_t)));
+        c->d_blocks_cap = c->blocks_host.size();
       }
-      if (!c->order_host.empty())
-        HIP_TRY(hipMemcpy(c->d_order, c->order_host.data(), c->order_host.size() * sizeof(int32_t),
+      if (!c->blocks_host.empty())
+        HIP_TRY(hipMemcpy(c->d_blocks, c->blocks_host.data(), c->blocks_host.size() * sizeof(int32_t),
                           hipMemcpyHostToDevice));
+      c->max_block_pixels = std::max(bigP, smallP);
       memcpy(c->order_key, key, sizeof key);
     }
-    p.tile_order = getenv("RTGO_NO_TILE_ORDER") ? nullptr : c->d_order;
+    p.blocks = c->d_blocks;
+    p.num_blocks = (int32_t)(c->blocks_host.size() / 4);
+    p.max_block_samples = c->max_block_pixels * st->samples;
     p.tile_masks = (c->masks_host.empty() || getenv("RTGO_NO_FRUSTUM")) ? nullptr : c->d_masks;
   }
   {  // LDS staging of the scene prefix + BVH stack placement
@@ -542,6 +551,7 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
     p.stage_bytes = getenv("RTGO_NO_STAGE") ? 0 : c->stage_bytes;
     p.stack_off = (p.stage_bytes + 15) & ~15;
   }
+  p.num_wgs = p.num_blocks;
   // the caller's stream, as given (NULL = the legacy default stream)
   hipStream_t s = (hipStream_t)stream;
   if (counts) HIP_TRY(hipMemsetAsync(c->d_counts, 0, 16 * sizeof(unsigned long long), s));

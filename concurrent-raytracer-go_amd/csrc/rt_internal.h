@@ -33,7 +33,11 @@ void build_sphere_bvh(FlatScene* fs);
 // Dispatch order of the local tiles of (rank, world): descending estimated
 // cost (primitives whose projected bounds overlap the tile), ties by index.
 void tile_dispatch_order(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
-                         std::vector<int32_t>* order);
+                         std::vector<int32_t>* order, std::vector<float>* local_cost);
+// Work blocks in dispatch order: {local tile, first pixel, pixel count, 0}
+// per block, small blocks on tiles with geometry (schedule.cpp).
+void build_blocks(const std::vector<int32_t>& order, const std::vector<float>& local_cost, int spp,
+                  int big_pixels, int small_pixels, std::vector<int32_t>* blocks);
 // Primary-ray candidate masks per local tile (2 x u64: spheres, triangles;
 // scenes with <= 64 of each): bit i set unless primitive i's bounding sphere
 // provably misses the cone of the tile's camera rays.
@@ -44,6 +48,10 @@ void tile_primary_masks(const FlatScene& fs, int32_t W, int32_t H, int32_t rank,
 // PCG jump-ahead entries: cooperative soft shadows evaluate up to 64
 // rejection tries (3 draws each) per round and then advance by 3*64 draws.
 constexpr int kJump = 3 * 64 + 1;
+// Largest block (pixels x spp) a workgroup renders (its hit list and
+// radiance slots live in LDS: 24 KB); the host picks P = floor(1024 / spp)
+// pixels per block (at most 64), so spp <= 1024.
+constexpr int kMaxBlockSamples = 1024;
 
 struct KParams {
   const DSphere* spheres;
@@ -56,7 +64,7 @@ struct KParams {
   uint8_t* out_rgba;
   unsigned long long* counts;  // 9 counters (rt_counts order) or null
   unsigned long long* dbg;     // per-WG timing records (RT_WG_TIMING builds only) or null
-  const int32_t* tile_order;   // local tile indices in dispatch order, or null (identity)
+  const int32_t* blocks;       // per block: {local tile, first pixel, pixel count, 0}, dispatch order
   const unsigned long long* tile_masks;  // per local tile: primary-ray candidate masks (spheres, tris) or null
   const void* stage_src;       // start of the scene prefix staged into LDS (spheres..lights)
   int32_t stage_bytes;         // bytes to stage (multiple of 16); 0 = read the scene from global memory
@@ -70,15 +78,15 @@ struct KParams {
   int32_t recursive, soft;
   int32_t rank, world;
   int32_t tiles_x, ntiles;
-  int32_t slices;          // S: sample slices per pixel
-  int32_t pix_per_wg;      // P = 256 / S (consecutive row-major pixels of a tile)
-  int32_t blocks_per_tile; // ceil(1024 / P)
+  int32_t max_block_samples; // largest P * spp of a block (<= kMaxBlockSamples)
+  int32_t num_blocks;        // this rank's blocks (one workgroup each)
   int32_t layout;     // RT_LAYOUT_*
-  int32_t num_wgs;
+  int32_t num_wgs;         // = num_blocks
 };
 
 // Enqueue the render kernel; returns hipError_t as int.
 int launch_render(const KParams& p, bool count, void* stream);
+size_t render_shmem(const KParams& p);
 int launch_unpack(int32_t W, int32_t H, int32_t world, int32_t max_local, const float* pl, const uint8_t* pr,
                   float* ol, uint8_t* orgba, void* stream);
 

@@ -2,23 +2,24 @@
 //
 // One launch renders every 32x32 tile (createRenderTasks,
 // internal/renderer/renderer.go:398-436) that this rank owns.  Design
-// (DESIGN.md §Kernels):
-//   workgroup (256 lanes = 4 wave64) = P consecutive row-major pixels of a
-//     tile x S sample slices (P = 256/S, S chosen by the host, ~spp/2);
-//   lane (p, q) traces samples q, q+S, ... of pixel p with a persistent,
-//     iterative bounce loop (traceRay, renderer.go:165-227, unrolled); a lane
-//     whose path ends regenerates its next camera sample at once, and a lane
-//     with no samples left stays in the loop as a HELPER;
+// (DESIGN.md §4):
+//   persistent waves take work BLOCKS (P pixels of a tile x all their spp
+//     samples) from an atomic queue, in the host's cost-sorted tile order;
+//   a wave alternates FILL (lanes without a path generate camera samples of
+//     the current block and run the primary closest-hit; misses end at once)
+//     and SHADE (every lane holding a path advances it one bounce of
+//     traceRay, renderer.go:165-227, unrolled), so the expensive shading
+//     runs with dense waves even when almost every camera ray misses;
 //   per bounce and light, the 16 jittered shadow rays (calculateSmartShadow,
 //     renderer.go:299-331) are produced in a wave-converged section: when
-//     only a few lanes of the wave still need them (the long multi-bounce
-//     paths that otherwise run alone at the end of the launch), all 64 lanes
-//     evaluate one owner's rejection tries in parallel (PCG jump-ahead, see
-//     include/rt_rng.h) and trace the accepted rays in parallel — same draws,
-//     same rays, same result as the sequential loop;
-//   the S slice sums of a pixel are tree-reduced in LDS in a fixed order,
-//     divided by spp, tone-mapped (toneMap, renderer.go:348-367) and written
-//     once: float3 linear radiance + RGBA8.
+//     only a few lanes of the wave need them, all 64 lanes evaluate one
+//     owner's rejection tries in parallel (PCG jump-ahead, include/rt_rng.h)
+//     and trace the accepted rays in parallel -- same draws, same rays, same
+//     result as the sequential loop;
+//   every sample's radiance lands in its own scratch slot; a finished block
+//     sums each pixel's samples in sample order (tracePixel,
+//     renderer.go:150-163), divides by spp, tone-maps (toneMap,
+//     renderer.go:348-367) and writes float3 linear radiance + RGBA8 once.
 // Small linear-scan scenes are staged into LDS by every workgroup; large
 // sphere scenes use a BVH (bvh.cpp) with per-lane LDS stacks.  Primitives
 // that provably cannot be hit (tile frustum / shadow cone tests with wide
@@ -640,22 +641,25 @@ __device__ __forceinline__ KArg fresh() {
   return k;
 }
 
-// Where workgroup wg works: which local tile (dispatch order) and which
-// block of P pixels inside it.
-struct TileLoc {
-  int blk, lt, tile, tx, ty;
+// ------------------------------------------------------------ work blocks
+// A BLOCK is np consecutive row-major pixels of one 32x32 tile with all
+// their spp samples: NB = np*spp sample ids, pixel-major (id = p*spp + s).
+// One workgroup renders one block.  The host lists the blocks in its tile
+// dispatch order (tiles sorted by estimated cost) and makes them small on
+// tiles with geometry (schedule.cpp build_blocks).
+struct BlockLoc {
+  int lt, tile, tx, ty, p0, np;  // local tile, global tile, tile coords, first pixel, pixel count
 };
-__device__ __forceinline__ TileLoc tile_loc(KArg k, int wg) {
-  TileLoc t;
-  // dispatch order: the host sorts this rank's tiles by estimated cost, so
-  // long multi-bounce paths start first instead of trailing the launch
-  const int slot = wg / k->blocks_per_tile;
-  t.blk = wg - slot * k->blocks_per_tile;
-  t.lt = k->tile_order ? k->tile_order[slot] : slot;  // local tile index
-  t.tile = k->rank + t.lt * k->world;
-  t.tx = t.tile % k->tiles_x;
-  t.ty = t.tile / k->tiles_x;
-  return t;
+__device__ __forceinline__ BlockLoc block_loc(KArg k, int b) {
+  BlockLoc r;
+  const int4 e = reinterpret_cast<const int4*>(k->blocks)[b];
+  r.lt = e.x;
+  r.p0 = e.y;
+  r.np = e.z;
+  r.tile = k->rank + r.lt * k->world;
+  r.tx = r.tile % k->tiles_x;
+  r.ty = r.tile / k->tiles_x;
+  return r;
 }
 
 // The scene view and switches of one phase of the bounce loop, re-read
@@ -693,14 +697,62 @@ __device__ __forceinline__ Hot hot() {
   return h;
 }
 
-template <bool kCount, bool kStage>
-__global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel(const KParams pk) {
-  __shared__ double red[3][256];
-  __shared__ unsigned long long cred[9];
-  // dynamic LDS (dyn_lds): [staged scene + PCG jump table (kStage)][BVH stacks (kStack x 256 ints)]
+// Camera ray of sample s of pixel (x, y): tracePixel's jitter
+// (renderer.go:155-156, the first two draws of the stream) and getRay
+// (renderer.go:377-390).  Leaves `rng` after those two draws.
+template <bool kCount>
+__device__ __forceinline__ void camera_ray(KArg k, int x, int y, int s, rt_rng& rng, d3& o, d3& d, Counters& c) {
+  rt_rng_init(&rng, k->seed_key, (uint32_t)y * (uint32_t)k->W + (uint32_t)x, (uint32_t)s);
+  const double u = ((double)x + draw<kCount>(rng, c)) / (double)k->W;
+  const double v = ((double)y + draw<kCount>(rng, c)) / (double)k->H;
+  // lowerLeftCorner = origin - horizontal/2 - vertical/2 - (0,0,focal)
+  const double vw = 2.0 * k->aspect;
+  const double llcx = k->cam[0] - vw / 2, llcy = k->cam[1] - 1.0, llcz = k->cam[2] - 1.0;
+  o = mk(k->cam[0], k->cam[1], k->cam[2]);
+  d = mk(((llcx + vw * u) + 0.0) - o.x, ((llcy + 0.0) + 2.0 * v) - o.y, ((llcz + 0.0) + 0.0) - o.z);
+}
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
+// Render kernel: one wave (64 lanes) per block, three phases.  A one-wave
+// workgroup needs no barriers and leaves the CU as soon as its own work is
+// done (4-wave workgroups held their slots until their slowest wave ended).
+//   1 VISIBILITY - the lanes generate the block's NB camera rays (NB/64
+//       each) and ask only "does it hit anything?" (an any-hit query over
+//       [0.001, +inf), with the tile's frustum candidates).  A miss is black
+//       (renderer.go:170-173) and is finished; a hit sets the sample's bit.
+//       At 800x600x100 97% of the camera rays end here.
+//   2 SHADE - the hit samples, ascending, form a list that the wave drains
+//       in rounds of kRound entries: a lane without a path takes the next
+//       entry, rebuilds its camera ray and runs the path (traceRay,
+//       renderer.go:165-227, unrolled: closest hit, direct lighting with
+//       hard + soft shadows, scatter) to its end, storing the radiance in
+//       the entry's LDS slot.  Shading runs on dense waves instead of on
+//       the ~3% of lanes whose camera ray hit.  Soft shadows of the few
+//       paths left at the end of a round run cooperatively (soft_coop).
+//   3 RESOLVE - after each round every pixel adds its entries' radiance to
+//       its running sum in sample order (misses add +0: the same sum as
+//       tracePixel, renderer.go:150-163, bit for bit); at the end the sum
+//       is divided by spp, tone-mapped (renderer.go:348-367) and written
+//       once (float3 linear + RGBA8).
+constexpr int kRound = 128;  // list entries shaded per round (LDS radiance slots)
+
+template <bool kCount, bool kStage>
+__global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KParams pk) {
+  __shared__ uint32_t hbits[kMaxBlockSamples / 32];  // hit samples of the block
+  __shared__ int hoff[kMaxBlockSamples / 32 + 1];    // list offset of each bit word; [words] = #hits
+  __shared__ uint16_t hlist[kMaxBlockSamples];       // hit sample ids, ascending
+  __shared__ double slot[kRound][3];                 // radiance of the round's entries
+  __shared__ double psum[64][3];                     // per pixel: running sum over samples
+  // dynamic LDS (dyn_lds): [staged scene + PCG jump table (kStage)][BVH stack (kStack x 64 ints)]
+
+  const int lane = threadIdx.x;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int* stack = reinterpret_cast<int*>(dyn_lds + pk.stack_off) + lane;
+  const BlockLoc blk = block_loc(fresh(), blockIdx.x);
+  const int nwords = (blk.np * pk.spp + 31) >> 5;
+  if (lane < nwords) hbits[lane] = 0;
+  psum[lane][0] = 0;
+  psum[lane][1] = 0;
+  psum[lane][2] = 0;
   if constexpr (kStage) {
     // LDS-staged scene primitives: spheres | triangles | materials | lights |
     // jump table (one contiguous prefix of the device scene buffer), so the
@@ -708,286 +760,318 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel(const KP
     // of L1/L2 (measured: 55% of wave time in memory waits without it)
     const uint4* __restrict__ src = reinterpret_cast<const uint4*>(pk.stage_src);
     uint4* dst = reinterpret_cast<uint4*>(dyn_lds);
-    for (int i = tid; i < pk.stage_bytes / 16; i += 256) dst[i] = src[i];
-    __syncthreads();
+    for (int i = lane; i < pk.stage_bytes / 16; i += 64) dst[i] = src[i];
   }
-  const int wg = blockIdx.x;
-  int x, y, q;
-  bool valid;
-  {
-    KArg k = fresh();
-    const int S = k->slices, Pw = k->pix_per_wg;
-    const TileLoc tl = tile_loc(k, wg);
-    const int pix = tid / S;           // pixel within the block
-    q = tid - pix * S;                 // sample slice
-    const int tp = tl.blk * Pw + pix;  // row-major pixel index within the 32x32 tile
-    x = tl.tx * 32 + (tp & 31);
-    y = tl.ty * 32 + (tp >> 5);
-    valid = pix < Pw && tp < 1024 && tl.tile < k->ntiles && x < k->W && y < k->H;
-  }
-  int* stack = reinterpret_cast<int*>(dyn_lds + pk.stack_off) + (tid >> 6) * (kStack * 64) + lane;
+  __syncthreads();
 
   Counters c;
   if constexpr (kCount) {
     for (int i = 0; i < 9; ++i) c.v[i] = 0;
-    if (tid < 9) cred[tid] = 0;
   }
 #ifdef RT_WG_TIMING
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   unsigned long long dbg_iter = 0;
-  // wave-uniform section clocks (s_memtime): hit, lighting, soft; coop / seq invocations
-  unsigned long long dbg_hit = 0, dbg_light = 0, dbg_soft = 0, dbg_ncoop = 0, dbg_nseq = 0;
+  // wave-uniform section clocks (s_memtime): hit, lighting, soft; phase 1 (visibility)
+  unsigned long long dbg_hit = 0, dbg_light = 0, dbg_soft = 0, dbg_vis = 0;
+  const unsigned long long tv0 = __builtin_amdgcn_s_memtime();
 #endif
-
-  const uint32_t pixel = (uint32_t)y * (uint32_t)pk.W + (uint32_t)x;
-
-  // primary-ray frustum culling (host-computed per tile, schedule.cpp): only
-  // primitives whose bounding sphere meets the cone of the tile's camera
-  // rays are scanned for depth-0 hits.  Every sample still generates and
-  // traces its ray; provably-missed primitives are skipped, like a BVH.
   const Cand all{~0ull, ~0ull};
-  Cand prim = all;
-  if (pk.tile_masks) {
-    const int lt = tile_loc(fresh(), wg).lt;
-    prim.s = pk.tile_masks[2 * lt];
-    prim.t = pk.tile_masks[2 * lt + 1];
-  }
 
-  // this lane's sample sum lives in LDS (frees 6 VGPRs of the bounce loop;
-  // same additions in the same order as a register sum)
-  red[0][tid] = 0;
-  red[1][tid] = 0;
-  red[2][tid] = 0;
-  d3 o = mk(0, 0, 0), d = mk(0, 0, 0), T = mk(1, 1, 1), L = mk(0, 0, 0);
-  rt_rng rng{0};
-  int depth = 0;
-  int s = q;
-  bool alive = false;
-
-  for (;;) {
-    // ---- (1) a lane without a path starts its next camera sample
+  // ---- phase 1: visibility of the block's camera rays
+  {
     KArg k = fresh();
-    if (!alive && valid && s < k->spp) {
-      rt_rng_init(&rng, k->seed_key, pixel, (uint32_t)s);
-      s += k->slices;
+    const BlockLoc loc = block_loc(k, blockIdx.x);
+    const int NB = loc.np * k->spp, spp = k->spp;
+    // primary-ray frustum culling (host-computed per tile, schedule.cpp):
+    // only primitives whose bounding sphere meets the cone of the tile's
+    // camera rays can be hit; every camera ray is still generated and tested
+    Cand prim = all;
+    if (k->tile_masks) {
+      prim.s = k->tile_masks[2 * loc.lt];
+      prim.t = k->tile_masks[2 * loc.lt + 1];
+    }
+    for (int id = lane; id < NB; id += 64) {
+      const int p = id / spp, s = id - p * spp;
+      const int tp = loc.p0 + p;
+      const int x = loc.tx * 32 + (tp & 31), y = loc.ty * 32 + (tp >> 5);
+      if (tp >= 1024 || loc.tile >= k->ntiles || x >= k->W || y >= k->H) continue;
       cnt<kCount>(c, C_CAM);
-      int xi = x, yi = y;
-      asm volatile("" : "+v"(xi), "+v"(yi));  // recompute (double)x, (double)y here rather than keep them live
-      double u = ((double)xi + draw<kCount>(rng, c)) / (double)k->W;
-      double v = ((double)yi + draw<kCount>(rng, c)) / (double)k->H;
-      // getRay (renderer.go:377-390): lowerLeftCorner = origin -
-      // horizontal/2 - vertical/2 - (0,0,focal)
-      const double vw = 2.0 * k->aspect;
-      const double llcx = k->cam[0] - vw / 2, llcy = k->cam[1] - 1.0, llcz = k->cam[2] - 1.0;
-      o = mk(k->cam[0], k->cam[1], k->cam[2]);
-      d = mk(((llcx + vw * u) + 0.0) - o.x, ((llcy + 0.0) + 2.0 * v) - o.y, ((llcz + 0.0) + 0.0) - o.z);
-      T = mk(1, 1, 1);
-      L = mk(0, 0, 0);
-      depth = 0;
-      alive = true;
-    }
-    if (__ballot(alive) == 0) break;  // wave-uniform: nothing left anywhere in the wave
-#ifdef RT_WG_TIMING
-    ++dbg_iter;
-    const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
-#endif
-
-    // ---- (2) closest hit (hitWorld, renderer.go:170)
-    bool shade = false, front = false;
-    d3 P = mk(0, 0, 0), N = mk(0, 0, 0);
-    int mi = 0, self = -1;
-    if (alive) {
+      rt_rng rng;
+      d3 o, d;
+      camera_ray<kCount>(k, x, y, s, rng, o, d, c);
+      if (k->max_depth <= 0) continue;  // traceRay's depth cut-off first: black
+      cnt<kCount>(c, C_BOUNCE);
       const Hot h = hot<kStage>();
-      const Geo& g = h.g;
-      bool done = depth >= h.max_depth;  // traceRay depth cut-off: contributes 0
-      HitSel hs;
-      if (!done) {
-        cnt<kCount>(c, C_BOUNCE);
-        done = !closest_hit<kCount>(g, o, d, hs, stack, depth == 0 ? prim : all, c);  // miss -> black
-      }
-      if (done) {
-        red[0][tid] += L.x;
-        red[1][tid] += L.y;
-        red[2][tid] += L.z;
-        alive = false;
-      } else {
-        shade = true;
-        cnt<kCount>(c, C_SHADE);
-        // HitRecord of the closest primitive (sphere.go:42-58, triangle.go:68-81)
-        if (!hs.is_tri) {
-          const DSphere& S0 = g.spheres[hs.idx];
-          const double t = hs.num / len2(d);
-          P = o + muls(d, t);
-          d3 outward = divs(P - ld3(S0.c), S0.r);
-          front = dot(d, outward) < 0;
-          N = front ? outward : neg(outward);
-          mi = S0.mat;
-          self = S0.obj;
-        } else {
-          const DTri& T0 = g.tris[hs.idx];
-          P = o + muls(d, hs.num);
-          double w = 1.0 - hs.u - hs.v;
-          d3 n = ld3(T0.n);
-          N = normalize((muls(n, w) + muls(n, hs.u)) + muls(n, hs.v));
-          front = dot(d, N) < 0;
-          if (!front) N = neg(N);
-          mi = T0.mat;
-          self = T0.obj;
-        }
-      }
+      // hit or miss is all this phase needs: an any-hit query over
+      // [0.001, +inf) decides exactly what hitWorld's closest hit would
+      const bool hit = h.masks ? any_hit_masked<kCount>(h.g, o, d, __builtin_inf(), prim, c)
+                               : any_hit<kCount>(h.g, o, d, __builtin_inf(), stack, c);
+      if (hit) atomicOr(&hbits[id >> 5], 1u << (id & 31));
     }
-
+  }
+  __syncthreads();
+  // ---- the hit list: ascending sample ids (the <= 32 bit words scanned across the wave)
+  {
+    const int cw = lane < nwords ? __popc(hbits[lane]) : 0;
+    int incl = cw;  // inclusive scan over the wave (Hillis-Steele)
+    for (int off = 1; off < 64; off <<= 1) {
+      const int t = __shfl_up(incl, off);
+      if (lane >= off) incl += t;
+    }
+    if (lane < nwords) hoff[lane] = incl - cw;
+    if (lane == 63) hoff[nwords] = incl;
+  }
+  __syncthreads();
+  for (int id = lane; id < nwords * 32; id += 64) {
+    const uint32_t word = hbits[id >> 5];
+    if ((word >> (id & 31)) & 1u) hlist[hoff[id >> 5] + __popc(word & ((1u << (id & 31)) - 1u))] = (uint16_t)id;
+  }
+  __syncthreads();
+  const int nh = hoff[nwords];
 #ifdef RT_WG_TIMING
-    const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
-    dbg_hit += ts1 - ts0;
+  dbg_vis = __builtin_amdgcn_s_memtime() - tv0;
 #endif
-    if (__ballot(shade) == 0) continue;  // wave-uniform: every path of the wave missed or ended
 
-    // ---- (3) calculateDirectLighting (renderer.go:229-297), light by light
-    const Hot h = hot<kStage>();
-    const Geo& g = h.g;
-    const bool masks = h.masks, soft = h.soft;
-    const DMat* __restrict__ m = h.mats + mi;
-    d3 D = mk(0, 0, 0);
-    if (shade) D = mk(m->ambient, m->ambient, m->ambient);
-    for (int li = 0; li < h.nl; ++li) {
-      const DLight& Lt = h.lights[li];
-      d3 ldir = mk(0, 0, 0);
-      double ldist = 0;
-      Cand cm{0ull, 0ull};
-      bool lit = false, occl = false;
-      if (shade) {
-        d3 lv = ld3(Lt.pos) - P;
-        ldist = sqrt(lv.x * lv.x + lv.y * lv.y + lv.z * lv.z);
-        ldir = ldist == 0 ? mk(0, 0, 0) : divs(lv, ldist);
-        lit = !(ldist < 0.001);
-        if (lit) {
-          cnt<kCount>(c, C_LIGHT);
-          cnt<kCount>(c, C_SHADOW);
-          if (masks) cm = cone_candidates(g, P, N, front, self, ldir, ldist);
-          occl = shadow_blocked<kCount>(g, masks, P, ldir, ldist, cm, stack, c);  // hard shadow ray
+  for (int base = 0; base < nh; base += kRound) {
+    const int end = min(nh, base + kRound);
+    int next = base;  // wave-uniform: next entry of this round to start
+
+    // ---- phase 2: shade the round's entries
+    d3 o = mk(0, 0, 0), d = mk(0, 0, 0), T = mk(1, 1, 1), L = mk(0, 0, 0);
+    rt_rng rng{0};
+    int depth = 0, entry = 0;
+    bool alive = false;
+    for (;;) {
+      // lanes without a path take the next entries, in lane order
+      const unsigned long long freem = __ballot(!alive);
+      const int e = next + __popcll(freem & below);
+      if (!alive && e < end) {
+        KArg k = fresh();
+        const BlockLoc loc = block_loc(k, blockIdx.x);
+        const int id = hlist[e], spp = k->spp;
+        const int p = id / spp, s = id - p * spp;
+        const int tp = loc.p0 + p;
+        Counters nc;  // phase 1 counted this camera ray and its draws
+        camera_ray<false>(k, loc.tx * 32 + (tp & 31), loc.ty * 32 + (tp >> 5), s, rng, o, d, nc);
+        T = mk(1, 1, 1);
+        L = mk(0, 0, 0);
+        depth = 0;
+        entry = e;
+        alive = true;
+      }
+      next = min(end, next + __popcll(freem));
+      if (__ballot(alive) == 0) break;  // wave-uniform: round drained
+#ifdef RT_WG_TIMING
+      ++dbg_iter;
+      const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+#endif
+
+      // (1) closest hit (hitWorld, renderer.go:170)
+      bool shade = false, front = false, fin = false;
+      d3 P = mk(0, 0, 0), N = mk(0, 0, 0);
+      int mi = 0, self = -1;
+      if (alive) {
+        const Hot h = hot<kStage>();
+        const Geo& gg = h.g;
+        bool done = depth >= h.max_depth;  // traceRay depth cut-off: contributes 0
+        HitSel hs;
+        if (!done) {
+          if (kCount && depth == 0) {  // phase 1 counted the primary query
+            Counters nc;
+            done = !closest_hit<false>(gg, o, d, hs, stack, all, nc);
+          } else {
+            cnt<kCount>(c, C_BOUNCE);
+            done = !closest_hit<kCount>(gg, o, d, hs, stack, all, c);  // miss -> black
+          }
+        }
+        if (done) {
+          fin = true;
+        } else {
+          shade = true;
+          cnt<kCount>(c, C_SHADE);
+          // HitRecord of the closest primitive (sphere.go:42-58, triangle.go:68-81)
+          if (!hs.is_tri) {
+            const DSphere& S0 = gg.spheres[hs.idx];
+            const double t = hs.num / len2(d);
+            P = o + muls(d, t);
+            d3 outward = divs(P - ld3(S0.c), S0.r);
+            front = dot(d, outward) < 0;
+            N = front ? outward : neg(outward);
+            mi = S0.mat;
+            self = S0.obj;
+          } else {
+            const DTri& T0 = gg.tris[hs.idx];
+            P = o + muls(d, hs.num);
+            double w = 1.0 - hs.u - hs.v;
+            d3 n = ld3(T0.n);
+            N = normalize((muls(n, w) + muls(n, hs.u)) + muls(n, hs.v));
+            front = dot(d, N) < 0;
+            if (!front) N = neg(N);
+            mi = T0.mat;
+            self = T0.obj;
+          }
         }
       }
-      const bool need_soft = lit && !occl && soft;
-      const bool trace = !masks || (cm.s | cm.t) != 0;
-      int unocc = 0;
-      // soft shadows: wave-converged decision between the two forms
-      const unsigned long long owners = __ballot(need_soft);
 #ifdef RT_WG_TIMING
-      const unsigned long long ts2 = __builtin_amdgcn_s_memtime();
+      const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
+      dbg_hit += ts1 - ts0;
 #endif
-      if (owners != 0) {
-#ifdef RT_WG_TIMING
-        if (__popcll(owners) <= RT_COOP_MAX)
-          dbg_ncoop += __popcll(owners);
-        else
-          dbg_nseq += 1;
-#endif
-        if (__popcll(owners) <= RT_COOP_MAX) {
-          for (unsigned long long b = owners; b; b &= b - 1) {
-            const int ow = __builtin_ctzll(b);
-            const CoopOut r = soft_coop<kCount>(
-                g, masks, rl32(trace ? 1u : 0u, ow) != 0, inv3(rl3(P, ow)), inv3(rl3(ldir, ow)), inv(rld(ldist, ow)),
-                Cand{rl64(cm.s, ow), rl64(cm.t, ow)}, rl64(rng.x, ow), h.jump, stack, c);
-            if (lane == ow) {
-              unocc = r.unocc;
-              rng.x = r.x;
-              cnt<kCount>(c, C_SHADOW, 16);
-              cnt<kCount>(c, C_RNG, 3ull * r.tries);
+
+      if (__ballot(shade) != 0) {
+        // (2) calculateDirectLighting (renderer.go:229-297), light by light
+        const Hot h = hot<kStage>();
+        const Geo& gg = h.g;
+        const bool masks = h.masks, soft = h.soft;
+        const DMat* __restrict__ m = h.mats + mi;
+        d3 D = mk(0, 0, 0);
+        if (shade) D = mk(m->ambient, m->ambient, m->ambient);
+        for (int li = 0; li < h.nl; ++li) {
+          const DLight& Lt = h.lights[li];
+          d3 ldir = mk(0, 0, 0);
+          double ldist = 0;
+          Cand cm{0ull, 0ull};
+          bool lit = false, occl = false;
+          if (shade) {
+            d3 lv = ld3(Lt.pos) - P;
+            ldist = sqrt(lv.x * lv.x + lv.y * lv.y + lv.z * lv.z);
+            ldir = ldist == 0 ? mk(0, 0, 0) : divs(lv, ldist);
+            lit = !(ldist < 0.001);
+            if (lit) {
+              cnt<kCount>(c, C_LIGHT);
+              cnt<kCount>(c, C_SHADOW);
+              if (masks) cm = cone_candidates(gg, P, N, front, self, ldir, ldist);
+              occl = shadow_blocked<kCount>(gg, masks, P, ldir, ldist, cm, stack, c);  // hard shadow ray
             }
           }
-        } else if (need_soft) {
-          unocc = soft_seq<kCount>(g, masks, trace, P, ldir, ldist, cm, rng, stack, c);
-        }
-      }
+          const bool need_soft = lit && !occl && soft;
+          // The 16 soft rays' draws are always consumed, but their result
+          // only scales terms multiplied by cos = Max(0, N.L): when that is
+          // exactly 0 (the light is behind the surface), the light and
+          // material terms are finite and D has no zero component (so adding
+          // a signed zero cannot change it), the shading is the same
+          // whatever the rays hit, and they are not traced (exact shortcut).
+          const bool quiet = gmax0(dot(N, ldir)) == 0.0 && D.x != 0.0 && D.y != 0.0 && D.z != 0.0 &&
+                             __builtin_isfinite(Lt.intensity) &&
+                             __builtin_isfinite(Lt.color[0] + Lt.color[1] + Lt.color[2]) &&
+                             __builtin_isfinite(m->albedo[0] + m->albedo[1] + m->albedo[2]) &&
+                             __builtin_isfinite(m->metallic);
+          const bool trace = (!masks || (cm.s | cm.t) != 0) && !quiet;
+          int unocc = 0;
+          // soft shadows: wave-converged decision between the two forms
+          const unsigned long long owners = __ballot(need_soft);
 #ifdef RT_WG_TIMING
-      dbg_soft += __builtin_amdgcn_s_memtime() - ts2;
+          const unsigned long long ts2 = __builtin_amdgcn_s_memtime();
 #endif
-      if (lit) {
-        const double sf = occl ? 0.0 : (soft ? (double)unocc / 16.0 : 1.0);  // shadowSum / 16
-        if (sf > 0.0) {
-          const double metallic = m->metallic;
-          double cos_t = gmax0(dot(N, ldir));
-          double intensity = cos_t * Lt.intensity / (ldist * ldist);
-          D = D + muls(ld3(m->albedo), m->diffuse_strength * intensity * sf);
-          if (metallic > 0.5) {
-            d3 view = normalize(neg(P));
-            d3 half = normalize(ldir + view);
-            double hc = gmax0(dot(N, half));
-            const int sp = m->spec_pow;
-            double si = sp == 64 ? pow_n<64>(hc) : (sp == 48 ? pow_n<48>(hc) : pow_n<32>(hc));
-            D = D + muls(ld3(Lt.color), si * intensity * sf * metallic * 3.0);
+          if (owners != 0) {
+            if (__popcll(owners) <= RT_COOP_MAX) {
+              for (unsigned long long b = owners; b; b &= b - 1) {
+                const int ow = __builtin_ctzll(b);
+                const CoopOut r = soft_coop<kCount>(
+                    gg, masks, rl32(trace ? 1u : 0u, ow) != 0, inv3(rl3(P, ow)), inv3(rl3(ldir, ow)),
+                    inv(rld(ldist, ow)), Cand{rl64(cm.s, ow), rl64(cm.t, ow)}, rl64(rng.x, ow), h.jump, stack, c);
+                if (lane == ow) {
+                  unocc = r.unocc;
+                  rng.x = r.x;
+                  cnt<kCount>(c, C_SHADOW, 16);
+                  cnt<kCount>(c, C_RNG, 3ull * r.tries);
+                }
+              }
+            } else if (need_soft) {
+              unocc = soft_seq<kCount>(gg, masks, trace, P, ldir, ldist, cm, rng, stack, c);
+            }
+          }
+#ifdef RT_WG_TIMING
+          dbg_soft += __builtin_amdgcn_s_memtime() - ts2;
+#endif
+          if (lit) {
+            const double sf = occl ? 0.0 : (soft ? (double)unocc / 16.0 : 1.0);  // shadowSum / 16
+            if (sf > 0.0) {
+              const double metallic = m->metallic;
+              double cos_t = gmax0(dot(N, ldir));
+              double intensity = cos_t * Lt.intensity / (ldist * ldist);
+              D = D + muls(ld3(m->albedo), m->diffuse_strength * intensity * sf);
+              if (metallic > 0.5) {
+                d3 view = normalize(neg(P));
+                d3 half = normalize(ldir + view);
+                double hc = gmax0(dot(N, half));
+                const int sp = m->spec_pow;
+                double si = sp == 64 ? pow_n<64>(hc) : (sp == 48 ? pow_n<48>(hc) : pow_n<32>(hc));
+                D = D + muls(ld3(Lt.color), si * intensity * sf * metallic * 3.0);
+              }
+            }
+          }
+        }
+#ifdef RT_WG_TIMING
+        dbg_light += __builtin_amdgcn_s_memtime() - ts1;
+#endif
+        // (3) Material.Scatter and the traceRay combination (renderer.go:181-226)
+        if (shade) {
+          d3 E = ld3(m->emit);
+          const Scat sc = scatter<kCount>(m, d, N, front, rng, c);
+          if (!sc.ok) {
+            L = L + mul(T, E + D);
+            fin = true;
+          } else {
+            L = L + mul(T, E + muls(D, m->dw));
+            fin = !h.recursive || depth + 1 >= h.max_depth;
+            if (!fin) {
+              T = mul(T, muls(sc.A, m->rw));
+              o = P;
+              d = sc.nd;
+              depth += 1;
+            }
           }
         }
       }
-    }
-
-#ifdef RT_WG_TIMING
-    dbg_light += __builtin_amdgcn_s_memtime() - ts1;
-#endif
-    // ---- (4) Material.Scatter and the traceRay combination (renderer.go:181-226)
-    if (shade) {
-      d3 E = ld3(m->emit);
-      const Scat sc = scatter<kCount>(m, d, N, front, rng, c);
-      bool fin;
-      if (!sc.ok) {
-        L = L + mul(T, E + D);
-        fin = true;
-      } else {
-        L = L + mul(T, E + muls(D, m->dw));
-        const Hot h2 = hot<kStage>();
-        fin = !h2.recursive || depth + 1 >= h2.max_depth;
-        if (!fin) {
-          T = mul(T, muls(sc.A, m->rw));
-          o = P;
-          d = sc.nd;
-          depth += 1;
-        }
-      }
-      if (fin) {
-        red[0][tid] += L.x;
-        red[1][tid] += L.y;
-        red[2][tid] += L.z;
+      if (fin) {  // the path's radiance goes to its entry's slot
+        slot[entry - base][0] = L.x;
+        slot[entry - base][1] = L.y;
+        slot[entry - base][2] = L.z;
         alive = false;
       }
     }
-  }
+    __syncthreads();
 
+    // ---- phase 3 (partial): each pixel adds its entries of this round, in order
+    {
+      KArg k = fresh();
+      const int P = blk.np, spp = k->spp;
+      if (lane < P) {
+        const int a0 = lane * spp, a1 = a0 + spp;
+        int e0 = hoff[a0 >> 5] + __popc(hbits[a0 >> 5] & ((1u << (a0 & 31)) - 1u));
+        int e1 = (a1 >> 5) < nwords ? hoff[a1 >> 5] + __popc(hbits[a1 >> 5] & ((1u << (a1 & 31)) - 1u)) : nh;
+        e0 = max(e0, base);
+        e1 = min(e1, end);
+        if (e0 < e1) {
+          double ax = psum[lane][0], ay = psum[lane][1], az = psum[lane][2];
+          for (int e = e0; e < e1; ++e) {
+            ax += slot[e - base][0];
+            ay += slot[e - base][1];
+            az += slot[e - base][2];
+          }
+          psum[lane][0] = ax;
+          psum[lane][1] = ay;
+          psum[lane][2] = az;
+        }
+      }
+    }
+    __syncthreads();
+  }
 #ifdef RT_WG_TIMING
   const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
 #endif
-  // ---- reduce the S slices of each pixel in a fixed pairwise order
-  if constexpr (kCount) {
-    __syncthreads();
-    for (int i = 0; i < 9; ++i) atomicAdd(&cred[i], c.v[i]);
-  }
+
+  // ---- phase 3 (final): mean, tone map, one write per pixel
   KArg k = fresh();
-  const int S = k->slices, Pw = k->pix_per_wg;
-  for (int n = S; n > 1;) {
-    const int h = (n + 1) >> 1;
-    __syncthreads();
-    if (tid < Pw * S && q < n - h) {
-      red[0][tid] += red[0][tid + h];
-      red[1][tid] += red[1][tid + h];
-      red[2][tid] += red[2][tid + h];
-    }
-    n = h;
-  }
-  __syncthreads();
-  if (tid < Pw) {
-    const TileLoc tl = tile_loc(k, wg);
-    const int tp2 = tl.blk * Pw + tid;
-    const int x2 = tl.tx * 32 + (tp2 & 31), y2 = tl.ty * 32 + (tp2 >> 5);
-    if (tp2 < 1024 && tl.tile < k->ntiles && x2 < k->W && y2 < k->H) {
-      const int base = tid * S;
-      const double ax = red[0][base], ay = red[1][base], az = red[2][base];
+  {
+    const BlockLoc loc = block_loc(k, blockIdx.x);
+    const int p = lane;
+    const int tp = loc.p0 + p;
+    const int x = loc.tx * 32 + (tp & 31), y = loc.ty * 32 + (tp >> 5);
+    if (p < loc.np && tp < 1024 && loc.tile < k->ntiles && x < k->W && y < k->H) {
       const double n = (double)k->spp;
-      const double mx = ax / n, my = ay / n, mz = az / n;  // DivScalar(float64(samples))
-      size_t oi;
-      if (k->layout == RT_LAYOUT_IMAGE)
-        oi = (size_t)y2 * k->W + x2;
-      else
-        oi = (size_t)tl.lt * 1024 + (size_t)tp2;
+      const double mx = psum[p][0] / n, my = psum[p][1] / n, mz = psum[p][2] / n;  // DivScalar(float64(samples))
+      const size_t oi = k->layout == RT_LAYOUT_IMAGE ? (size_t)y * k->W + x : (size_t)loc.lt * 1024 + (size_t)tp;
       if (k->out_linear) {
         k->out_linear[oi * 3 + 0] = (float)mx;
         k->out_linear[oi * 3 + 1] = (float)my;
@@ -1006,19 +1090,23 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel(const KP
     }
   }
   if constexpr (kCount) {
-    __syncthreads();
-    if (tid < 9) atomicAdd(&k->counts[tid], cred[tid]);
+    for (int i = 0; i < 9; ++i) {
+      // wave reduction, then one atomic per counter
+      unsigned long long v = c.v[i];
+      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0) atomicAdd(&k->counts[i], v);
+    }
   }
 #ifdef RT_WG_TIMING
   if (k->dbg && lane == 0) {
-    unsigned long long* r = k->dbg + ((size_t)wg * 4 + (tid >> 6)) * 8;
+    unsigned long long* r = k->dbg + (size_t)blockIdx.x * 8;
     r[0] = t_start;
     r[1] = t_loop;
     r[2] = __builtin_amdgcn_s_memrealtime();
     r[3] = dbg_hit;
     r[4] = dbg_light;
     r[5] = dbg_soft;
-    r[6] = (dbg_ncoop << 32) | dbg_nseq;
+    r[6] = dbg_vis;
     r[7] = dbg_iter;
   }
 #endif
@@ -1048,19 +1136,23 @@ __global__ __launch_bounds__(256) void unpack_kernel(int W, int H, int world, in
   if (orgba && pr) *reinterpret_cast<uint32_t*>(orgba + o * 4) = *reinterpret_cast<const uint32_t*>(pr + i * 4);
 }
 
+size_t render_shmem(const KParams& p) {
+  return (size_t)p.stack_off + (p.use_bvh ? sizeof(int) * kStack * 64 : 0);
+}
+
 int launch_render(const KParams& p, bool count, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (p.num_wgs <= 0) return hipSuccess;
-  const size_t shmem = (size_t)p.stack_off + (p.use_bvh ? sizeof(int) * kStack * 256 : 0);
+  const size_t shmem = render_shmem(p);
   const bool stage = p.stage_bytes > 0;
   if (count && stage)
-    hipLaunchKernelGGL((render_kernel<true, true>), dim3(p.num_wgs), dim3(256), shmem, st, p);
+    hipLaunchKernelGGL((render_kernel<true, true>), dim3(p.num_wgs), dim3(64), shmem, st, p);
   else if (count)
-    hipLaunchKernelGGL((render_kernel<true, false>), dim3(p.num_wgs), dim3(256), shmem, st, p);
+    hipLaunchKernelGGL((render_kernel<true, false>), dim3(p.num_wgs), dim3(64), shmem, st, p);
   else if (stage)
-    hipLaunchKernelGGL((render_kernel<false, true>), dim3(p.num_wgs), dim3(256), shmem, st, p);
+    hipLaunchKernelGGL((render_kernel<false, true>), dim3(p.num_wgs), dim3(64), shmem, st, p);
   else
-    hipLaunchKernelGGL((render_kernel<false, false>), dim3(p.num_wgs), dim3(256), shmem, st, p);
+    hipLaunchKernelGGL((render_kernel<false, false>), dim3(p.num_wgs), dim3(64), shmem, st, p);
   return (int)hipGetLastError();
 }
 

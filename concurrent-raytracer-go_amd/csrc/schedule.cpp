@@ -21,7 +21,7 @@
 namespace rtgo {
 
 void tile_dispatch_order(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
-                         std::vector<int32_t>* order) {
+                         std::vector<int32_t>* order, std::vector<float>* local_cost) {
   const int tiles_x = (W + 31) / 32, tiles_y = (H + 31) / 32, ntiles = tiles_x * tiles_y;
   std::vector<float> cost(ntiles, 0.0f);
   const double vw = 2.0 * fs.aspect;
@@ -54,10 +54,32 @@ void tile_dispatch_order(const FlatScene& fs, int32_t W, int32_t H, int32_t rank
   for (const DTri& t : fs.tris) add_sphere(t.bc, t.br);
 
   order->clear();
-  for (int t = rank, lt = 0; t < ntiles; t += world, ++lt) order->push_back(lt);
+  local_cost->clear();
+  for (int t = rank, lt = 0; t < ntiles; t += world, ++lt) {
+    order->push_back(lt);
+    local_cost->push_back(cost[t]);
+  }
   std::stable_sort(order->begin(), order->end(), [&](int32_t a, int32_t b) {
     return cost[rank + a * world] > cost[rank + b * world];
   });
+}
+
+void build_blocks(const std::vector<int32_t>& order, const std::vector<float>& local_cost, int spp,
+                  int big_pixels, int small_pixels, std::vector<int32_t>* blocks) {
+  // a tile that no primitive projects onto is cheap per sample (every
+  // camera ray misses): big blocks; a tile with geometry gets small blocks,
+  // so one workgroup never holds more than small_pixels pixels of long paths
+  blocks->clear();
+  for (int32_t lt : order) {
+    const int P = local_cost[lt] > 0 ? small_pixels : big_pixels;
+    for (int p0 = 0; p0 < 1024; p0 += P) {
+      blocks->push_back(lt);
+      blocks->push_back(p0);
+      blocks->push_back(std::min(P, 1024 - p0));
+      blocks->push_back(0);
+    }
+  }
+  (void)spp;
 }
 
 // Does the cone (apex, unit axis, cos/sin of its half-angle) meet the sphere

@@ -24,7 +24,7 @@ st = rtgo.default_settings()
 st.samples = SPP
 lin = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
 rgba = torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda")
-nwg_max = 2_000_000
+nwg_max = 200_000
 dbg = torch.zeros(nwg_max * 32, dtype=torch.int64, device="cuda")
 ctx.set_debug_buffer(dbg.data_ptr())
 RANK, WORLD = int(os.environ.get("WG_RANK", "0")), int(os.environ.get("WG_WORLD", "1"))
@@ -38,7 +38,8 @@ for _ in range(2):
     e1.record()
     torch.cuda.synchronize()
 print(f"kernel {e0.elapsed_time(e1):.3f} ms (rank {RANK}/{WORLD}, depth {st.max_depth})")
-d = dbg.cpu().numpy().reshape(-1, 4, 8)
+WPG = int(os.environ.get("WG_WAVES", "1"))  # waves per workgroup of the kernel
+d = dbg.cpu().numpy().reshape(-1, WPG, 8)
 used = d[:, 0, 0] != 0
 d = d[used]
 nwg = d.shape[0]
@@ -61,17 +62,16 @@ wgdur = end.max(axis=1) - start.min(axis=1)
 order = np.argsort(-wgdur)[:10]
 print("  slowest WGs (index, us, start us):", [(int(i), round(float(wgdur[i]), 1), round(float(start[i].min()), 1))
                                               for i in order])
-hit, light, soft, it = (d[:, :, k].astype(np.float64) for k in (3, 4, 5, 7))
-ncoop = (d[:, :, 6].astype(np.uint64) >> np.uint64(32)).astype(np.float64)
-nseq = (d[:, :, 6].astype(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.float64)
-tot = hit.sum() + light.sum()
-print(f"  section clocks: hit {hit.sum() / tot:.1%}  lighting {light.sum() / tot:.1%} "
-      f"(soft part {soft.sum() / tot:.1%});  per iteration hit {hit.sum() / it.sum():.0f} light {light.sum() / it.sum():.0f}")
-print(f"  soft sections: coop owners {ncoop.sum():.0f}, seq waves {nseq.sum():.0f}, iterations {it.sum():.0f}")
+hit, light, soft, fill, it = (d[:, :, k].astype(np.float64) for k in (3, 4, 5, 6, 7))
+tot = hit.sum() + light.sum() + fill.sum()
+print(f"  section clocks: fill {fill.sum() / tot:.1%}  hit {hit.sum() / tot:.1%}  lighting {light.sum() / tot:.1%} "
+      f"(soft part {soft.sum() / tot:.1%});  shade iterations {it.sum():.0f}, per iteration hit "
+      f"{hit.sum() / max(it.sum(), 1):.0f} light {light.sum() / max(it.sum(), 1):.0f}")
+wave_clk = (end - start) * 2100.0  # us -> shader clocks at ~2.1 GHz
+print(f"  accounted / wave time: {tot / wave_clk.sum():.1%}")
 for i in order[:3]:
-    for w in range(4):
-        if it[i, w]:
-            print(f"    WG {int(i)} wave {w}: iters {int(it[i, w])}, clocks hit {int(hit[i, w])} light {int(light[i, w])} "
-                  f"soft {int(soft[i, w])}, coop owners {int(ncoop[i, w])} seq {int(nseq[i, w])}; wave us {end[i, w] - start[i, w]:.0f}")
+    for w in range(WPG):
+        print(f"    WG {int(i)} wave {w}: shade iters {int(it[i, w])}, clocks fill {int(fill[i, w])} hit {int(hit[i, w])} "
+              f"light {int(light[i, w])} soft {int(soft[i, w])}; wave us {end[i, w] - start[i, w]:.0f}")
 busy = dur.sum()
 print(f"  mean waves in flight {busy / span:.1f}")
