@@ -199,10 +199,29 @@ void flatten_scene(const rt_scene& s, FlatScene* fs) {
                  add(pos, mk(h.x, h.y, h.z)),    add(pos, mk(-h.x, h.y, h.z))};
       static const int faces[6][4] = {{0, 1, 2, 3}, {1, 5, 6, 2}, {5, 4, 7, 6},
                                       {4, 0, 3, 7}, {3, 2, 6, 7}, {4, 5, 1, 0}};
+      DBox b;
+      memset(&b, 0, sizeof b);
+      b.first = (int32_t)fs->tris.size();
+      b.count = 12;
+      b.obj = i;
       for (int f = 0; f < 6; ++f) {
         push_tri(fs, v[faces[f][0]], v[faces[f][1]], v[faces[f][2]], mat, i);
         push_tri(fs, v[faces[f][0]], v[faces[f][2]], v[faces[f][3]], mat, i);
       }
+      // the box of the 8 corners, padded outward (culling only; the
+      // triangle tests stay exact)
+      for (int a = 0; a < 3; ++a) {
+        double lo = INFINITY, hi = -INFINITY;
+        for (const v3& q : v) {
+          const double c = a == 0 ? q.x : (a == 1 ? q.y : q.z);
+          lo = fmin(lo, c);
+          hi = fmax(hi, c);
+        }
+        const double pad = (fmax(fabs(lo), fabs(hi)) + (hi - lo)) * 1e-9 + 1e-12;
+        b.lo[a] = lo - pad;
+        b.hi[a] = hi + pad;
+      }
+      fs->boxes.push_back(b);
     }
   }
   for (int i = 0; i < s.num_lights; ++i) {
@@ -286,6 +305,7 @@ struct rt_context {
   size_t d_scene_bytes = 0;
   const DSphere* d_spheres = nullptr;
   const DTri* d_tris = nullptr;
+  const DBox* d_boxes = nullptr;
   const DMat* d_mats = nullptr;
   const DLight* d_lights = nullptr;
   const DBVHNode* d_bvh = nullptr;
@@ -405,7 +425,8 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
   size_t off_s = 0;
   size_t off_t = off_s + al(f.spheres.size() * sizeof(DSphere));
-  size_t off_m = off_t + al(f.tris.size() * sizeof(DTri));
+  size_t off_x = off_t + al(f.tris.size() * sizeof(DTri));
+  size_t off_m = off_x + al(f.boxes.size() * sizeof(DBox));
   size_t off_l = off_m + al(f.mats.size() * sizeof(DMat));
   size_t off_j = off_l + al(f.lights.size() * sizeof(DLight));
   size_t off_b = off_j + al(kJump * 2 * sizeof(uint64_t));
@@ -423,6 +444,7 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   std::vector<char> host(total, 0);
   memcpy(host.data() + off_s, f.spheres.data(), f.spheres.size() * sizeof(DSphere));
   memcpy(host.data() + off_t, f.tris.data(), f.tris.size() * sizeof(DTri));
+  memcpy(host.data() + off_x, f.boxes.data(), f.boxes.size() * sizeof(DBox));
   memcpy(host.data() + off_m, f.mats.data(), f.mats.size() * sizeof(DMat));
   memcpy(host.data() + off_l, f.lights.data(), f.lights.size() * sizeof(DLight));
   {
@@ -439,6 +461,7 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   HIP_TRY(hipMemcpy(base, host.data(), total, hipMemcpyHostToDevice));
   c->d_spheres = (const DSphere*)(base + off_s);
   c->d_tris = (const DTri*)(base + off_t);
+  c->d_boxes = (const DBox*)(base + off_x);
   c->d_mats = (const DMat*)(base + off_m);
   c->d_lights = (const DLight*)(base + off_l);
   c->d_bvh = (const DBVHNode*)(base + off_b);
@@ -473,6 +496,7 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   memset(&p, 0, sizeof p);
   p.spheres = c->d_spheres;
   p.tris = c->d_tris;
+  p.boxes = c->d_boxes;
   p.mats = c->d_mats;
   p.lights = c->d_lights;
   p.bvh = c->d_bvh;
@@ -487,6 +511,7 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   p.ns = (int32_t)f.spheres.size();
   p.nt = (int32_t)f.tris.size();
   p.nl = (int32_t)f.lights.size();
+  p.nb = (int32_t)f.boxes.size();
   p.use_bvh = f.bvh.empty() ? 0 : 1;
   p.W = w;
   p.H = h;

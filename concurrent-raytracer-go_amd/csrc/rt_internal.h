@@ -18,6 +18,7 @@ void set_error(const std::string& msg);
 struct FlatScene {
   std::vector<DSphere> spheres;
   std::vector<DTri> tris;
+  std::vector<DBox> boxes;    // one per cube, over its 12 triangles
   std::vector<DMat> mats;
   std::vector<DLight> lights;
   std::vector<DBVHNode> bvh;  // empty => linear scan
@@ -56,6 +57,7 @@ constexpr int kMaxBlockSamples = 1024;
 struct KParams {
   const DSphere* spheres;
   const DTri* tris;
+  const DBox* boxes;
   const DMat* mats;
   const DLight* lights;
   const DBVHNode* bvh;
@@ -72,7 +74,7 @@ struct KParams {
   double cam[3];
   double aspect;
   uint64_t seed_key;
-  int32_t ns, nt, nl, use_bvh;
+  int32_t ns, nt, nl, use_bvh, nb;
   int32_t W, H;
   int32_t spp, max_depth;
   int32_t recursive, soft;

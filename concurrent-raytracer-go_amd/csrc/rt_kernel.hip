@@ -271,9 +271,21 @@ __device__ __forceinline__ d3 inv_dir(d3 d) {
 struct Geo {
   const DSphere* spheres;
   const DTri* tris;
+  const DBox* boxes;  // one per cube: its 12 consecutive triangles
   const DBVHNode* bvh;
-  int32_t ns, nt, use_bvh;
+  int32_t ns, nt, use_bvh, nb;
 };
+
+// Can the ray meet the (padded) box within [tmin, tmax]?  Conservative:
+// slab test with the same slack as box_hit; `id` from inv_dir().
+__device__ __forceinline__ bool ray_box(const DBox& b, d3 o, d3 id, double tmin, double tmax) {
+  const double tx0 = (b.lo[0] - o.x) * id.x, tx1 = (b.hi[0] - o.x) * id.x;
+  const double ty0 = (b.lo[1] - o.y) * id.y, ty1 = (b.hi[1] - o.y) * id.y;
+  const double tz0 = (b.lo[2] - o.z) * id.z, tz1 = (b.hi[2] - o.z) * id.z;
+  const double tn = fmax(fmax(fmin(tx0, tx1), fmin(ty0, ty1)), fmax(fmin(tz0, tz1), tmin));
+  const double tf = fmin(fmin(fmax(tx0, tx1), fmax(ty0, ty1)), fmin(fmax(tz0, tz1), tmax));
+  return tn <= tf + fabs(tf) * KC(1e-9) + KC(1e-12);
+}
 
 struct Cand {
   unsigned long long s, t;  // bit i: sphere i / triangle i may be hit (linear scenes, <= 64 each)
@@ -353,21 +365,29 @@ __device__ __forceinline__ bool closest_hit(const Geo& p, d3 o, d3 d, HitSel& hs
       found = true;
     }
   }
-  for (int i = 0; i < p.nt; ++i) {
-    if (use_m && !((m.t >> i) & 1)) continue;
-    cnt<kCount>(c, C_TRI);
-    const DTri& T = p.tris[i];
-    double t, u, v;
-    if (tri_test(T, o, d, tmin, closest, t, u, v)) {
-      if (t == closest && best_obj > T.obj) continue;
-      closest = t;
-      hs.num = t;
-      hs.u = u;
-      hs.v = v;
-      hs.idx = i;
-      hs.is_tri = 1;
-      best_obj = T.obj;
-      found = true;
+  // triangles cube by cube, in hittable order: a cube whose box the ray
+  // misses within [tmin, closest] cannot hold an accepted hit
+  const d3 id = inv_dir(d);
+  for (int j = 0; j < p.nb; ++j) {
+    const DBox& B = p.boxes[j];
+    if (use_m && !((m.t >> B.first) & 0xFFFull)) continue;
+    if (!ray_box(B, o, id, tmin, closest)) continue;
+    for (int i = B.first; i < B.first + B.count; ++i) {
+      if (use_m && !((m.t >> i) & 1)) continue;
+      cnt<kCount>(c, C_TRI);
+      const DTri& T = p.tris[i];
+      double t, u, v;
+      if (tri_test(T, o, d, tmin, closest, t, u, v)) {
+        if (t == closest && best_obj > T.obj) continue;
+        closest = t;
+        hs.num = t;
+        hs.u = u;
+        hs.v = v;
+        hs.idx = i;
+        hs.is_tri = 1;
+        best_obj = T.obj;
+        found = true;
+      }
     }
   }
   return found;
@@ -412,10 +432,15 @@ __device__ __forceinline__ bool any_hit(const Geo& p, d3 o, d3 d, double tmax, i
     double num;
     if (sphere_query(p.spheres[i], o, d, a, inv_a, tmin, tmax, num)) return true;
   }
-  for (int i = 0; i < p.nt; ++i) {
-    cnt<kCount>(c, C_TRI);
-    double t, u, v;
-    if (tri_test(p.tris[i], o, d, tmin, tmax, t, u, v)) return true;
+  const d3 id = inv_dir(d);
+  for (int j = 0; j < p.nb; ++j) {
+    const DBox& B = p.boxes[j];
+    if (!ray_box(B, o, id, tmin, tmax)) continue;
+    for (int i = B.first; i < B.first + B.count; ++i) {
+      cnt<kCount>(c, C_TRI);
+      double t, u, v;
+      if (tri_test(p.tris[i], o, d, tmin, tmax, t, u, v)) return true;
+    }
   }
   return false;
 }
@@ -469,6 +494,14 @@ template <bool kCount>
 __device__ __forceinline__ bool any_hit_masked(const Geo& p, d3 o, d3 d, double tmax, Cand m, Counters& c) {
   const double a = len2(d);
   const double inv_a = approx_rcp(a);
+  if (m.t) {  // a cube whose box the ray misses cannot be hit: drop its 12 triangles
+    const d3 id = inv_dir(d);
+    for (int j = 0; j < p.nb; ++j) {
+      const DBox& B = p.boxes[j];
+      const unsigned long long g = 0xFFFull << B.first;
+      if ((m.t & g) && !ray_box(B, o, id, 0.001, tmax)) m.t &= ~g;
+    }
+  }
   for (unsigned long long b = m.s; b; b &= b - 1) {
     const int i = __builtin_ctzll(b);
     cnt<kCount>(c, C_SPH);
@@ -677,7 +710,7 @@ template <bool kStage>
 __device__ __forceinline__ Hot hot() {
   KArg k = fresh();
   Hot h;
-  h.g = Geo{k->spheres, k->tris, k->bvh, k->ns, k->nt, k->use_bvh};
+  h.g = Geo{k->spheres, k->tris, k->boxes, k->bvh, k->ns, k->nt, k->use_bvh, k->nb};
   h.mats = k->mats;
   h.lights = k->lights;
   h.jump = k->jump;
@@ -685,6 +718,7 @@ __device__ __forceinline__ Hot hot() {
     const unsigned char* base = reinterpret_cast<const unsigned char*>(k->stage_src);
     h.g.spheres = reinterpret_cast<const DSphere*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->spheres) - base));
     h.g.tris = reinterpret_cast<const DTri*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->tris) - base));
+    h.g.boxes = reinterpret_cast<const DBox*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->boxes) - base));
     h.mats = reinterpret_cast<const DMat*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->mats) - base));
     h.lights = reinterpret_cast<const DLight*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->lights) - base));
     h.jump = reinterpret_cast<const uint64_t*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->jump) - base));

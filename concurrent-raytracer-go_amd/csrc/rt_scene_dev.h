@@ -37,6 +37,18 @@ struct alignas(16) DTri {  // 144 B
   int32_t pad[2];
 };
 
+// Axis-aligned box of one cube's 12 triangles (createCube, scene.go:150-190,
+// builds an axis-aligned box), padded outward by ~1e-9 relative: culling
+// only -- a ray that misses it cannot hit any of its triangles.
+struct alignas(16) DBox {  // 64 B
+  double lo[3];
+  double hi[3];
+  int32_t first;  // first triangle (12 consecutive)
+  int32_t count;
+  int32_t obj;
+  int32_t pad;
+};
+
 // Material kinds: RT_MAT_* of rt_api.h.
 struct alignas(16) DMat {  // 192 B
   int32_t kind;
