@@ -221,6 +221,12 @@ void flatten_scene(const rt_scene& s, FlatScene* fs) {
         b.lo[a] = lo - pad;
         b.hi[a] = hi + pad;
       }
+      double r2 = 0;
+      for (int a = 0; a < 3; ++a) {
+        b.bc[a] = 0.5 * (b.lo[a] + b.hi[a]);
+        r2 += (b.hi[a] - b.bc[a]) * (b.hi[a] - b.bc[a]);
+      }
+      b.br = sqrt(r2) * (1.0 + 1e-12);  // covers the padded box (the kernel adds its own margins)
       fs->boxes.push_back(b);
     }
   }

@@ -481,10 +481,12 @@ __device__ __forceinline__ Cand cone_candidates(const Geo& p, d3 P, d3 N, bool f
     if (self_out && S.obj == self && S.r > 0) continue;
     if (in_cone(S.c, S.r, P, ldir, ldist)) m.s |= 1ull << i;
   }
-  for (int i = 0; i < p.nt; ++i) {
-    const DTri& T = p.tris[i];
-    if (self_out && T.obj == self) continue;
-    if (in_cone(T.bc, T.br, P, ldir, ldist)) m.t |= 1ull << i;
+  // triangles by cube: one cone test against the bounding sphere of the
+  // cube's box admits its 12 triangles (their exact tests follow per ray)
+  for (int j = 0; j < p.nb; ++j) {
+    const DBox& B = p.boxes[j];
+    if (self_out && B.obj == self) continue;
+    if (in_cone(B.bc, B.br, P, ldir, ldist)) m.t |= 0xFFFull << B.first;
   }
   return m;
 }

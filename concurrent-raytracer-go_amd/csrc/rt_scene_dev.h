@@ -40,9 +40,11 @@ struct alignas(16) DTri {  // 144 B
 // Axis-aligned box of one cube's 12 triangles (createCube, scene.go:150-190,
 // builds an axis-aligned box), padded outward by ~1e-9 relative: culling
 // only -- a ray that misses it cannot hit any of its triangles.
-struct alignas(16) DBox {  // 64 B
+struct alignas(16) DBox {  // 96 B
   double lo[3];
   double hi[3];
+  double bc[3];   // bounding sphere of the box (shadow-cone culling)
+  double br;
   int32_t first;  // first triangle (12 consecutive)
   int32_t count;
   int32_t obj;
