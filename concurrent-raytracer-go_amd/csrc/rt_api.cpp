@@ -245,15 +245,10 @@ void flatten_scene(const rt_scene& s, FlatScene* fs) {
 
 // Pixels per work block.  Tiles without geometry: up to
 // kMaxBlockSamples sample ids (the block's hit list lives in LDS), at most
-// 64 pixels.  Tiles with geometry: about 256 samples, so the long paths of
-// one region spread over many workgroups.
+// 64 pixels; tiles with work get smaller blocks (prepare_schedule).
 static int big_block_pixels(int spp) {
   if (spp <= 0) return 64;
   return std::max(1, std::min(64, kMaxBlockSamples / spp));
-}
-static int small_block_pixels(int spp) {
-  if (spp <= 0) return 64;
-  return std::max(1, std::min(big_block_pixels(spp), 256 / spp));
 }
 
 static int validate_scene(const rt_scene* s) {
@@ -322,12 +317,16 @@ struct rt_context {
   unsigned long long* dbg = nullptr;
   // tile dispatch order (schedule.cpp), cached per (scene, W, H, rank, world)
   uint64_t scene_gen = 0;
-  int64_t order_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
-  std::vector<int32_t> order_host;   // local tiles in dispatch order
+  int64_t order_key[12] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+  std::vector<int32_t> order_host;   // local tiles by projected-primitive count (fallback estimate)
   std::vector<int32_t> blocks_host;  // work blocks, 4 ints each (schedule.cpp build_blocks)
   int32_t* d_blocks = nullptr;
   size_t d_blocks_cap = 0;
-  int32_t max_block_pixels = 1;
+  int32_t nsplit = 0;       // split pixels of the current schedule
+  void* d_split = nullptr;  // their per-sample radiance rows + sub-block counters
+  size_t split_cap = 0;
+  void* d_pilot = nullptr;  // pilot render scratch: packed float3 + rgba + per-tile work
+  size_t pilot_cap = 0;     // pixels
   std::vector<unsigned long long> masks_host;  // per local tile primary-ray masks
   unsigned long long* d_masks = nullptr;
   size_t d_masks_cap = 0;
@@ -402,6 +401,8 @@ void rt_context_destroy(rt_context* c) {
   if (c->d_counts) (void)hipFree(c->d_counts);
 
   if (c->d_blocks) (void)hipFree(c->d_blocks);
+  if (c->d_pilot) (void)hipFree(c->d_pilot);
+  if (c->d_split) (void)hipFree(c->d_split);
   if (c->d_masks) (void)hipFree(c->d_masks);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -479,6 +480,141 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   return RT_OK;
 }
 
+// Per (scene, frame, rank, settings) schedule, cached in the context: the
+// tiles' primary-ray candidate masks and the work blocks.  Block sizes and
+// their dispatch order come from a ONE-SAMPLE PILOT render of this rank's
+// tiles (same kernel, same stream keys, output discarded) that reports the
+// path bounces traced per tile: tiles whose samples bounce a lot are cut
+// into blocks of a single pixel and dispatched first, empty-sky tiles into
+// large blocks.  This only partitions and orders the work; every block is
+// rendered by the same code, so the image does not depend on it.
+static size_t split_flags_bytes(int nsplit, int spp) {
+  return (size_t)nsplit * ((spp + 31) / 32) * sizeof(uint32_t) + (size_t)nsplit * sizeof(int32_t);
+}
+
+static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st) {
+  const FlatScene& f = c->flat;
+  const int w = p->W, h = p->H, rank = p->rank, world = p->world;
+  int bigP = big_block_pixels(st->samples);
+  double block_work = 512.0;  // path bounces per block (8 full-wave bounce steps)
+  if (const char* e = getenv("RTGO_BLOCK_WORK")) block_work = std::max(1.0, atof(e));  // experiments only
+  const bool pilot = !getenv("RTGO_NO_PILOT");
+  const int64_t key[12] = {(int64_t)c->scene_gen, w, h, rank, world, st->samples, st->max_depth,
+                           st->recursive_reflections, st->soft_shadows, bigP, (int64_t)(block_work * 16), pilot};
+  if (memcmp(key, c->order_key, sizeof key) != 0) {
+    // primary-ray candidate masks per local tile
+    if (f.bvh.empty() && f.spheres.size() <= 64 && f.tris.size() <= 64) {
+      tile_primary_masks(f, w, h, rank, world, &c->masks_host);
+      if (c->masks_host.size() > c->d_masks_cap) {
+        if (c->d_masks) HIP_TRY(hipFree(c->d_masks));
+        c->d_masks = nullptr;
+        HIP_TRY(hipMalloc((void**)&c->d_masks, c->masks_host.size() * sizeof(unsigned long long)));
+        c->d_masks_cap = c->masks_host.size();
+      }
+      if (!c->masks_host.empty())
+        HIP_TRY(hipMemcpy(c->d_masks, c->masks_host.data(), c->masks_host.size() * sizeof(unsigned long long),
+                          hipMemcpyHostToDevice));
+    } else {
+      c->masks_host.clear();
+    }
+    const int local = rt_tiles_for_rank(w, h, rank, world);
+    // fallback estimate: primitives projected onto the tile
+    std::vector<float> tile_cost;
+    tile_dispatch_order(f, w, h, rank, world, &c->order_host, &tile_cost);
+    // without a pilot: every pixel of a tile with geometry weighs half a block
+    // (2-pixel blocks), tiles ordered by their count
+    std::vector<float> work((size_t)local * 1024, 0.0f);
+    for (int lt = 0; lt < local; ++lt)
+      if (tile_cost[lt] > 0)
+        for (int q = 0; q < 1024; ++q)
+          work[(size_t)lt * 1024 + q] = (float)(block_work / (2.0 * std::max(1, st->samples))) *
+                                        (1.0f + 1e-3f * std::min(tile_cost[lt], 100.0f));
+    auto upload_blocks = [&](const std::vector<int32_t>& b) -> int {
+      if (b.size() > c->d_blocks_cap) {
+        if (c->d_blocks) HIP_TRY(hipFree(c->d_blocks));
+        c->d_blocks = nullptr;
+        HIP_TRY(hipMalloc((void**)&c->d_blocks, b.size() * sizeof(int32_t)));
+        c->d_blocks_cap = b.size();
+      }
+      if (!b.empty()) HIP_TRY(hipMemcpy(c->d_blocks, b.data(), b.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+      return RT_OK;
+    };
+    if (pilot && local > 0 && st->samples > 0 && st->max_depth > 0) {
+      // one sample per pixel, blocks of 64 pixels, packed output into scratch
+      std::vector<int32_t> pb;
+      for (int lt = 0; lt < local; ++lt)
+        for (int p0 = 0; p0 < 1024; p0 += 64) pb.insert(pb.end(), {lt, p0, 64, 0, 1, -1, 1, 0});
+      int rc = upload_blocks(pb);
+      if (rc) return rc;
+      const size_t npx = (size_t)local * 1024;
+      if (npx > c->pilot_cap) {
+        if (c->d_pilot) HIP_TRY(hipFree(c->d_pilot));
+        c->d_pilot = nullptr;
+        HIP_TRY(hipMalloc(&c->d_pilot, npx * 20 + 256));
+        c->pilot_cap = npx;
+      }
+      float* plin = (float*)c->d_pilot;
+      uint8_t* prgba = (uint8_t*)c->d_pilot + npx * 12;
+      unsigned int* plen = (unsigned int*)((uint8_t*)c->d_pilot + npx * 16);
+      KParams q = *p;
+      q.spp = 1;
+      q.blocks = c->d_blocks;
+      q.num_blocks = (int32_t)(pb.size() / 8);
+      q.num_wgs = q.num_blocks;
+      q.layout = RT_LAYOUT_PACKED_TILES;
+      q.out_linear = plin;
+      q.out_rgba = prgba;
+      q.counts = nullptr;
+      q.dbg = nullptr;
+      q.tile_work = plen;
+      q.tile_masks = c->masks_host.empty() ? nullptr : c->d_masks;
+      HIP_TRY(hipMemsetAsync(plen, 0, npx * sizeof(unsigned int), c->stream));
+      const int e = launch_render(q, false, c->stream);
+      if (e != hipSuccess) {
+        set_error(std::string("pilot launch failed: ") + hipGetErrorString((hipError_t)e));
+        return RT_E_DEVICE;
+      }
+      std::vector<unsigned int> len(npx);
+      HIP_TRY(hipMemcpyAsync(len.data(), plen, npx * sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      // a pixel's estimate: the longest pilot path among it and its 4
+      // neighbours (one sample is a noisy estimate of a pixel's mean), plus
+      // a small constant for the camera ray of every sample
+      for (int lt = 0; lt < local; ++lt) {
+        const unsigned int* L = len.data() + (size_t)lt * 1024;
+        for (int q = 0; q < 1024; ++q) {
+          const int x = q & 31, y = q >> 5;
+          unsigned int m = L[q];
+          if (x > 0) m = std::max(m, L[q - 1]);
+          if (x < 31) m = std::max(m, L[q + 1]);
+          if (y > 0) m = std::max(m, L[q - 32]);
+          if (y < 31) m = std::max(m, L[q + 32]);
+          work[(size_t)lt * 1024 + q] = (float)m + 0.02f;
+        }
+      }
+    }
+    c->nsplit = build_blocks(work, st->samples, bigP, block_work, &c->blocks_host);
+    int rc = upload_blocks(c->blocks_host);
+    if (rc) return rc;
+    const size_t need = (size_t)c->nsplit * st->samples * 3 * sizeof(double) + split_flags_bytes(c->nsplit, st->samples);
+    if (need > c->split_cap) {
+      if (c->d_split) HIP_TRY(hipFree(c->d_split));
+      c->d_split = nullptr;
+      HIP_TRY(hipMalloc(&c->d_split, need + 256));
+      c->split_cap = need;
+    }
+    memcpy(c->order_key, key, sizeof key);
+  }
+  p->blocks = c->d_blocks;
+  p->num_blocks = (int32_t)(c->blocks_host.size() / 8);
+  p->split_rad = c->nsplit ? (double*)c->d_split : nullptr;
+  p->split_hits = c->nsplit ? (uint32_t*)((char*)c->d_split + (size_t)c->nsplit * st->samples * 3 * sizeof(double))
+                            : nullptr;
+  p->split_cnt = c->nsplit ? (int32_t*)(p->split_hits + (size_t)c->nsplit * ((st->samples + 31) / 32)) : nullptr;
+  p->tile_masks = (c->masks_host.empty() || getenv("RTGO_NO_FRUSTUM")) ? nullptr : c->d_masks;
+  return RT_OK;
+}
+
 int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settings* st, int32_t rank,
                             int32_t world, int32_t layout, float* d_linear, uint8_t* d_rgba, void* stream,
                             rt_counts* counts) {
@@ -530,62 +666,19 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   p.tiles_x = (w + 31) / 32;
   p.ntiles = rt_num_tiles(w, h);
   p.layout = layout;
-  {  // tile dispatch order (expensive tiles first) and work blocks, uploaded when they change
-    int bigP = big_block_pixels(st->samples), smallP = small_block_pixels(st->samples);
-    if (const char* e = getenv("RTGO_BLOCK_PIXELS")) {  // experiments only: "BIGxSMALL"
-      int b1 = 0, b2 = 0;
-      if (sscanf(e, "%dx%d", &b1, &b2) == 2 && b1 >= 1 && b2 >= 1 && b1 <= 64 && b2 <= 64 &&
-          std::max(b1, b2) * std::max(1, st->samples) <= kMaxBlockSamples) {
-        bigP = b1;
-        smallP = b2;
-      }
-    }
-    const int64_t key[8] = {(int64_t)c->scene_gen, w, h, rank, world, st->samples, bigP, smallP};
-    if (memcmp(key, c->order_key, sizeof key) != 0) {
-      std::vector<float> cost;
-      tile_dispatch_order(f, w, h, rank, world, &c->order_host, &cost);
-      if (getenv("RTGO_NO_TILE_ORDER")) std::sort(c->order_host.begin(), c->order_host.end());
-      build_blocks(c->order_host, cost, st->samples, bigP, smallP, &c->blocks_host);
-      if (f.bvh.empty() && f.spheres.size() <= 64 && f.tris.size() <= 64) {
-        tile_primary_masks(f, w, h, rank, world, &c->masks_host);
-        if (c->masks_host.size() > c->d_masks_cap) {
-          if (c->d_masks) HIP_TRY(hipFree(c->d_masks));
-          c->d_masks = nullptr;
-          HIP_TRY(hipMalloc((void**)&c->d_masks, c->masks_host.size() * sizeof(unsigned long long)));
-          c->d_masks_cap = c->masks_host.size();
-        }
-        if (!c->masks_host.empty())
-          HIP_TRY(hipMemcpy(c->d_masks, c->masks_host.data(), c->masks_host.size() * sizeof(unsigned long long),
-                            hipMemcpyHostToDevice));
-      } else {
-        c->masks_host.clear();
-      }
-      if (c->blocks_host.size() > c->d_blocks_cap) {
-        if (c->d_blocks) HIP_TRY(hipFree(c->d_blocks));
-        c->d_blocks = nullptr;
-        HIP_TRY(hipMalloc((void**)&c->d_blocks, c->blocks_host.size() * sizeof(int32_t)));
-        c->d_blocks_cap = c->blocks_host.size();
-      }
-      if (!c->blocks_host.empty())
-        HIP_TRY(hipMemcpy(c->d_blocks, c->blocks_host.data(), c->blocks_host.size() * sizeof(int32_t),
-                          hipMemcpyHostToDevice));
-      c->max_block_pixels = std::max(bigP, smallP);
-      memcpy(c->order_key, key, sizeof key);
-    }
-    p.blocks = c->d_blocks;
-    p.num_blocks = (int32_t)(c->blocks_host.size() / 4);
-    p.max_block_samples = c->max_block_pixels * st->samples;
-    p.tile_masks = (c->masks_host.empty() || getenv("RTGO_NO_FRUSTUM")) ? nullptr : c->d_masks;
-  }
   {  // LDS staging of the scene prefix + BVH stack placement
     p.stage_src = c->d_scene;
     p.stage_bytes = getenv("RTGO_NO_STAGE") ? 0 : c->stage_bytes;
     p.stack_off = (p.stage_bytes + 15) & ~15;
   }
+  rc = prepare_schedule(c, &p, st);
+  if (rc) return rc;
   p.num_wgs = p.num_blocks;
   // the caller's stream, as given (NULL = the legacy default stream)
   hipStream_t s = (hipStream_t)stream;
   if (counts) HIP_TRY(hipMemsetAsync(c->d_counts, 0, 16 * sizeof(unsigned long long), s));
+  if (c->nsplit)  // split pixels: hit bits and sub-block counters start at zero
+    HIP_TRY(hipMemsetAsync(p.split_hits, 0, split_flags_bytes(c->nsplit, st->samples), s));
   HIP_TRY(hipEventRecord(c->ev0, s));
   int e = launch_render(p, counts != nullptr, s);
   if (e != hipSuccess) {

@@ -35,10 +35,12 @@ void build_sphere_bvh(FlatScene* fs);
 // cost (primitives whose projected bounds overlap the tile), ties by index.
 void tile_dispatch_order(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
                          std::vector<int32_t>* order, std::vector<float>* local_cost);
-// Work blocks in dispatch order: {local tile, first pixel, pixel count, 0}
-// per block, small blocks on tiles with geometry (schedule.cpp).
-void build_blocks(const std::vector<int32_t>& order, const std::vector<float>& local_cost, int spp,
-                  int big_pixels, int small_pixels, std::vector<int32_t>* blocks);
+// Work blocks in dispatch order, 8 ints each (KParams::blocks): sized by
+// estimated work per pixel-sample (pixel_work[lt * 1024 + p]), the heaviest
+// pixels split into sample ranges, most expensive first (schedule.cpp).
+// Returns the number of split pixels.
+int build_blocks(const std::vector<float>& pixel_work, int spp, int big_pixels, double block_work,
+                 std::vector<int32_t>* blocks);
 // Primary-ray candidate masks per local tile (2 x u64: spheres, triangles;
 // scenes with <= 64 of each): bit i set unless primitive i's bounding sphere
 // provably misses the cone of the tile's camera rays.
@@ -66,7 +68,12 @@ struct KParams {
   uint8_t* out_rgba;
   unsigned long long* counts;  // 9 counters (rt_counts order) or null
   unsigned long long* dbg;     // per-WG timing records (RT_WG_TIMING builds only) or null
-  const int32_t* blocks;       // per block: {local tile, first pixel, pixel count, 0}, dispatch order
+  const int32_t* blocks;       // per block, 8 ints: {local tile, first pixel, pixel count, first sample,
+                               //   samples, split slot (-1: none), sub-blocks of the split pixel, 0}
+  double* split_rad;           // split pixels: [slot][spp][3] radiance of the hit samples
+  uint32_t* split_hits;        // split pixels: [slot][(spp+31)/32] hit-sample bits (zeroed per launch)
+  int32_t* split_cnt;          // split pixels: sub-blocks finished (zeroed per launch)
+  unsigned int* tile_work;     // pilot renders (spp 1, 64-pixel blocks): per pixel, its path length (else null)
   const unsigned long long* tile_masks;  // per local tile: primary-ray candidate masks (spheres, tris) or null
   const void* stage_src;       // start of the scene prefix staged into LDS (spheres..lights)
   int32_t stage_bytes;         // bytes to stage (multiple of 16); 0 = read the scene from global memory
@@ -80,7 +87,6 @@ struct KParams {
   int32_t recursive, soft;
   int32_t rank, world;
   int32_t tiles_x, ntiles;
-  int32_t max_block_samples; // largest P * spp of a block (<= kMaxBlockSamples)
   int32_t num_blocks;        // this rank's blocks (one workgroup each)
   int32_t layout;     // RT_LAYOUT_*
   int32_t num_wgs;         // = num_blocks

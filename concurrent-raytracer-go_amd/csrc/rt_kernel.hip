@@ -683,14 +683,22 @@ __device__ __forceinline__ KArg fresh() {
 // dispatch order (tiles sorted by estimated cost) and makes them small on
 // tiles with geometry (schedule.cpp build_blocks).
 struct BlockLoc {
-  int lt, tile, tx, ty, p0, np;  // local tile, global tile, tile coords, first pixel, pixel count
+  int lt, tile, tx, ty;  // local tile, global tile, tile coords
+  int p0, np;            // first pixel (row-major in the tile), pixel count
+  int s0, ns;            // samples [s0, s0+ns) of each pixel (all spp unless split)
+  int slot, nsub;        // split pixel: its radiance slot row and number of sub-blocks (slot < 0: not split)
 };
 __device__ __forceinline__ BlockLoc block_loc(KArg k, int b) {
   BlockLoc r;
-  const int4 e = reinterpret_cast<const int4*>(k->blocks)[b];
+  const int4 e = reinterpret_cast<const int4*>(k->blocks)[2 * b];
+  const int4 f = reinterpret_cast<const int4*>(k->blocks)[2 * b + 1];
   r.lt = e.x;
   r.p0 = e.y;
   r.np = e.z;
+  r.s0 = e.w;
+  r.ns = f.x;
+  r.slot = f.y;
+  r.nsub = f.z;
   r.tile = k->rank + r.lt * k->world;
   r.tx = r.tile % k->tiles_x;
   r.ty = r.tile / k->tiles_x;
@@ -784,7 +792,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   const unsigned long long below = (1ull << lane) - 1ull;
   int* stack = reinterpret_cast<int*>(dyn_lds + pk.stack_off) + lane;
   const BlockLoc blk = block_loc(fresh(), blockIdx.x);
-  const int nwords = (blk.np * pk.spp + 31) >> 5;
+  const int nwords = (blk.np * blk.ns + 31) >> 5;
   if (lane < nwords) hbits[lane] = 0;
   psum[lane][0] = 0;
   psum[lane][1] = 0;
@@ -817,7 +825,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   {
     KArg k = fresh();
     const BlockLoc loc = block_loc(k, blockIdx.x);
-    const int NB = loc.np * k->spp, spp = k->spp;
+    const int NB = loc.np * loc.ns, ns = loc.ns;
     // primary-ray frustum culling (host-computed per tile, schedule.cpp):
     // only primitives whose bounding sphere meets the cone of the tile's
     // camera rays can be hit; every camera ray is still generated and tested
@@ -827,7 +835,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       prim.t = k->tile_masks[2 * loc.lt + 1];
     }
     for (int id = lane; id < NB; id += 64) {
-      const int p = id / spp, s = id - p * spp;
+      const int p = id / ns, s = loc.s0 + id - p * ns;
       const int tp = loc.p0 + p;
       const int x = loc.tx * 32 + (tp & 31), y = loc.ty * 32 + (tp >> 5);
       if (tp >= 1024 || loc.tile >= k->ntiles || x >= k->W || y >= k->H) continue;
@@ -884,8 +892,8 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       if (!alive && e < end) {
         KArg k = fresh();
         const BlockLoc loc = block_loc(k, blockIdx.x);
-        const int id = hlist[e], spp = k->spp;
-        const int p = id / spp, s = id - p * spp;
+        const int id = hlist[e], ns = loc.ns;
+        const int p = id / ns, s = loc.s0 + id - p * ns;
         const int tp = loc.p0 + p;
         Counters nc;  // phase 1 counted this camera ray and its draws
         camera_ray<false>(k, loc.tx * 32 + (tp & 31), loc.ty * 32 + (tp >> 5), s, rng, o, d, nc);
@@ -1060,6 +1068,8 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
         }
       }
       if (fin) {  // the path's radiance goes to its entry's slot
+        if (pk.tile_work)  // pilot render (one sample per pixel): the path's length
+          fresh()->tile_work[blockIdx.x * 64 + hlist[entry]] = depth + 1;
         slot[entry - base][0] = L.x;
         slot[entry - base][1] = L.y;
         slot[entry - base][2] = L.z;
@@ -1068,10 +1078,21 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     }
     __syncthreads();
 
-    // ---- phase 3 (partial): each pixel adds its entries of this round, in order
-    {
+    // ---- phase 3 (partial): each pixel adds its entries of this round, in
+    // order; a split pixel's block stores them in its radiance slot row
+    if (blk.slot >= 0) {
       KArg k = fresh();
-      const int P = blk.np, spp = k->spp;
+      double* row = k->split_rad + (size_t)blk.slot * k->spp * 3;
+      uint32_t* hw = k->split_hits + (size_t)blk.slot * ((k->spp + 31) >> 5);
+      for (int e = base + lane; e < end; e += 64) {
+        const int s = blk.s0 + hlist[e];  // one pixel: id = sample - s0
+        row[3 * s + 0] = slot[e - base][0];
+        row[3 * s + 1] = slot[e - base][1];
+        row[3 * s + 2] = slot[e - base][2];
+        atomicOr(hw + (s >> 5), 1u << (s & 31));
+      }
+    } else {
+      const int P = blk.np, spp = blk.ns;
       if (lane < P) {
         const int a0 = lane * spp, a1 = a0 + spp;
         int e0 = hoff[a0 >> 5] + __popc(hbits[a0 >> 5] & ((1u << (a0 & 31)) - 1u));
@@ -1099,7 +1120,29 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
 
   // ---- phase 3 (final): mean, tone map, one write per pixel
   KArg k = fresh();
-  {
+  bool resolve = true;
+  if (blk.slot >= 0) {
+    // a split pixel: the last of its sub-blocks to finish sums the hit
+    // samples of the slot row in sample order (misses add +0) and writes it
+    __threadfence();
+    int old = 0;
+    if (lane == 0) old = atomicAdd(&k->split_cnt[blk.slot], 1);
+    old = __builtin_amdgcn_readfirstlane(old);
+    resolve = old == blk.nsub - 1;
+    if (resolve) {
+      __threadfence();
+      const double* row = k->split_rad + (size_t)blk.slot * k->spp * 3;
+      const uint32_t* hw = k->split_hits + (size_t)blk.slot * ((k->spp + 31) >> 5);
+      double a = 0;
+      if (lane < 3)
+        for (int s0 = 0; s0 < k->spp; s0 += 32)
+          for (uint32_t b = __atomic_load_n(hw + (s0 >> 5), __ATOMIC_RELAXED); b; b &= b - 1)
+            a += row[3 * (s0 + __builtin_ctz(b)) + lane];
+      if (lane < 3) psum[0][lane] = a;
+      __syncthreads();
+    }
+  }
+  if (resolve) {
     const BlockLoc loc = block_loc(k, blockIdx.x);
     const int p = lane;
     const int tp = loc.p0 + p;

@@ -1,15 +1,21 @@
-// schedule.cpp — dispatch order of a rank's 32x32 tiles.
+// schedule.cpp — how a rank's 32x32 tiles become work blocks.
 //
 // The reference hands tiles to goroutines in row-major order through a
 // channel (createRenderTasks, internal/renderer/renderer.go:398-436); a
 // goroutine that draws a slow tile just keeps it while the others continue.
 // On the GPU a workgroup is dispatched once and runs to completion, so a
-// slow tile dispatched late (long multi-bounce paths between mirrors) runs
-// alone at the end of the launch.  Tiles are therefore dispatched in order
-// of an estimated cost: the number of primitives whose projected bounding
-// sphere overlaps the tile (cheap, host-side, camera model of getRay,
-// renderer.go:377-390).  This only permutes work: every tile is rendered by
-// exactly the same code, so the image does not depend on the order.
+// slow block dispatched late (long multi-bounce paths between mirrors and
+// inside glass) runs alone at the end of the launch.  The host therefore
+//   - estimates each tile's cost from the primitives projected onto it
+//     (tile_dispatch_order) and each tile's primary-ray candidates
+//     (tile_primary_masks),
+//   - and, from a one-sample pilot render (rt_api.cpp prepare_schedule),
+//     each pixel's path length; build_blocks cuts the pixels into blocks of
+//     about equal work, splits the heaviest pixels into sample ranges, and
+//     orders the blocks most expensive first.
+// This only partitions and orders work: every block is rendered by the same
+// code and every pixel's samples are summed in sample order, so the image
+// does not depend on the schedule.
 #include <math.h>
 
 #include <algorithm>
@@ -64,22 +70,53 @@ void tile_dispatch_order(const FlatScene& fs, int32_t W, int32_t H, int32_t rank
   });
 }
 
-void build_blocks(const std::vector<int32_t>& order, const std::vector<float>& local_cost, int spp,
-                  int big_pixels, int small_pixels, std::vector<int32_t>* blocks) {
-  // a tile that no primitive projects onto is cheap per sample (every
-  // camera ray misses): big blocks; a tile with geometry gets small blocks,
-  // so one workgroup never holds more than small_pixels pixels of long paths
-  blocks->clear();
-  for (int32_t lt : order) {
-    const int P = local_cost[lt] > 0 ? small_pixels : big_pixels;
-    for (int p0 = 0; p0 < 1024; p0 += P) {
-      blocks->push_back(lt);
-      blocks->push_back(p0);
-      blocks->push_back(std::min(P, 1024 - p0));
-      blocks->push_back(0);
+int build_blocks(const std::vector<float>& pixel_work, int spp, int big_pixels, double block_work,
+                 std::vector<int32_t>* blocks) {
+  // pixel_work[lt * 1024 + p]: estimated path work per sample of pixel p
+  // (row-major) of local tile lt.  Pixels are taken in row-major order and
+  // grouped into blocks of consecutive pixels while the block's work
+  // spp * sum(work) stays within block_work (at most big_pixels pixels).  A
+  // pixel whose own work exceeds block_work is split into sample ranges of
+  // at most 64 samples (one path per lane), each its own block; the pixel
+  // is resolved by whichever of its blocks finishes last.  Blocks are
+  // dispatched most expensive first, so the longest paths start at once.
+  struct B {
+    double est;
+    int32_t lt, p0, np, s0, ns, slot, nsub;
+  };
+  std::vector<B> v;
+  int nsplit = 0;
+  const double S = std::max(spp, 1);
+  const int local = (int)(pixel_work.size() / 1024);
+  for (int lt = 0; lt < local; ++lt) {
+    const float* w = pixel_work.data() + (size_t)lt * 1024;
+    int p = 0;
+    while (p < 1024) {
+      const double e = S * w[p];
+      if (spp > 1 && e > block_work) {  // split this pixel
+        const int k = (int)std::min((double)((spp + 15) / 16), std::max((double)((spp + 63) / 64), ceil(e / block_work)));
+        const int slot = nsplit++;
+        for (int j = 0; j < k; ++j) {
+          const int s0 = (int)((long long)spp * j / k), s1 = (int)((long long)spp * (j + 1) / k);
+          v.push_back(B{(s1 - s0) * (double)w[p], lt, p, 1, s0, s1 - s0, slot, k});
+        }
+        ++p;
+        continue;
+      }
+      int np = 1;
+      double sum = e;
+      while (p + np < 1024 && np < big_pixels && S * w[p + np] <= block_work && sum + S * w[p + np] <= block_work) {
+        sum += S * w[p + np];
+        ++np;
+      }
+      v.push_back(B{sum, lt, p, np, 0, spp, -1, 1});
+      p += np;
     }
   }
-  (void)spp;
+  std::stable_sort(v.begin(), v.end(), [](const B& a, const B& b) { return a.est > b.est; });
+  blocks->clear();
+  for (const B& b : v) blocks->insert(blocks->end(), {b.lt, b.p0, b.np, b.s0, b.ns, b.slot, b.nsub, 0});
+  return nsplit;
 }
 
 // Does the cone (apex, unit axis, cos/sin of its half-angle) meet the sphere
