@@ -1133,11 +1133,23 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       __threadfence();
       const double* row = k->split_rad + (size_t)blk.slot * k->spp * 3;
       const uint32_t* hw = k->split_hits + (size_t)blk.slot * ((k->spp + 31) >> 5);
+      // chunks of kRound samples: all lanes load (in parallel) into the LDS
+      // slots, misses as +0, then one lane per channel adds them in order
       double a = 0;
-      if (lane < 3)
-        for (int s0 = 0; s0 < k->spp; s0 += 32)
-          for (uint32_t b = __atomic_load_n(hw + (s0 >> 5), __ATOMIC_RELAXED); b; b &= b - 1)
-            a += row[3 * (s0 + __builtin_ctz(b)) + lane];
+      for (int c0 = 0; c0 < k->spp; c0 += kRound) {
+        const int cn = min(kRound, k->spp - c0);
+        for (int i = lane; i < cn; i += 64) {
+          const int s = c0 + i;
+          const bool hit = (hw[s >> 5] >> (s & 31)) & 1u;
+          slot[i][0] = hit ? row[3 * s + 0] : 0.0;
+          slot[i][1] = hit ? row[3 * s + 1] : 0.0;
+          slot[i][2] = hit ? row[3 * s + 2] : 0.0;
+        }
+        __syncthreads();
+        if (lane < 3)
+          for (int i = 0; i < cn; ++i) a += slot[i][lane];
+        __syncthreads();
+      }
       if (lane < 3) psum[0][lane] = a;
       __syncthreads();
     }

@@ -94,7 +94,7 @@ int build_blocks(const std::vector<float>& pixel_work, int spp, int big_pixels, 
     while (p < 1024) {
       const double e = S * w[p];
       if (spp > 1 && e > block_work) {  // split this pixel
-        const int k = (int)std::min((double)((spp + 15) / 16), std::max((double)((spp + 63) / 64), ceil(e / block_work)));
+        const int k = (spp + 63) / 64;  // ranges of <= 64 samples: one path per lane
         const int slot = nsplit++;
         for (int j = 0; j < k; ++j) {
           const int s0 = (int)((long long)spp * j / k), s1 = (int)((long long)spp * (j + 1) / k);
