@@ -834,8 +834,14 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       prim.s = k->tile_masks[2 * loc.lt];
       prim.t = k->tile_masks[2 * loc.lt + 1];
     }
+    // id / ns by a multiply-high with m = floor((2^32 - 1) / ns) + 1: exact
+    // for id, ns < 2^16 (NB <= kMaxBlockSamples); ns == 1 has no 32-bit m
+    const uint32_t mdiv = ns > 1 ? 0xFFFFFFFFu / (uint32_t)ns + 1u : 0u;
+#ifdef RT_VIS_UNROLL
+#pragma unroll RT_VIS_UNROLL
+#endif
     for (int id = lane; id < NB; id += 64) {
-      const int p = id / ns, s = loc.s0 + id - p * ns;
+      const int p = ns > 1 ? (int)__umulhi((uint32_t)id, mdiv) : id, s = loc.s0 + id - p * ns;
       const int tp = loc.p0 + p;
       const int x = loc.tx * 32 + (tp & 31), y = loc.ty * 32 + (tp >> 5);
       if (tp >= 1024 || loc.tile >= k->ntiles || x >= k->W || y >= k->H) continue;
