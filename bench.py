@@ -299,7 +299,7 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": round(achieved_tf / PEAK_FP64_TFLOPS, 5),
                 "traffic": pmc_traffic(workload),
-                "kernel": "rtgo::render_kernel<false,true>",
+                "kernel": "rtgo::render_kernel<false, true, false>",
                 "kernel_ms": round(kernel_s * 1e3, 4),
                 "flops_per_launch": flops,
                 "note": "FP64 VALU-bound branchy path (binary64 like the Go reference; no matrix shape, no MFMA). "

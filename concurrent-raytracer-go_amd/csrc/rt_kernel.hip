@@ -779,7 +779,7 @@ __device__ __forceinline__ void camera_ray(KArg k, int x, int y, int s, rt_rng& 
 //       once (float3 linear + RGBA8).
 constexpr int kRound = 128;  // list entries shaded per round (LDS radiance slots)
 
-template <bool kCount, bool kStage>
+template <bool kCount, bool kStage, bool kPilot>
 __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KParams pk) {
   __shared__ uint32_t hbits[kMaxBlockSamples / 32];  // hit samples of the block
   __shared__ int hoff[kMaxBlockSamples / 32 + 1];    // list offset of each bit word; [words] = #hits
@@ -1074,7 +1074,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
         }
       }
       if (fin) {  // the path's radiance goes to its entry's slot
-        if (pk.tile_work)  // pilot render (one sample per pixel): the path's length
+        if constexpr (kPilot)  // pilot render (one sample per pixel): the path's length
           fresh()->tile_work[blockIdx.x * 64 + hlist[entry]] = depth + 1;
         slot[entry - base][0] = L.x;
         slot[entry - base][1] = L.y;
@@ -1242,14 +1242,21 @@ int launch_render(const KParams& p, bool count, void* stream) {
   if (p.num_wgs <= 0) return hipSuccess;
   const size_t shmem = render_shmem(p);
   const bool stage = p.stage_bytes > 0;
-  if (count && stage)
-    hipLaunchKernelGGL((render_kernel<true, true>), dim3(p.num_wgs), dim3(64), shmem, st, p);
-  else if (count)
-    hipLaunchKernelGGL((render_kernel<true, false>), dim3(p.num_wgs), dim3(64), shmem, st, p);
-  else if (stage)
-    hipLaunchKernelGGL((render_kernel<false, true>), dim3(p.num_wgs), dim3(64), shmem, st, p);
-  else
-    hipLaunchKernelGGL((render_kernel<false, false>), dim3(p.num_wgs), dim3(64), shmem, st, p);
+  const dim3 g(p.num_wgs), b(64);
+  if (p.tile_work) {  // the scheduler's pilot render: its own instantiation (and kernel name)
+    if (stage)
+      hipLaunchKernelGGL((render_kernel<false, true, true>), g, b, shmem, st, p);
+    else
+      hipLaunchKernelGGL((render_kernel<false, false, true>), g, b, shmem, st, p);
+  } else if (count && stage) {
+    hipLaunchKernelGGL((render_kernel<true, true, false>), g, b, shmem, st, p);
+  } else if (count) {
+    hipLaunchKernelGGL((render_kernel<true, false, false>), g, b, shmem, st, p);
+  } else if (stage) {
+    hipLaunchKernelGGL((render_kernel<false, true, false>), g, b, shmem, st, p);
+  } else {
+    hipLaunchKernelGGL((render_kernel<false, false, false>), g, b, shmem, st, p);
+  }
   return (int)hipGetLastError();
 }
 
