@@ -247,8 +247,10 @@ void flatten_scene(const rt_scene& s, FlatScene* fs) {
 // kMaxBlockSamples sample ids (the block's hit list lives in LDS), at most
 // 64 pixels; tiles with work get smaller blocks (prepare_schedule).
 static int big_block_pixels(int spp) {
+  int cap = kMaxBlockSamples;
+  if (const char* e = getenv("RTGO_BLOCK_SAMPLES")) cap = std::max(1, std::min(cap, atoi(e)));  // experiments only
   if (spp <= 0) return 64;
-  return std::max(1, std::min(64, kMaxBlockSamples / spp));
+  return std::max(1, std::min(64, cap / spp));
 }
 
 static int validate_scene(const rt_scene* s) {
@@ -483,11 +485,14 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
 // Per (scene, frame, rank, settings) schedule, cached in the context: the
 // tiles' primary-ray candidate masks and the work blocks.  Block sizes and
 // their dispatch order come from a ONE-SAMPLE PILOT render of this rank's
-// tiles (same kernel, same stream keys, output discarded) that reports the
-// path bounces traced per tile: tiles whose samples bounce a lot are cut
-// into blocks of a single pixel and dispatched first, empty-sky tiles into
-// large blocks.  This only partitions and orders the work; every block is
-// rendered by the same code, so the image does not depend on it.
+// pixels (same kernel, kPilot instantiation, output discarded) that reports
+// each pixel's path length: pixels whose paths bounce a lot go into small
+// blocks (or are split into sample ranges) dispatched first, empty sky into
+// large blocks.  The pilot traces hard shadows only: the soft rays do not
+// change how long a path is, only what a bounce costs, and tracing them
+// would make the pilot's own tail (one 50-bounce path) several times longer.
+// This only partitions and orders the work; every block is rendered by the
+// same code, so the image does not depend on it (tests/test_gpu_schedules.py).
 static size_t split_flags_bytes(int nsplit, int spp) {
   return (size_t)nsplit * ((spp + 31) / 32) * sizeof(uint32_t) + (size_t)nsplit * sizeof(int32_t);
 }
@@ -567,6 +572,7 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st) {
       q.counts = nullptr;
       q.dbg = nullptr;
       q.tile_work = plen;
+      q.soft = 0;  // path lengths only (see above)
       q.tile_masks = c->masks_host.empty() ? nullptr : c->d_masks;
       HIP_TRY(hipMemsetAsync(plen, 0, npx * sizeof(unsigned int), c->stream));
       const int e = launch_render(q, false, c->stream);
