@@ -680,6 +680,7 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   rc = prepare_schedule(c, &p, st);
   if (rc) return rc;
   p.num_wgs = p.num_blocks;
+  if (const char* e = getenv("RTGO_PRIO")) p.prio_blocks = atoi(e);  // experiments only
   // the caller's stream, as given (NULL = the legacy default stream)
   hipStream_t s = (hipStream_t)stream;
   if (counts) HIP_TRY(hipMemsetAsync(c->d_counts, 0, 16 * sizeof(unsigned long long), s));

@@ -90,6 +90,7 @@ struct KParams {
   int32_t num_blocks;        // this rank's blocks (one workgroup each)
   int32_t layout;     // RT_LAYOUT_*
   int32_t num_wgs;         // = num_blocks
+  int32_t prio_blocks;     // blocks [0, prio_blocks) of the dispatch order raise their wave priority
 };
 
 // Enqueue the render kernel; returns hipError_t as int.

@@ -455,17 +455,25 @@ __device__ __forceinline__ bool any_hit(const Geo& p, d3 o, d3 d, double tmax, i
 // their tests; everything else gets the exact Sphere.Hit / Triangle.Hit
 // test, so occlusion results are unchanged.  Margins (~1e-7 relative) are
 // eight orders of magnitude above binary64 rounding.
+//
+// The two square roots are single-precision hardware roots (v_sqrt_f32 of
+// the binary64 value rounded to float: relative error < 2e-7, far inside
+// the 1e-5 relative margins below).  A culling test only has to be
+// conservative, not exact: float overflow gives dc = inf (kept), underflow
+// gives dc = 0 (kept).  No early exits, so the compiler can batch the
+// loads of consecutive spheres.
 __device__ __forceinline__ bool in_cone(const double* cc, double r, d3 P, d3 ldir, double ldist) {
   const d3 v = ld3(cc) - P;
   const double dc2 = len2(v);
-  const double dc = sqrt(dc2);
-  const double ra = fabs(r) * KC(1.0 + 1e-7) + KC(1e-7) * dc + KC(1e-12);  // inflated radius
-  if (dc <= ra) return true;                                       // P inside / on it
-  if (dc - ra > ldist * KC(1.0 + 1e-7) + KC(1e-9)) return false;         // beyond the light
+  const double dc = (double)__builtin_amdgcn_sqrtf((float)dc2);
+  const double ra = fabs(r) * KC(1.0 + 1e-5) + KC(1e-5) * dc + KC(1e-12);  // inflated radius
+  const bool inside = dc <= ra;                                           // P inside / on it
+  const bool beyond = dc - ra > ldist * KC(1.0 + 1e-5) + KC(1e-9);      // beyond the light
   // angle(v, ldir) <= alpha + beta, sin(alpha) = 0.1, sin(beta) = ra/dc:
   // v.ldir >= dc*cos(alpha+beta) = cos(alpha)*sqrt(dc^2-ra^2) - 0.1*ra
-  const double tl = sqrt(fmax(dc2 - ra * ra, 0.0));
-  return dot(v, ldir) >= KC(0.99498) * tl - KC(0.1) * ra - KC(1e-7) * dc;
+  const double tl = (double)__builtin_amdgcn_sqrtf((float)fmax(dc2 - ra * ra, 0.0));
+  const bool meets = dot(v, ldir) >= KC(0.99498) * tl - KC(0.1) * ra - KC(1e-5) * dc;
+  return inside || (!beyond && meets);
 }
 
 // `self` is the hittable that was hit.  When the hit is on its outside
@@ -743,17 +751,42 @@ __device__ __forceinline__ Hot hot() {
 
 // Camera ray of sample s of pixel (x, y): tracePixel's jitter
 // (renderer.go:155-156, the first two draws of the stream) and getRay
-// (renderer.go:377-390).  Leaves `rng` after those two draws.
+// (renderer.go:377-390).  Leaves `rng` after those two draws.  CamK holds
+// the launch-uniform inputs; phase 1 loads it once per block (SGPRs), the
+// shading loop rebuilds it from the kernarg segment where it needs it.
+struct CamK {
+  uint64_t key;
+  uint32_t W;
+  double dW, dH, vw, llcx, llcy, llcz, ox, oy, oz;
+};
+__device__ __forceinline__ CamK cam_k(KArg k) {
+  CamK r;
+  r.key = k->seed_key;
+  r.W = (uint32_t)k->W;
+  r.dW = (double)k->W;
+  r.dH = (double)k->H;
+  // lowerLeftCorner = origin - horizontal/2 - vertical/2 - (0,0,focal)
+  r.vw = 2.0 * k->aspect;
+  r.llcx = k->cam[0] - r.vw / 2;
+  r.llcy = k->cam[1] - 1.0;
+  r.llcz = k->cam[2] - 1.0;
+  r.ox = k->cam[0];
+  r.oy = k->cam[1];
+  r.oz = k->cam[2];
+  return r;
+}
+template <bool kCount>
+__device__ __forceinline__ void camera_ray_c(const CamK& ck, int x, int y, int s, rt_rng& rng, d3& o, d3& d,
+                                             Counters& c) {
+  rt_rng_init(&rng, ck.key, (uint32_t)y * ck.W + (uint32_t)x, (uint32_t)s);
+  const double u = ((double)x + draw<kCount>(rng, c)) / ck.dW;
+  const double v = ((double)y + draw<kCount>(rng, c)) / ck.dH;
+  o = mk(ck.ox, ck.oy, ck.oz);
+  d = mk(((ck.llcx + ck.vw * u) + 0.0) - o.x, ((ck.llcy + 0.0) + 2.0 * v) - o.y, ((ck.llcz + 0.0) + 0.0) - o.z);
+}
 template <bool kCount>
 __device__ __forceinline__ void camera_ray(KArg k, int x, int y, int s, rt_rng& rng, d3& o, d3& d, Counters& c) {
-  rt_rng_init(&rng, k->seed_key, (uint32_t)y * (uint32_t)k->W + (uint32_t)x, (uint32_t)s);
-  const double u = ((double)x + draw<kCount>(rng, c)) / (double)k->W;
-  const double v = ((double)y + draw<kCount>(rng, c)) / (double)k->H;
-  // lowerLeftCorner = origin - horizontal/2 - vertical/2 - (0,0,focal)
-  const double vw = 2.0 * k->aspect;
-  const double llcx = k->cam[0] - vw / 2, llcy = k->cam[1] - 1.0, llcz = k->cam[2] - 1.0;
-  o = mk(k->cam[0], k->cam[1], k->cam[2]);
-  d = mk(((llcx + vw * u) + 0.0) - o.x, ((llcy + 0.0) + 2.0 * v) - o.y, ((llcz + 0.0) + 0.0) - o.z);
+  camera_ray_c<kCount>(cam_k(k), x, y, s, rng, o, d, c);
 }
 
 // Render kernel: one wave (64 lanes) per block, three phases.  A one-wave
@@ -765,19 +798,23 @@ __device__ __forceinline__ void camera_ray(KArg k, int x, int y, int s, rt_rng& 
 //       (renderer.go:170-173) and is finished; a hit sets the sample's bit.
 //       At 800x600x100 97% of the camera rays end here.
 //   2 SHADE - the hit samples, ascending, form a list that the wave drains
-//       in rounds of kRound entries: a lane without a path takes the next
-//       entry, rebuilds its camera ray and runs the path (traceRay,
-//       renderer.go:165-227, unrolled: closest hit, direct lighting with
-//       hard + soft shadows, scatter) to its end, storing the radiance in
-//       the entry's LDS slot.  Shading runs on dense waves instead of on
-//       the ~3% of lanes whose camera ray hit.  Soft shadows of the few
-//       paths left at the end of a round run cooperatively (soft_coop).
-//   3 RESOLVE - after each round every pixel adds its entries' radiance to
-//       its running sum in sample order (misses add +0: the same sum as
-//       tracePixel, renderer.go:150-163, bit for bit); at the end the sum
-//       is divided by spp, tone-mapped (renderer.go:348-367) and written
-//       once (float3 linear + RGBA8).
-constexpr int kRound = 128;  // list entries shaded per round (LDS radiance slots)
+//       through a ring of kRound LDS radiance slots: a lane without a path
+//       takes the next entry, rebuilds its camera ray and runs the path
+//       (traceRay, renderer.go:165-227, unrolled: closest hit, direct
+//       lighting with hard + soft shadows, scatter) to its end, storing the
+//       radiance in the entry's slot.  Shading runs on dense waves instead
+//       of on the ~3% of lanes whose camera ray hit.  Soft shadows of the
+//       few paths still running at the end run cooperatively (soft_coop).
+//   3 RESOLVE - whenever the ring is full, every pixel adds the finished
+//       entries before the earliest running path to its running sum, in
+//       sample order (misses add +0: the same sum as tracePixel,
+//       renderer.go:150-163, bit for bit); at the end the sum is divided by
+//       spp, tone-mapped (renderer.go:348-367) and written once (float3
+//       linear + RGBA8).
+#ifndef RT_ROUND
+#define RT_ROUND 128
+#endif
+constexpr int kRound = RT_ROUND;  // list entries shaded per round (LDS radiance slots)
 
 template <bool kCount, bool kStage, bool kPilot>
 __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KParams pk) {
@@ -792,6 +829,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   const unsigned long long below = (1ull << lane) - 1ull;
   int* stack = reinterpret_cast<int*>(dyn_lds + pk.stack_off) + lane;
   const BlockLoc blk = block_loc(fresh(), blockIdx.x);
+  if ((int)blockIdx.x < fresh()->prio_blocks) __builtin_amdgcn_s_setprio(3);
   const int nwords = (blk.np * blk.ns + 31) >> 5;
   if (lane < nwords) hbits[lane] = 0;
   psum[lane][0] = 0;
@@ -817,12 +855,17 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   unsigned long long dbg_iter = 0;
   // wave-uniform section clocks (s_memtime): hit, lighting, soft; phase 1 (visibility)
   unsigned long long dbg_hit = 0, dbg_light = 0, dbg_soft = 0, dbg_vis = 0;
+  // cone + hard shadow, scatter, lane-iterations alive, coop owners served, soft_seq passes
+  unsigned long long dbg_hard = 0, dbg_scat = 0, dbg_alive = 0, dbg_coop = 0, dbg_seq = 0;
   const unsigned long long tv0 = __builtin_amdgcn_s_memtime();
 #endif
   const Cand all{~0ull, ~0ull};
 
   // ---- phase 1: visibility of the block's camera rays
   {
+    // everything the loop needs is loaded once, before it (wave-uniform:
+    // SGPRs); re-reading the kernarg segment inside the loop put scalar
+    // load round trips on every iteration
     KArg k = fresh();
     const BlockLoc loc = block_loc(k, blockIdx.x);
     const int NB = loc.np * loc.ns, ns = loc.ns;
@@ -834,6 +877,12 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       prim.s = k->tile_masks[2 * loc.lt];
       prim.t = k->tile_masks[2 * loc.lt + 1];
     }
+    const CamK ck = cam_k(k);
+    const int W = k->W, H = k->H;
+    // traceRay's depth cut-off comes first: with max_depth <= 0 every sample is black
+    const bool live = loc.tile < k->ntiles, trace = k->max_depth > 0;
+    const int x0 = loc.tx * 32, y0 = loc.ty * 32, p0 = loc.p0, s0 = loc.s0;
+    const Hot h = hot<kStage>();
     // id / ns by a multiply-high with m = floor((2^32 - 1) / ns) + 1: exact
     // for id, ns < 2^16 (NB <= kMaxBlockSamples); ns == 1 has no 32-bit m
     const uint32_t mdiv = ns > 1 ? 0xFFFFFFFFu / (uint32_t)ns + 1u : 0u;
@@ -841,17 +890,16 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
 #pragma unroll RT_VIS_UNROLL
 #endif
     for (int id = lane; id < NB; id += 64) {
-      const int p = ns > 1 ? (int)__umulhi((uint32_t)id, mdiv) : id, s = loc.s0 + id - p * ns;
-      const int tp = loc.p0 + p;
-      const int x = loc.tx * 32 + (tp & 31), y = loc.ty * 32 + (tp >> 5);
-      if (tp >= 1024 || loc.tile >= k->ntiles || x >= k->W || y >= k->H) continue;
+      const int p = ns > 1 ? (int)__umulhi((uint32_t)id, mdiv) : id, s = s0 + id - p * ns;
+      const int tp = p0 + p;
+      const int x = x0 + (tp & 31), y = y0 + (tp >> 5);
+      if (tp >= 1024 || !live || x >= W || y >= H) continue;
       cnt<kCount>(c, C_CAM);
       rt_rng rng;
       d3 o, d;
-      camera_ray<kCount>(k, x, y, s, rng, o, d, c);
-      if (k->max_depth <= 0) continue;  // traceRay's depth cut-off first: black
+      camera_ray_c<kCount>(ck, x, y, s, rng, o, d, c);
+      if (!trace) continue;
       cnt<kCount>(c, C_BOUNCE);
-      const Hot h = hot<kStage>();
       // hit or miss is all this phase needs: an any-hit query over
       // [0.001, +inf) decides exactly what hitWorld's closest hit would
       const bool hit = h.masks ? any_hit_masked<kCount>(h.g, o, d, __builtin_inf(), prim, c)
@@ -882,20 +930,88 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   dbg_vis = __builtin_amdgcn_s_memtime() - tv0;
 #endif
 
-  for (int base = 0; base < nh; base += kRound) {
-    const int end = min(nh, base + kRound);
-    int next = base;  // wave-uniform: next entry of this round to start
-
-    // ---- phase 2: shade the round's entries
+  // ---- phases 2 + 3: shade the hit list through a RING of kRound radiance
+  // slots (entry e -> slot e % kRound).  Paths finish out of order; the
+  // per-pixel sums are taken in entry order (= sample order) by
+  // resolve_entries once every entry before the earliest path still running
+  // has finished.  A long path therefore holds only its own slot: the other
+  // lanes keep taking entries until the ring is full (a barrier per batch of
+  // kRound entries made every batch wait for its longest path).
+  static_assert((kRound & (kRound - 1)) == 0, "kRound must be a power of two");
+  // adds entries [a, b) (all finished) to their pixels' sums in order; a
+  // split pixel's block stores them in its radiance slot row instead
+  auto resolve_entries = [&](int a, int b) {
+    // the lane id laundered through a volatile move: keeps this rarely run
+    // code's lane-dependent addresses from being hoisted out of the shading
+    // loop (they would occupy registers, or scratch, for the whole loop)
+    int lane;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"((int)threadIdx.x));
+    if (blk.slot >= 0) {
+      KArg k = fresh();
+      double* row = k->split_rad + (size_t)blk.slot * k->spp * 3;
+      uint32_t* hw = k->split_hits + (size_t)blk.slot * ((k->spp + 31) >> 5);
+      for (int e = a + lane; e < b; e += 64) {
+        const int s = blk.s0 + hlist[e];  // one pixel: id = sample - s0
+        const int q = e & (kRound - 1);
+        row[3 * s + 0] = slot[q][0];
+        row[3 * s + 1] = slot[q][1];
+        row[3 * s + 2] = slot[q][2];
+        atomicOr(hw + (s >> 5), 1u << (s & 31));
+      }
+    } else {
+      const int P = blk.np, spp = blk.ns;
+      if (lane < P) {
+        const int a0 = lane * spp, a1 = a0 + spp;
+        int e0 = hoff[a0 >> 5] + __popc(hbits[a0 >> 5] & ((1u << (a0 & 31)) - 1u));
+        int e1 = (a1 >> 5) < nwords ? hoff[a1 >> 5] + __popc(hbits[a1 >> 5] & ((1u << (a1 & 31)) - 1u)) : nh;
+        e0 = max(e0, a);
+        e1 = min(e1, b);
+        if (e0 < e1) {
+          double ax = psum[lane][0], ay = psum[lane][1], az = psum[lane][2];
+          for (int e = e0; e < e1; ++e) {
+            const int q = e & (kRound - 1);
+            ax += slot[q][0];
+            ay += slot[q][1];
+            az += slot[q][2];
+          }
+          psum[lane][0] = ax;
+          psum[lane][1] = ay;
+          psum[lane][2] = az;
+        }
+      }
+    }
+  };
+  if (nh > 0) {
     d3 o = mk(0, 0, 0), d = mk(0, 0, 0), T = mk(1, 1, 1), L = mk(0, 0, 0);
     rt_rng rng{0};
     int depth = 0, entry = 0;
     bool alive = false;
+    int next = 0, resolved = 0;  // wave-uniform: next entry to start; entries [0, resolved) summed
     for (;;) {
-      // lanes without a path take the next entries, in lane order
       const unsigned long long freem = __ballot(!alive);
+      int limit = min(nh, resolved + kRound);
+      if (freem != 0 && next == limit && next < nh) {
+        // the ring is full and lanes are idle: sum every entry before the
+        // earliest one still running (a wave-wide min over the live lanes)
+        // (swizzles within each half-wave, then the two halves' lane 0)
+        int lo = alive ? entry : next;
+        lo = min(lo, __builtin_amdgcn_ds_swizzle(lo, 0x1F | (16 << 10)));
+        lo = min(lo, __builtin_amdgcn_ds_swizzle(lo, 0x1F | (8 << 10)));
+        lo = min(lo, __builtin_amdgcn_ds_swizzle(lo, 0x1F | (4 << 10)));
+        lo = min(lo, __builtin_amdgcn_ds_swizzle(lo, 0x1F | (2 << 10)));
+        lo = min(lo, __builtin_amdgcn_ds_swizzle(lo, 0x1F | (1 << 10)));
+        lo = min(__builtin_amdgcn_readlane(lo, 0), __builtin_amdgcn_readlane(lo, 32));
+        if (lo > resolved) {
+          __syncthreads();
+          resolve_entries(resolved, lo);
+          __syncthreads();
+          resolved = lo;
+          limit = min(nh, resolved + kRound);
+        }
+      }
+      // lanes without a path take the next entries, in lane order
       const int e = next + __popcll(freem & below);
-      if (!alive && e < end) {
+      if (!alive && e < limit) {
         KArg k = fresh();
         const BlockLoc loc = block_loc(k, blockIdx.x);
         const int id = hlist[e], ns = loc.ns;
@@ -909,10 +1025,16 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
         entry = e;
         alive = true;
       }
-      next = min(end, next + __popcll(freem));
-      if (__ballot(alive) == 0) break;  // wave-uniform: round drained
+      next = min(limit, next + __popcll(freem));
+      if (__ballot(alive) == 0) {  // wave-uniform
+        if (next >= nh) break;     // every entry done
+        continue;                  // ring full of finished entries: resolve, then refill
+      }
 #ifdef RT_WG_TIMING
       ++dbg_iter;
+      dbg_alive += __popcll(__ballot(alive));
+      if (dbg_iter % 4 == 0 && dbg_iter / 4 < 16 && lane == 0 && fresh()->dbg)
+        fresh()->dbg[(size_t)blockIdx.x * 32 + 16 + dbg_iter / 4] = __builtin_amdgcn_s_memrealtime();
       const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -981,6 +1103,9 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
           double ldist = 0;
           Cand cm{0ull, 0ull};
           bool lit = false, occl = false;
+#ifdef RT_WG_TIMING
+          const unsigned long long th0 = __builtin_amdgcn_s_memtime();
+#endif
           if (shade) {
             d3 lv = ld3(Lt.pos) - P;
             ldist = sqrt(lv.x * lv.x + lv.y * lv.y + lv.z * lv.z);
@@ -993,6 +1118,9 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
               occl = shadow_blocked<kCount>(gg, masks, P, ldir, ldist, cm, stack, c);  // hard shadow ray
             }
           }
+#ifdef RT_WG_TIMING
+          dbg_hard += __builtin_amdgcn_s_memtime() - th0;
+#endif
           const bool need_soft = lit && !occl && soft;
           // The 16 soft rays' draws are always consumed, but their result
           // only scales terms multiplied by cos = Max(0, N.L): when that is
@@ -1013,6 +1141,9 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
           const unsigned long long ts2 = __builtin_amdgcn_s_memtime();
 #endif
           if (owners != 0) {
+#ifdef RT_WG_TIMING
+            if (__popcll(owners) <= RT_COOP_MAX) dbg_coop += __popcll(owners); else ++dbg_seq;
+#endif
             if (__popcll(owners) <= RT_COOP_MAX) {
               for (unsigned long long b = owners; b; b &= b - 1) {
                 const int ow = __builtin_ctzll(b);
@@ -1055,6 +1186,9 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
         dbg_light += __builtin_amdgcn_s_memtime() - ts1;
 #endif
         // (3) Material.Scatter and the traceRay combination (renderer.go:181-226)
+#ifdef RT_WG_TIMING
+        const unsigned long long tc0 = __builtin_amdgcn_s_memtime();
+#endif
         if (shade) {
           d3 E = ld3(m->emit);
           const Scat sc = scatter<kCount>(m, d, N, front, rng, c);
@@ -1072,52 +1206,22 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
             }
           }
         }
+#ifdef RT_WG_TIMING
+        dbg_scat += __builtin_amdgcn_s_memtime() - tc0;
+#endif
       }
-      if (fin) {  // the path's radiance goes to its entry's slot
+      if (fin) {  // the path's radiance goes to its entry's ring slot
         if constexpr (kPilot)  // pilot render (one sample per pixel): the path's length
           fresh()->tile_work[blockIdx.x * 64 + hlist[entry]] = depth + 1;
-        slot[entry - base][0] = L.x;
-        slot[entry - base][1] = L.y;
-        slot[entry - base][2] = L.z;
+        const int q = entry & (kRound - 1);
+        slot[q][0] = L.x;
+        slot[q][1] = L.y;
+        slot[q][2] = L.z;
         alive = false;
       }
     }
     __syncthreads();
-
-    // ---- phase 3 (partial): each pixel adds its entries of this round, in
-    // order; a split pixel's block stores them in its radiance slot row
-    if (blk.slot >= 0) {
-      KArg k = fresh();
-      double* row = k->split_rad + (size_t)blk.slot * k->spp * 3;
-      uint32_t* hw = k->split_hits + (size_t)blk.slot * ((k->spp + 31) >> 5);
-      for (int e = base + lane; e < end; e += 64) {
-        const int s = blk.s0 + hlist[e];  // one pixel: id = sample - s0
-        row[3 * s + 0] = slot[e - base][0];
-        row[3 * s + 1] = slot[e - base][1];
-        row[3 * s + 2] = slot[e - base][2];
-        atomicOr(hw + (s >> 5), 1u << (s & 31));
-      }
-    } else {
-      const int P = blk.np, spp = blk.ns;
-      if (lane < P) {
-        const int a0 = lane * spp, a1 = a0 + spp;
-        int e0 = hoff[a0 >> 5] + __popc(hbits[a0 >> 5] & ((1u << (a0 & 31)) - 1u));
-        int e1 = (a1 >> 5) < nwords ? hoff[a1 >> 5] + __popc(hbits[a1 >> 5] & ((1u << (a1 & 31)) - 1u)) : nh;
-        e0 = max(e0, base);
-        e1 = min(e1, end);
-        if (e0 < e1) {
-          double ax = psum[lane][0], ay = psum[lane][1], az = psum[lane][2];
-          for (int e = e0; e < e1; ++e) {
-            ax += slot[e - base][0];
-            ay += slot[e - base][1];
-            az += slot[e - base][2];
-          }
-          psum[lane][0] = ax;
-          psum[lane][1] = ay;
-          psum[lane][2] = az;
-        }
-      }
-    }
+    resolve_entries(resolved, nh);
     __syncthreads();
   }
 #ifdef RT_WG_TIMING
@@ -1196,7 +1300,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   }
 #ifdef RT_WG_TIMING
   if (k->dbg && lane == 0) {
-    unsigned long long* r = k->dbg + (size_t)blockIdx.x * 8;
+    unsigned long long* r = k->dbg + (size_t)blockIdx.x * 32;
     r[0] = t_start;
     r[1] = t_loop;
     r[2] = __builtin_amdgcn_s_memrealtime();
@@ -1205,6 +1309,13 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     r[5] = dbg_soft;
     r[6] = dbg_vis;
     r[7] = dbg_iter;
+    r[8] = dbg_hard;
+    r[9] = dbg_scat;
+    r[10] = dbg_alive;
+    r[11] = dbg_coop;
+    r[12] = dbg_seq;
+    r[13] = (unsigned long long)blk.np * 65536ull + (unsigned long long)blk.ns;
+    r[14] = (unsigned long long)(blk.slot + 1);
   }
 #endif
 }

@@ -39,7 +39,7 @@ for _ in range(2):
     torch.cuda.synchronize()
 print(f"kernel {e0.elapsed_time(e1):.3f} ms (rank {RANK}/{WORLD}, depth {st.max_depth})")
 WPG = int(os.environ.get("WG_WAVES", "1"))  # waves per workgroup of the kernel
-d = dbg.cpu().numpy().reshape(-1, WPG, 8)
+d = dbg.cpu().numpy().reshape(-1, WPG, 32)
 used = d[:, 0, 0] != 0
 d = d[used]
 nwg = d.shape[0]
@@ -69,9 +69,24 @@ print(f"  section clocks: fill {fill.sum() / tot:.1%}  hit {hit.sum() / tot:.1%}
       f"{hit.sum() / max(it.sum(), 1):.0f} light {light.sum() / max(it.sum(), 1):.0f}")
 wave_clk = (end - start) * 2100.0  # us -> shader clocks at ~2.1 GHz
 print(f"  accounted / wave time: {tot / wave_clk.sum():.1%}")
-for i in order[:3]:
+hard, scat, alive, coop, seq = (d[:, :, k].astype(np.float64) for k in (8, 9, 10, 11, 12))
+print(f"  lighting split: cone+hard {hard.sum() / tot:.1%}  soft {soft.sum() / tot:.1%}  rest "
+      f"{(light.sum() - hard.sum() - soft.sum()) / tot:.1%};  scatter {scat.sum() / tot:.1%}")
+print(f"  lanes alive per shade iteration {alive.sum() / max(it.sum(), 1):.1f}; coop owners {coop.sum():.0f}, "
+      f"soft_seq passes {seq.sum():.0f}")
+for i in order[:6]:
     for w in range(WPG):
-        print(f"    WG {int(i)} wave {w}: shade iters {int(it[i, w])}, clocks fill {int(fill[i, w])} hit {int(hit[i, w])} "
-              f"light {int(light[i, w])} soft {int(soft[i, w])}; wave us {end[i, w] - start[i, w]:.0f}")
+        npx, ns = int(d[i, w, 13]) >> 16, int(d[i, w, 13]) & 0xFFFF
+        print(f"    WG {int(i)}: np {npx} ns {ns} split {int(d[i, w, 14]) - 1}; iters {int(it[i, w])}, alive/iter "
+              f"{alive[i, w] / max(it[i, w], 1):.1f}; clocks fill {int(fill[i, w])} hit {int(hit[i, w])} "
+              f"hard {int(hard[i, w])} soft {int(soft[i, w])} light-rest {int(light[i, w] - hard[i, w] - soft[i, w])} "
+              f"scat {int(scat[i, w])}; coop {int(coop[i, w])} seq {int(seq[i, w])}; wave us {end[i, w] - start[i, w]:.0f}"
+              f" start {start[i, w]:.0f}")
+for i in order[:4]:
+    ts = [(int(v) - t0) / 100.0 for v in d[i, 0, 17:32] if v != 0]
+    print(f"    WG {int(i)} time at every 4th shade iteration (us):", [round(t, 1) for t in ts])
+late = end.max(axis=1) > 0.7 * span
+print(f"  WGs ending after 70% of the span: {int(late.sum())}; of them split {int((d[late, 0, 14] > 0).sum())}, "
+      f"mean iters {it[late].mean():.0f}, mean start {start[late].mean():.0f} us")
 busy = dur.sum()
 print(f"  mean waves in flight {busy / span:.1f}")
