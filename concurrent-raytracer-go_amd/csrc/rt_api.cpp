@@ -282,7 +282,8 @@ static int validate_settings(const rt_settings* st, int32_t w, int32_t h) {
     set_error("settings is NULL");
     return RT_E_INVALID;
   }
-  if (w <= 0 || h <= 0 || (long long)w * h > (1LL << 31) / 4) {
+  // (each side at most 65536: the kernel's camera-jitter division relies on it)
+  if (w <= 0 || h <= 0 || w > 65536 || h > 65536 || (long long)w * h > (1LL << 31) / 4) {
     set_error("invalid image size " + std::to_string(w) + "x" + std::to_string(h));
     return RT_E_INVALID;
   }
@@ -476,7 +477,11 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   c->d_bvh = (const DBVHNode*)(base + off_b);
   c->d_jump = (const uint64_t*)(base + off_j);
   // small linear-scan scenes are staged into LDS by every workgroup
-  c->stage_bytes = (f.bvh.empty() && off_b <= 48 * 1024) ? (int32_t)off_b : 0;
+  // (the PCG jump table stays in global memory unless RTGO_STAGE_JUMP is set: only
+  // the cooperative soft-shadow form reads it, and its 3 KB of LDS per workgroup
+  // cost more occupancy than the L1-cached reads cost time)
+  const size_t stage_end = getenv("RTGO_STAGE_JUMP") ? off_b : off_j;
+  c->stage_bytes = (f.bvh.empty() && stage_end <= 48 * 1024) ? (int32_t)stage_end : 0;
   c->have_scene = true;
   c->scene_gen += 1;
   return RT_OK;

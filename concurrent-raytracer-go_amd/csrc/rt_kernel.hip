@@ -38,6 +38,15 @@
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 3  // measured best of 2/3/4 (4 spills the FP64 path state)
 #endif
+// sphere scans of closest_hit and cone_candidates: unroll factor (a lone
+// wave at the end of a launch waits on each sphere's LDS loads otherwise)
+#ifdef RT_SPH_UNROLL
+#define RT_PRAGMA(x) _Pragma(#x)
+#define RT_SPH_LOOP_(n) RT_PRAGMA(unroll n)
+#define RT_SPH_LOOP RT_SPH_LOOP_(RT_SPH_UNROLL)
+#else
+#define RT_SPH_LOOP
+#endif
 #ifndef RT_COOP_MAX
 #define RT_COOP_MAX 8  // cooperative soft shadows when at most this many lanes need them
 #endif
@@ -427,6 +436,7 @@ __device__ __forceinline__ bool any_hit(const Geo& p, d3 o, d3 d, double tmax, i
     }
     return false;
   }
+  RT_SPH_LOOP
   for (int i = 0; i < p.ns; ++i) {
     cnt<kCount>(c, C_SPH);
     double num;
@@ -484,6 +494,7 @@ __device__ __forceinline__ Cand cone_candidates(const Geo& p, d3 P, d3 N, bool f
                                                 double ldist) {
   const bool self_out = front && dot(N, ldir) >= KC(0.1015);
   Cand m{0ull, 0ull};
+  RT_SPH_LOOP
   for (int i = 0; i < p.ns; ++i) {
     const DSphere& S = p.spheres[i];
     if (self_out && S.obj == self && S.r > 0) continue;
@@ -502,8 +513,6 @@ __device__ __forceinline__ Cand cone_candidates(const Geo& p, d3 P, d3 N, bool f
 // hitWorld(shadowRay, 0.001, dist) restricted to the candidates.
 template <bool kCount>
 __device__ __forceinline__ bool any_hit_masked(const Geo& p, d3 o, d3 d, double tmax, Cand m, Counters& c) {
-  const double a = len2(d);
-  const double inv_a = approx_rcp(a);
   if (m.t) {  // a cube whose box the ray misses cannot be hit: drop its 12 triangles
     const d3 id = inv_dir(d);
     for (int j = 0; j < p.nb; ++j) {
@@ -512,11 +521,15 @@ __device__ __forceinline__ bool any_hit_masked(const Geo& p, d3 o, d3 d, double 
       if ((m.t & g) && !ray_box(B, o, id, 0.001, tmax)) m.t &= ~g;
     }
   }
-  for (unsigned long long b = m.s; b; b &= b - 1) {
-    const int i = __builtin_ctzll(b);
-    cnt<kCount>(c, C_SPH);
-    double num;
-    if (sphere_query(p.spheres[i], o, d, a, inv_a, 0.001, tmax, num)) return true;
+  if (m.s) {  // (most camera rays have no candidate at all)
+    const double a = len2(d);
+    const double inv_a = approx_rcp(a);
+    for (unsigned long long b = m.s; b; b &= b - 1) {
+      const int i = __builtin_ctzll(b);
+      cnt<kCount>(c, C_SPH);
+      double num;
+      if (sphere_query(p.spheres[i], o, d, a, inv_a, 0.001, tmax, num)) return true;
+    }
   }
   for (unsigned long long b = m.t; b; b &= b - 1) {
     const int i = __builtin_ctzll(b);
@@ -603,6 +616,72 @@ RT_COOP_FN CoopOut soft_coop(const Geo p, bool masks, bool trace, d3 P, d3 ldir,
     x = jump[2 * (3 * used)] * x + jump[2 * (3 * used) + 1];
   }
   return CoopOut{x, unocc, tries};
+}
+
+// Queue form for many owners (more than RT_COOP_MAX lanes need soft
+// shadows for this light), executed by the whole converged wave.  Each
+// owner runs its own rejection tries on its own stream, in order (the same
+// draws as 16 calls of RandomVec3InUnitSphere); an accepted point is
+// appended to an LDS queue as its three raw 32-bit draws and the owner's
+// lane.  Whenever 64 points are queued, every lane takes one, rebuilds the
+// point from the raw draws, reads the owner's hit point, light direction,
+// distance and candidates across lanes, and traces the jittered ray.  The
+// sequential form traced a ray in nearly every try step at about half the
+// lanes; here the tries run alone and the rays run on full waves.  The
+// result is a count of unoccluded rays, so the order in which rays are
+// traced does not change it.  Returns the owner's count (0 elsewhere).
+template <bool kCount>
+__device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_soft, bool trace, d3 P, d3 ldir,
+                                          double ldist, Cand cm, rt_rng& rng, int* stack, Counters& c) {
+  __shared__ uint4 sq[128];   // queued points: raw draws x, y, z, owner lane (a ring)
+  __shared__ int sq_unocc[64];  // per owner: unoccluded rays
+  const int lane = (int)(threadIdx.x & 63);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  sq_unocc[lane] = 0;
+  int need = need_soft ? 16 : 0, free_rays = 0;  // free_rays: points of an owner with nothing to trace
+  int head = 0, tail = 0;  // wave-uniform ring positions
+  for (;;) {
+    bool acc = false;
+    uint32_t ux = 0, uy = 0, uz = 0;
+    if (need > 0) {
+      ux = rt_rng_next(&rng);
+      uy = rt_rng_next(&rng);
+      uz = rt_rng_next(&rng);
+      cnt<kCount>(c, C_RNG, 3);
+      const d3 pt = mk(rt_bits_to_unit(ux) * 2 - 1, rt_bits_to_unit(uy) * 2 - 1, rt_bits_to_unit(uz) * 2 - 1);
+      if (len2(pt) < 1) {
+        --need;
+        cnt<kCount>(c, C_SHADOW);
+        if (trace) acc = true;  // only rays that can be blocked are queued
+        else ++free_rays;
+      }
+    }
+    const unsigned long long am = __ballot(acc);
+    if (acc) sq[(tail + __popcll(am & below)) & 127] = make_uint4(ux, uy, uz, (uint32_t)lane);
+    tail += __popcll(am);
+    const bool more = __ballot(need > 0) != 0;
+    if (tail - head >= 64 || (!more && tail > head)) {
+      __syncthreads();
+      const int n = min(64, tail - head);
+      const uint4 e = sq[(head + lane) & 127];
+      const int ow = lane < n ? (int)e.w : lane;
+      // the owner's ray inputs, read across lanes (every lane takes part)
+      const d3 Po = mk(__shfl(P.x, ow), __shfl(P.y, ow), __shfl(P.z, ow));
+      const d3 Lo = mk(__shfl(ldir.x, ow), __shfl(ldir.y, ow), __shfl(ldir.z, ow));
+      const double dist = __shfl(ldist, ow);
+      const Cand co{__shfl(cm.s, ow), __shfl(cm.t, ow)};
+      if (lane < n) {
+        const d3 pt = mk(rt_bits_to_unit(e.x) * 2 - 1, rt_bits_to_unit(e.y) * 2 - 1, rt_bits_to_unit(e.z) * 2 - 1);
+        if (!shadow_blocked<kCount>(p, masks, Po, normalize(Lo + muls(pt, 0.1)), dist, co, stack, c))
+          atomicAdd(&sq_unocc[ow], 1);
+      }
+      head += n;
+      __syncthreads();
+    }
+    if (!more && head == tail) break;
+  }
+  __syncthreads();
+  return need_soft ? sq_unocc[lane] + free_rays : 0;
 }
 
 // ------------------------------------------------------------ scatter
@@ -739,7 +818,8 @@ __device__ __forceinline__ Hot hot() {
     h.g.boxes = reinterpret_cast<const DBox*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->boxes) - base));
     h.mats = reinterpret_cast<const DMat*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->mats) - base));
     h.lights = reinterpret_cast<const DLight*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->lights) - base));
-    h.jump = reinterpret_cast<const uint64_t*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->jump) - base));
+    const long jo = reinterpret_cast<const unsigned char*>(k->jump) - base;
+    if (jo < k->stage_bytes) h.jump = reinterpret_cast<const uint64_t*>(dyn_lds + jo);
   }
   h.nl = k->nl;
   h.max_depth = k->max_depth;
@@ -758,13 +838,35 @@ struct CamK {
   uint64_t key;
   uint32_t W;
   double dW, dH, vw, llcx, llcy, llcz, ox, oy, oz;
+  double rW, rH;  // refined reciprocals of dW, dH (div_by)
 };
+// The compiler's binary64 division n / d is v_div_scale (n and d), v_rcp_f64,
+// two Newton steps on the reciprocal, q = n*r, the residual fma, v_div_fmas
+// and v_div_fixup.  For the camera jitter n = x + rand is in [0, W) with
+// rand a multiple of 2^-32 (so n is 0 or at least 2^-32) and d = W or H is
+// an integer in [1, 2^16]: v_div_scale scales nothing, v_div_fmas is a plain
+// fma and v_div_fixup returns its input, so the sequence is the three
+// operations below with the reciprocal refinement done once per block, and
+// the quotient is the IEEE one bit for bit (validate_settings bounds W, H).
+__device__ __forceinline__ double refined_rcp(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+__device__ __forceinline__ double div_by(double n, double d, double r) {
+  const double q = n * r;
+  return __builtin_fma(__builtin_fma(-d, q, n), r, q);
+}
 __device__ __forceinline__ CamK cam_k(KArg k) {
   CamK r;
   r.key = k->seed_key;
   r.W = (uint32_t)k->W;
   r.dW = (double)k->W;
   r.dH = (double)k->H;
+  r.rW = refined_rcp(r.dW);
+  r.rH = refined_rcp(r.dH);
   // lowerLeftCorner = origin - horizontal/2 - vertical/2 - (0,0,focal)
   r.vw = 2.0 * k->aspect;
   r.llcx = k->cam[0] - r.vw / 2;
@@ -779,8 +881,8 @@ template <bool kCount>
 __device__ __forceinline__ void camera_ray_c(const CamK& ck, int x, int y, int s, rt_rng& rng, d3& o, d3& d,
                                              Counters& c) {
   rt_rng_init(&rng, ck.key, (uint32_t)y * ck.W + (uint32_t)x, (uint32_t)s);
-  const double u = ((double)x + draw<kCount>(rng, c)) / ck.dW;
-  const double v = ((double)y + draw<kCount>(rng, c)) / ck.dH;
+  const double u = div_by((double)x + draw<kCount>(rng, c), ck.dW, ck.rW);
+  const double v = div_by((double)y + draw<kCount>(rng, c), ck.dH, ck.rH);
   o = mk(ck.ox, ck.oy, ck.oz);
   d = mk(((ck.llcx + ck.vw * u) + 0.0) - o.x, ((ck.llcy + 0.0) + 2.0 * v) - o.y, ((ck.llcz + 0.0) + 0.0) - o.z);
 }
@@ -823,7 +925,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   __shared__ uint16_t hlist[kMaxBlockSamples];       // hit sample ids, ascending
   __shared__ double slot[kRound][3];                 // radiance of the round's entries
   __shared__ double psum[64][3];                     // per pixel: running sum over samples
-  // dynamic LDS (dyn_lds): [staged scene + PCG jump table (kStage)][BVH stack (kStack x 64 ints)]
+  // dynamic LDS (dyn_lds): [staged scene prefix (kStage)][BVH stack (kStack x 64 ints)]
 
   const int lane = threadIdx.x;
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -836,8 +938,8 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   psum[lane][1] = 0;
   psum[lane][2] = 0;
   if constexpr (kStage) {
-    // LDS-staged scene primitives: spheres | triangles | materials | lights |
-    // jump table (one contiguous prefix of the device scene buffer), so the
+    // LDS-staged scene primitives: spheres | triangles | boxes | materials |
+    // lights [| jump table] (one contiguous prefix of the device scene buffer), so the
     // divergent per-lane reads of the shadow / scatter code hit LDS instead
     // of L1/L2 (measured: 55% of wave time in memory waits without it)
     const uint4* __restrict__ src = reinterpret_cast<const uint4*>(pk.stage_src);
@@ -1157,8 +1259,17 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
                   cnt<kCount>(c, C_RNG, 3ull * r.tries);
                 }
               }
-            } else if (need_soft) {
-              unocc = soft_seq<kCount>(gg, masks, trace, P, ldir, ldist, cm, rng, stack, c);
+            } else {
+#if defined(RT_SOFT_SEQ)
+              if (need_soft) unocc = soft_seq<kCount>(gg, masks, trace, P, ldir, ldist, cm, rng, stack, c);
+#elif defined(RT_QUEUE_MIN)
+              if (__popcll(owners) > RT_QUEUE_MIN)
+                unocc = soft_queue<kCount>(gg, masks, need_soft, trace, P, ldir, ldist, cm, rng, stack, c);
+              else if (need_soft)
+                unocc = soft_seq<kCount>(gg, masks, trace, P, ldir, ldist, cm, rng, stack, c);
+#else
+              unocc = soft_queue<kCount>(gg, masks, need_soft, trace, P, ldir, ldist, cm, rng, stack, c);
+#endif
             }
           }
 #ifdef RT_WG_TIMING

@@ -186,3 +186,14 @@ def test_invalid_arguments_are_rejected_without_a_device():
     assert lib.rt_context_create(0, None) != 0
     assert lib.rt_context_set_scene(None, None, 0) != 0
     assert lib.rt_last_error()
+
+
+def test_image_size_bounds_are_checked_before_the_device():
+    # each side <= 65536 (the kernel's camera-jitter division relies on it)
+    r = rtgo.ParallelRenderer(1)
+    r.set_samples(1)
+    s = rtgo.Scene.load_from_file(os.path.join(ROOT, "scenes", "sphere_reflections_light_facing.json"))
+    for w, h in ((65537, 1), (1, 65537), (0, 4)):
+        with pytest.raises(rtgo.RenderError) as e:
+            r.render(s, w, h)
+        assert "image size" in str(e.value)
