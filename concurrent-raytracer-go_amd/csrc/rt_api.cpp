@@ -460,9 +460,11 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   {
     uint64_t* jt = reinterpret_cast<uint64_t*>(host.data() + off_j);
     uint64_t a = 1, cc = 0;  // x_{i+j} = A_j x_i + C_j, built incrementally (rt_pcg_jump_coeffs)
-    for (int j = 0; j < kJump; ++j) {
-      jt[2 * j] = a;
-      jt[2 * j + 1] = cc;
+    for (int j = 0; j < 3 * kJump; ++j) {
+      if (j % 3 == 0) {  // entry h = j / 3: the jump by 3h draws
+        jt[2 * (j / 3)] = a;
+        jt[2 * (j / 3) + 1] = cc;
+      }
       cc = cc * RT_PCG_MULT + RT_PCG_INC;
       a = a * RT_PCG_MULT;
     }
@@ -477,9 +479,9 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   c->d_bvh = (const DBVHNode*)(base + off_b);
   c->d_jump = (const uint64_t*)(base + off_j);
   // small linear-scan scenes are staged into LDS by every workgroup
-  // (the PCG jump table stays in global memory unless RTGO_STAGE_JUMP is set: only
-  // the cooperative soft-shadow form reads it, and its 3 KB of LDS per workgroup
-  // cost more occupancy than the L1-cached reads cost time)
+  // (the 1 KB PCG jump table stays in global memory, L1-cached: only the
+  // cooperative soft-shadow form reads it, and scenes near the LDS limit of 12
+  // workgroups per CU ran faster without it; RTGO_STAGE_JUMP: experiments only)
   const size_t stage_end = getenv("RTGO_STAGE_JUMP") ? off_b : off_j;
   c->stage_bytes = (f.bvh.empty() && stage_end <= 48 * 1024) ? (int32_t)stage_end : 0;
   c->have_scene = true;

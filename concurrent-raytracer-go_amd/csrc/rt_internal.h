@@ -49,8 +49,10 @@ void tile_primary_masks(const FlatScene& fs, int32_t W, int32_t H, int32_t rank,
 
 // ---------------------------------------------------------------- kernels
 // PCG jump-ahead entries: cooperative soft shadows evaluate up to 64
-// rejection tries (3 draws each) per round and then advance by 3*64 draws.
-constexpr int kJump = 3 * 64 + 1;
+// rejection tries (3 draws each) per round and then advance by 3*used
+// draws; entry h holds (A_3h, C_3h), h = 0..64 (draws 3h+1, 3h+2 are plain
+// steps from 3h).
+constexpr int kJump = 64 + 1;
 // Largest block (pixels x spp) a workgroup renders (its hit list and
 // radiance slots live in LDS: 24 KB); the host picks P = floor(1024 / spp)
 // pixels per block (at most 64), so spp <= 1024.
@@ -63,7 +65,7 @@ struct KParams {
   const DMat* mats;
   const DLight* lights;
   const DBVHNode* bvh;
-  const uint64_t* jump;        // PCG jump table: (A_j, C_j) for j = 0..kJump-1 (rt_rng.h)
+  const uint64_t* jump;        // PCG jump table: (A_3h, C_3h) for h = 0..kJump-1 (rt_rng.h)
   float* out_linear;
   uint8_t* out_rgba;
   unsigned long long* counts;  // 9 counters (rt_counts order) or null

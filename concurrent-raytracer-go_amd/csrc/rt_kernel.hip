@@ -173,10 +173,10 @@ __device__ __forceinline__ double draw(rt_rng& r, Counters& c) {
   return rt_rng_draw(&r);
 }
 
-// draw i of a stream whose state is x: x_i = A_i x + C_i (jump table in LDS)
-__device__ __forceinline__ double draw_at(uint64_t x, const uint64_t* jump, int i) {
-  const uint64_t xi = jump[2 * i] * x + jump[2 * i + 1];
-  return rt_bits_to_unit(rt_pcg_out(xi));
+// State before draw 3h of a stream whose state is x: x_3h = A_3h x + C_3h
+// (jump table entry h, in LDS); draws 3h+1, 3h+2 follow by plain steps.
+__device__ __forceinline__ uint64_t state_at3(uint64_t x, const uint64_t* jump, int h) {
+  return jump[2 * h] * x + jump[2 * h + 1];
 }
 
 // RandomVec3InUnitSphere, vector.go:132-139.
@@ -597,8 +597,10 @@ RT_COOP_FN CoopOut soft_coop(const Geo p, bool masks, bool trace, d3 P, d3 ldir,
   int need = 16, unocc = 0, tries = 0;
   const unsigned long long below = (1ull << lane) - 1ull;
   while (need > 0) {
-    const double dx = draw_at(x, jump, 3 * lane), dy = draw_at(x, jump, 3 * lane + 1),
-                 dz = draw_at(x, jump, 3 * lane + 2);
+    const uint64_t x0 = state_at3(x, jump, lane), x1 = x0 * RT_PCG_MULT + RT_PCG_INC,
+                   x2 = x1 * RT_PCG_MULT + RT_PCG_INC;
+    const double dx = rt_bits_to_unit(rt_pcg_out(x0)), dy = rt_bits_to_unit(rt_pcg_out(x1)),
+                 dz = rt_bits_to_unit(rt_pcg_out(x2));
     const d3 pt = mk(dx * 2 - 1, dy * 2 - 1, dz * 2 - 1);
     const bool acc = len2(pt) < 1;
     const unsigned long long am = __ballot(acc);
@@ -613,7 +615,7 @@ RT_COOP_FN CoopOut soft_coop(const Geo p, bool masks, bool trace, d3 P, d3 ldir,
     unocc += nch - __popcll(__ballot(chosen && occ));
     need -= nch;
     tries += used;
-    x = jump[2 * (3 * used)] * x + jump[2 * (3 * used) + 1];
+    x = state_at3(x, jump, used);
   }
   return CoopOut{x, unocc, tries};
 }
@@ -922,7 +924,9 @@ template <bool kCount, bool kStage, bool kPilot>
 __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KParams pk) {
   __shared__ uint32_t hbits[kMaxBlockSamples / 32];  // hit samples of the block
   __shared__ int hoff[kMaxBlockSamples / 32 + 1];    // list offset of each bit word; [words] = #hits
+#ifdef RT_HLIST
   __shared__ uint16_t hlist[kMaxBlockSamples];       // hit sample ids, ascending
+#endif
   __shared__ double slot[kRound][3];                 // radiance of the round's entries
   __shared__ double psum[64][3];                     // per pixel: running sum over samples
   // dynamic LDS (dyn_lds): [staged scene prefix (kStage)][BVH stack (kStack x 64 ints)]
@@ -1022,12 +1026,38 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     if (lane == 63) hoff[nwords] = incl;
   }
   __syncthreads();
+#ifdef RT_HLIST
   for (int id = lane; id < nwords * 32; id += 64) {
     const uint32_t word = hbits[id >> 5];
     if ((word >> (id & 31)) & 1u) hlist[hoff[id >> 5] + __popc(word & ((1u << (id & 31)) - 1u))] = (uint16_t)id;
   }
   __syncthreads();
+#endif
   const int nh = hoff[nwords];
+  // sample id (pixel * ns + sample - s0) of hit-list entry e < nh: the bit
+  // word holding it (the last word whose list offset is <= e, by binary
+  // search over hoff), then the (e - offset)-th set bit of that word.  No
+  // materialized list: its 2 KB of LDS cost occupancy.
+  auto entry_id = [&](int e) -> int {
+#ifdef RT_HLIST
+    return hlist[e];
+#else
+    int w = 0;
+    for (int step = 16; step; step >>= 1)
+      if (w + step < nwords && hoff[w + step] <= e) w += step;
+    uint32_t word = hbits[w];
+    int k = e - hoff[w], pos = 0;
+    for (int sh = 16; sh; sh >>= 1) {
+      const int n = __popc(word & ((1u << sh) - 1u));
+      if (k >= n) {
+        k -= n;
+        word >>= sh;
+        pos += sh;
+      }
+    }
+    return w * 32 + pos;
+#endif
+  };
 #ifdef RT_WG_TIMING
   dbg_vis = __builtin_amdgcn_s_memtime() - tv0;
 #endif
@@ -1053,7 +1083,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       double* row = k->split_rad + (size_t)blk.slot * k->spp * 3;
       uint32_t* hw = k->split_hits + (size_t)blk.slot * ((k->spp + 31) >> 5);
       for (int e = a + lane; e < b; e += 64) {
-        const int s = blk.s0 + hlist[e];  // one pixel: id = sample - s0
+        const int s = blk.s0 + entry_id(e);  // one pixel: id = sample - s0
         const int q = e & (kRound - 1);
         row[3 * s + 0] = slot[q][0];
         row[3 * s + 1] = slot[q][1];
@@ -1116,7 +1146,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       if (!alive && e < limit) {
         KArg k = fresh();
         const BlockLoc loc = block_loc(k, blockIdx.x);
-        const int id = hlist[e], ns = loc.ns;
+        const int id = entry_id(e), ns = loc.ns;
         const int p = id / ns, s = loc.s0 + id - p * ns;
         const int tp = loc.p0 + p;
         Counters nc;  // phase 1 counted this camera ray and its draws
@@ -1323,7 +1353,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       }
       if (fin) {  // the path's radiance goes to its entry's ring slot
         if constexpr (kPilot)  // pilot render (one sample per pixel): the path's length
-          fresh()->tile_work[blockIdx.x * 64 + hlist[entry]] = depth + 1;
+          fresh()->tile_work[blockIdx.x * 64 + entry_id(entry)] = depth + 1;
         const int q = entry & (kRound - 1);
         slot[q][0] = L.x;
         slot[q][1] = L.y;
