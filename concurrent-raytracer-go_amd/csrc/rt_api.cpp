@@ -688,6 +688,8 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   if (rc) return rc;
   p.num_wgs = p.num_blocks;
   if (const char* e = getenv("RTGO_PRIO")) p.prio_blocks = atoi(e);  // experiments only
+  if (const char* e = getenv("RTGO_MAX_BLOCKS"))  // experiments only: the first N blocks (partial image)
+    p.num_wgs = p.num_blocks = std::min(p.num_blocks, std::max(0, atoi(e)));
   // the caller's stream, as given (NULL = the legacy default stream)
   hipStream_t s = (hipStream_t)stream;
   if (counts) HIP_TRY(hipMemsetAsync(c->d_counts, 0, 16 * sizeof(unsigned long long), s));

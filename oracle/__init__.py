@@ -88,7 +88,11 @@ def render(scene, width, height, settings, rank=0, world=1, nthreads=None, max_t
     """Render with the oracle. Returns (linear float64 (H,W,3), rgba uint8 (H,W,4), counts|None)."""
     rt = _rtgo()
     if nthreads is None:
-        nthreads = os.cpu_count() or 1
+        # the CPUs this process may run on, at most 16 (a GPU box's share)
+        try:
+            nthreads = min(16, len(os.sched_getaffinity(0)))
+        except AttributeError:
+            nthreads = min(16, os.cpu_count() or 1)
     lin = np.full((height, width, 3), np.nan, np.float64)
     rgba = np.zeros((height, width, 4), np.uint8)
     c = rt.Counts()

@@ -150,3 +150,19 @@ def test_cli_writes_png_and_benchmark_data(tmp_path):
     r.set_samples(3)
     rgba = r.render(rtgo.Scene.load_from_file(scene_file), 64, 48)
     assert np.array_equal(img, rgba[:, :, :3])
+
+
+def test_ten_thousand_sphere_field_matches_oracle():
+    """Config C4's scene (scenes/gen_spheres.py, 10k spheres: the BVH path)
+    at a size the linear-scan oracle finishes in seconds."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("gen_spheres", os.path.join(ROOT, "scenes", "gen_spheres.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    scene = rtgo.Scene.from_json_text(g.dumps(g.generate(10000)))
+    st = make_settings(rtgo, {"samples": 2, "max_depth": 4})
+    lin, rgba = _gpu(scene, 32, 18, st)
+    ref, ref_rgba, _ = oracle.render(scene, 32, 18, st)
+    assert lin.tobytes() == ref.astype(np.float32).tobytes()
+    assert rgba.tobytes() == ref_rgba.tobytes()
