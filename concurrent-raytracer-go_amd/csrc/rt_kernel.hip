@@ -38,15 +38,6 @@
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 3  // measured best of 2/3/4 (4 spills the FP64 path state)
 #endif
-// sphere scans of closest_hit and cone_candidates: unroll factor (a lone
-// wave at the end of a launch waits on each sphere's LDS loads otherwise)
-#ifdef RT_SPH_UNROLL
-#define RT_PRAGMA(x) _Pragma(#x)
-#define RT_SPH_LOOP_(n) RT_PRAGMA(unroll n)
-#define RT_SPH_LOOP RT_SPH_LOOP_(RT_SPH_UNROLL)
-#else
-#define RT_SPH_LOOP
-#endif
 #ifndef RT_COOP_MAX
 #define RT_COOP_MAX 8  // cooperative soft shadows when at most this many lanes need them
 #endif
@@ -271,6 +262,23 @@ __device__ __forceinline__ bool box_hit(const DBVHNode& n, d3 o, d3 id, double t
   return tn <= tf + fabs(tf) * KC(1e-9) + KC(1e-12);
 }
 
+// box_hit that also returns the entry distance (child ordering)
+__device__ __forceinline__ bool box_hit_t(const DBVHNode& n, d3 o, d3 id, double tmin, double tmax, double& tn) {
+  const double tx0 = ((double)n.lo[0] - o.x) * id.x, tx1 = ((double)n.hi[0] - o.x) * id.x;
+  const double ty0 = ((double)n.lo[1] - o.y) * id.y, ty1 = ((double)n.hi[1] - o.y) * id.y;
+  const double tz0 = ((double)n.lo[2] - o.z) * id.z, tz1 = ((double)n.hi[2] - o.z) * id.z;
+  tn = fmax(fmax(fmin(tx0, tx1), fmin(ty0, ty1)), fmax(fmin(tz0, tz1), tmin));
+  const double tf = fmin(fmin(fmax(tx0, tx1), fmax(ty0, ty1)), fmin(fmax(tz0, tz1), tmax));
+  return tn <= tf + fabs(tf) * KC(1e-9) + KC(1e-12);
+}
+// BVH traversal state: a node is (first << 3) | count, count 0 = internal
+// node whose children are the adjacent records first, first + 1 (bvh.cpp),
+// count 1..4 = leaf of spheres [first, first + count).  Children are tested
+// together, from the one 64-B load of their two records; the nearer one hit
+// is entered and the other pushed, so the per-lane LDS stack holds ready
+// node codes and a pop needs no memory access.
+__device__ __forceinline__ int bvh_code(const DBVHNode& n) { return (n.left_or_first << 3) | n.count; }
+
 __device__ __forceinline__ d3 inv_dir(d3 d) {
   // zero components get a huge finite inverse: no 0*inf NaN in the slabs
   return mk(1.0 / (d.x != 0 ? d.x : 1e-300), 1.0 / (d.y != 0 ? d.y : 1e-300), 1.0 / (d.z != 0 ? d.z : 1e-300));
@@ -322,18 +330,28 @@ __device__ __forceinline__ bool closest_hit(const Geo& p, d3 o, d3 d, HitSel& hs
   if (p.use_bvh) {
     const d3 id = inv_dir(d);
     int sp = 0;
-    int node = 0;
+    cnt<kCount>(c, C_BOX);
+    const DBVHNode root = p.bvh[0];
+    if (!box_hit(root, o, id, tmin, closest)) return false;
+    int cur = bvh_code(root);
     for (;;) {
-      const DBVHNode n = p.bvh[node];
-      cnt<kCount>(c, C_BOX);
-      if (box_hit(n, o, id, tmin, closest)) {
-        if (n.count == 0) {
-          stack[sp * 64] = n.left_or_first + 1;
-          ++sp;
-          node = n.left_or_first;
+      const int first = cur >> 3, count = cur & 7;
+      if (count == 0) {
+        const DBVHNode L = p.bvh[first], R = p.bvh[first + 1];
+        cnt<kCount>(c, C_BOX, 2);
+        double tl, tr;
+        const bool hl = box_hit_t(L, o, id, tmin, closest, tl), hr = box_hit_t(R, o, id, tmin, closest, tr);
+        if (hl || hr) {
+          const bool lfirst = hl && (!hr || tl <= tr);
+          if (hl && hr) {
+            stack[sp * 64] = lfirst ? bvh_code(R) : bvh_code(L);
+            ++sp;
+          }
+          cur = lfirst ? bvh_code(L) : bvh_code(R);
           continue;
         }
-        for (int i = n.left_or_first; i < n.left_or_first + n.count; ++i) {
+      } else {
+        for (int i = first; i < first + count; ++i) {
           cnt<kCount>(c, C_SPH);
           const DSphere& S = p.spheres[i];
           double num;
@@ -351,7 +369,7 @@ __device__ __forceinline__ bool closest_hit(const Geo& p, d3 o, d3 d, HitSel& hs
       }
       if (sp == 0) break;
       --sp;
-      node = stack[sp * 64];
+      cur = stack[sp * 64];
     }
     return found;
   }
@@ -413,18 +431,28 @@ __device__ __forceinline__ bool any_hit(const Geo& p, d3 o, d3 d, double tmax, i
   if (p.use_bvh) {
     const d3 id = inv_dir(d);
     int sp = 0;
-    int node = 0;
+    cnt<kCount>(c, C_BOX);
+    const DBVHNode root = p.bvh[0];
+    if (!box_hit(root, o, id, tmin, tmax)) return false;
+    int cur = bvh_code(root);
     for (;;) {
-      const DBVHNode n = p.bvh[node];
-      cnt<kCount>(c, C_BOX);
-      if (box_hit(n, o, id, tmin, tmax)) {
-        if (n.count == 0) {
-          stack[sp * 64] = n.left_or_first + 1;
-          ++sp;
-          node = n.left_or_first;
+      const int first = cur >> 3, count = cur & 7;
+      if (count == 0) {
+        const DBVHNode L = p.bvh[first], R = p.bvh[first + 1];
+        cnt<kCount>(c, C_BOX, 2);
+        double tl, tr;
+        const bool hl = box_hit_t(L, o, id, tmin, tmax, tl), hr = box_hit_t(R, o, id, tmin, tmax, tr);
+        if (hl || hr) {
+          const bool lfirst = hl && (!hr || tl <= tr);
+          if (hl && hr) {
+            stack[sp * 64] = lfirst ? bvh_code(R) : bvh_code(L);
+            ++sp;
+          }
+          cur = lfirst ? bvh_code(L) : bvh_code(R);
           continue;
         }
-        for (int i = n.left_or_first; i < n.left_or_first + n.count; ++i) {
+      } else {
+        for (int i = first; i < first + count; ++i) {
           cnt<kCount>(c, C_SPH);
           double num;
           if (sphere_query(p.spheres[i], o, d, a, inv_a, tmin, tmax, num)) return true;
@@ -432,11 +460,10 @@ __device__ __forceinline__ bool any_hit(const Geo& p, d3 o, d3 d, double tmax, i
       }
       if (sp == 0) break;
       --sp;
-      node = stack[sp * 64];
+      cur = stack[sp * 64];
     }
     return false;
   }
-  RT_SPH_LOOP
   for (int i = 0; i < p.ns; ++i) {
     cnt<kCount>(c, C_SPH);
     double num;
@@ -494,7 +521,6 @@ __device__ __forceinline__ Cand cone_candidates(const Geo& p, d3 P, d3 N, bool f
                                                 double ldist) {
   const bool self_out = front && dot(N, ldir) >= KC(0.1015);
   Cand m{0ull, 0ull};
-  RT_SPH_LOOP
   for (int i = 0; i < p.ns; ++i) {
     const DSphere& S = p.spheres[i];
     if (self_out && S.obj == self && S.r > 0) continue;
@@ -822,6 +848,9 @@ __device__ __forceinline__ Hot hot() {
     h.lights = reinterpret_cast<const DLight*>(dyn_lds + (reinterpret_cast<const unsigned char*>(k->lights) - base));
     const long jo = reinterpret_cast<const unsigned char*>(k->jump) - base;
     if (jo < k->stage_bytes) h.jump = reinterpret_cast<const uint64_t*>(dyn_lds + jo);
+    // staged scenes are linear-scan scenes (set_scene stages only without a
+    // BVH): the staged kernels carry no BVH traversal code at all
+    h.g.use_bvh = 0;
   }
   h.nl = k->nl;
   h.max_depth = k->max_depth;

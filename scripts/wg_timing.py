@@ -19,7 +19,14 @@ import rtgo  # noqa: E402
 scene = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "scenes", "sphere_reflections_light_facing.json")
 W, H, SPP = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (800, 600, 100)
 ctx = rtgo.Context(0)
-ctx.set_scene(rtgo.Scene.load_from_file(scene))
+if scene == "spheres10k":  # config C4/C5 scene (scenes/gen_spheres.py)
+    import importlib.util
+    _spec = importlib.util.spec_from_file_location("g", os.path.join(ROOT, "scenes", "gen_spheres.py"))
+    _g = importlib.util.module_from_spec(_spec)
+    _spec.loader.exec_module(_g)
+    ctx.set_scene(rtgo.Scene.from_json_text(_g.dumps(_g.generate(10000))))
+else:
+    ctx.set_scene(rtgo.Scene.load_from_file(scene))
 st = rtgo.default_settings()
 st.samples = SPP
 lin = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
