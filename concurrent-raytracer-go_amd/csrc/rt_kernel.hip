@@ -333,10 +333,12 @@ __device__ __forceinline__ bool closest_hit(const Geo& p, d3 o, d3 d, HitSel& hs
     cnt<kCount>(c, C_BOX);
     const DBVHNode root = p.bvh[0];
     if (!box_hit(root, o, id, tmin, closest)) return false;
+    // while-while (Aila & Laine): lanes descend internal nodes together,
+    // then test their leaves together; -1 = traversal finished
     int cur = bvh_code(root);
-    for (;;) {
-      const int first = cur >> 3, count = cur & 7;
-      if (count == 0) {
+    while (cur != -1) {
+      while ((cur & 7) == 0) {
+        const int first = cur >> 3;
         const DBVHNode L = p.bvh[first], R = p.bvh[first + 1];
         cnt<kCount>(c, C_BOX, 2);
         double tl, tr;
@@ -348,28 +350,28 @@ __device__ __forceinline__ bool closest_hit(const Geo& p, d3 o, d3 d, HitSel& hs
             ++sp;
           }
           cur = lfirst ? bvh_code(L) : bvh_code(R);
-          continue;
-        }
-      } else {
-        for (int i = first; i < first + count; ++i) {
-          cnt<kCount>(c, C_SPH);
-          const DSphere& S = p.spheres[i];
-          double num;
-          if (sphere_query(S, o, d, a, inv_a, tmin, closest, num)) {
-            const double t = num / a;
-            if (t == closest && best_obj > S.obj) continue;
-            closest = t;
-            hs.num = num;
-            hs.idx = i;
-            hs.is_tri = 0;
-            best_obj = S.obj;
-            found = true;
-          }
+        } else {
+          cur = sp == 0 ? -1 : stack[--sp * 64];
         }
       }
-      if (sp == 0) break;
-      --sp;
-      cur = stack[sp * 64];
+      if (cur == -1) break;
+      const int first = cur >> 3, count = cur & 7;
+      for (int i = first; i < first + count; ++i) {
+        cnt<kCount>(c, C_SPH);
+        const DSphere& S = p.spheres[i];
+        double num;
+        if (sphere_query(S, o, d, a, inv_a, tmin, closest, num)) {
+          const double t = num / a;
+          if (t == closest && best_obj > S.obj) continue;
+          closest = t;
+          hs.num = num;
+          hs.idx = i;
+          hs.is_tri = 0;
+          best_obj = S.obj;
+          found = true;
+        }
+      }
+      cur = sp == 0 ? -1 : stack[--sp * 64];
     }
     return found;
   }
@@ -434,10 +436,10 @@ __device__ __forceinline__ bool any_hit(const Geo& p, d3 o, d3 d, double tmax, i
     cnt<kCount>(c, C_BOX);
     const DBVHNode root = p.bvh[0];
     if (!box_hit(root, o, id, tmin, tmax)) return false;
-    int cur = bvh_code(root);
-    for (;;) {
-      const int first = cur >> 3, count = cur & 7;
-      if (count == 0) {
+    int cur = bvh_code(root);  // while-while, as in closest_hit
+    while (cur != -1) {
+      while ((cur & 7) == 0) {
+        const int first = cur >> 3;
         const DBVHNode L = p.bvh[first], R = p.bvh[first + 1];
         cnt<kCount>(c, C_BOX, 2);
         double tl, tr;
@@ -449,18 +451,18 @@ __device__ __forceinline__ bool any_hit(const Geo& p, d3 o, d3 d, double tmax, i
             ++sp;
           }
           cur = lfirst ? bvh_code(L) : bvh_code(R);
-          continue;
-        }
-      } else {
-        for (int i = first; i < first + count; ++i) {
-          cnt<kCount>(c, C_SPH);
-          double num;
-          if (sphere_query(p.spheres[i], o, d, a, inv_a, tmin, tmax, num)) return true;
+        } else {
+          cur = sp == 0 ? -1 : stack[--sp * 64];
         }
       }
-      if (sp == 0) break;
-      --sp;
-      cur = stack[sp * 64];
+      if (cur == -1) break;
+      const int first = cur >> 3, count = cur & 7;
+      for (int i = first; i < first + count; ++i) {
+        cnt<kCount>(c, C_SPH);
+        double num;
+        if (sphere_query(p.spheres[i], o, d, a, inv_a, tmin, tmax, num)) return true;
+      }
+      cur = sp == 0 ? -1 : stack[--sp * 64];
     }
     return false;
   }

@@ -13,12 +13,22 @@ import rtgo  # noqa: E402
 
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 W, H, SPP = 800, 600, 100
+SCENE = os.environ.get("PMC_SCENE", "")  # "spheres10k": config C4's scene at PMC_SIZE (W,H,SPP)
+if os.environ.get("PMC_SIZE"):
+    W, H, SPP = (int(v) for v in os.environ["PMC_SIZE"].split(","))
 st = rtgo.default_settings()
 st.samples = SPP
 s = torch.cuda.Stream()
 torch.cuda.set_stream(s)
 ctx = rtgo.Context(0)
-ctx.set_scene(rtgo.Scene.load_from_file(os.path.join(ROOT, "scenes", "sphere_reflections_light_facing.json")))
+if SCENE == "spheres10k":
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("g", os.path.join(ROOT, "scenes", "gen_spheres.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    ctx.set_scene(rtgo.Scene.from_json_text(g.dumps(g.generate(10000))))
+else:
+    ctx.set_scene(rtgo.Scene.load_from_file(os.path.join(ROOT, "scenes", "sphere_reflections_light_facing.json")))
 lin = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
 rgba = torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda")
 for _ in range(K):
