@@ -10,7 +10,11 @@
 //
 // Layout: nodes in depth-first order with the two children of an internal
 // node adjacent (left = i, right = i + 1), 32 B each, float bounds rounded
-// outward by one ulp so a box never excludes a point of its spheres.
+// outward by one ulp so a box never excludes a point of its spheres.  Every
+// sphere box is also padded by pad = 2^-18 * M, M the largest coordinate
+// magnitude of the scene (sphere extents and the camera): the kernel's slab
+// test runs in binary32 on the ray origin rounded to float, an error of at
+// most 2^-24 * M per axis, which the padding covers 64 times over.
 // Spheres are reordered so every leaf is a contiguous range.
 #include <math.h>
 #include <string.h>
@@ -73,12 +77,17 @@ void build_sphere_bvh(FlatScene* fs) {
   if (n == 0) return;
   std::vector<Box> pb(n);
   std::vector<double> cen(3 * (size_t)n);
+  double M = 1.0;
+  for (int k = 0; k < 3; ++k) M = std::max(M, fabs(fs->cam_pos[k]));
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < 3; ++k) M = std::max(M, fabs(fs->spheres[i].c[k]) + fabs(fs->spheres[i].r));
+  const double pad = ldexp(M, -18);
   for (int i = 0; i < n; ++i) {
     const DSphere& s = fs->spheres[i];
     double r = fabs(s.r);
     for (int k = 0; k < 3; ++k) {
-      pb[i].lo[k] = s.c[k] - r;
-      pb[i].hi[k] = s.c[k] + r;
+      pb[i].lo[k] = s.c[k] - r - pad;
+      pb[i].hi[k] = s.c[k] + r + pad;
       cen[3 * (size_t)i + k] = s.c[k];
     }
   }

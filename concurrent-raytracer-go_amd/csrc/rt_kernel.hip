@@ -262,14 +262,30 @@ __device__ __forceinline__ bool box_hit(const DBVHNode& n, d3 o, d3 id, double t
   return tn <= tf + fabs(tf) * KC(1e-9) + KC(1e-12);
 }
 
-// box_hit that also returns the entry distance (child ordering)
-__device__ __forceinline__ bool box_hit_t(const DBVHNode& n, d3 o, d3 id, double tmin, double tmax, double& tn) {
-  const double tx0 = ((double)n.lo[0] - o.x) * id.x, tx1 = ((double)n.hi[0] - o.x) * id.x;
-  const double ty0 = ((double)n.lo[1] - o.y) * id.y, ty1 = ((double)n.hi[1] - o.y) * id.y;
-  const double tz0 = ((double)n.lo[2] - o.z) * id.z, tz1 = ((double)n.hi[2] - o.z) * id.z;
-  tn = fmax(fmax(fmin(tx0, tx1), fmin(ty0, ty1)), fmax(fmin(tz0, tz1), tmin));
-  const double tf = fmin(fmin(fmax(tx0, tx1), fmax(ty0, ty1)), fmin(fmax(tz0, tz1), tmax));
-  return tn <= tf + fabs(tf) * KC(1e-9) + KC(1e-12);
+// The ray in binary32 for the slab tests below the root: origin rounded to
+// float (error <= 2^-24 |o| per axis, covered by the boxes' padding,
+// bvh.cpp), inverse direction rounded and clamped to 1e30 (inv_dir's 1e300
+// for a zero component stays a huge finite value, no 0 * inf).
+struct Ray32 {
+  float ox, oy, oz, ix, iy, iz;
+};
+__device__ __forceinline__ Ray32 ray32(d3 o, d3 id) {
+  return Ray32{(float)o.x, (float)o.y, (float)o.z, (float)fmin(fmax(id.x, -1e30), 1e30),
+               (float)fmin(fmax(id.y, -1e30), 1e30), (float)fmin(fmax(id.z, -1e30), 1e30)};
+}
+// a [tmin, tmax] window widened for binary32 (both are >= 0)
+__device__ __forceinline__ float t_lo32(double t) { return (float)(t * (1.0 - 0x1p-20)); }
+__device__ __forceinline__ float t_hi32(double t) { return (float)(t * (1.0 + 0x1p-20)); }
+// binary32 slab test of a child box, conservative: the products carry
+// < 2^-21 relative error, the slack below is 2^-20 of the interval ends;
+// also returns the entry distance (child ordering)
+__device__ __forceinline__ bool box_hit32(const DBVHNode& n, const Ray32& r, float tmin, float tmax, float& tn) {
+  const float tx0 = (n.lo[0] - r.ox) * r.ix, tx1 = (n.hi[0] - r.ox) * r.ix;
+  const float ty0 = (n.lo[1] - r.oy) * r.iy, ty1 = (n.hi[1] - r.oy) * r.iy;
+  const float tz0 = (n.lo[2] - r.oz) * r.iz, tz1 = (n.hi[2] - r.oz) * r.iz;
+  tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+  const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+  return tn <= tf + (fabsf(tn) + fabsf(tf)) * 0x1p-20f;
 }
 // BVH traversal state: a node is (first << 3) | count, count 0 = internal
 // node whose children are the adjacent records first, first + 1 (bvh.cpp),
@@ -333,6 +349,8 @@ __device__ __forceinline__ bool closest_hit(const Geo& p, d3 o, d3 d, HitSel& hs
     cnt<kCount>(c, C_BOX);
     const DBVHNode root = p.bvh[0];
     if (!box_hit(root, o, id, tmin, closest)) return false;
+    const Ray32 r32 = ray32(o, id);
+    const float tminf = t_lo32(tmin);
     // while-while (Aila & Laine): lanes descend internal nodes together,
     // then test their leaves together; -1 = traversal finished
     int cur = bvh_code(root);
@@ -341,8 +359,9 @@ __device__ __forceinline__ bool closest_hit(const Geo& p, d3 o, d3 d, HitSel& hs
         const int first = cur >> 3;
         const DBVHNode L = p.bvh[first], R = p.bvh[first + 1];
         cnt<kCount>(c, C_BOX, 2);
-        double tl, tr;
-        const bool hl = box_hit_t(L, o, id, tmin, closest, tl), hr = box_hit_t(R, o, id, tmin, closest, tr);
+        float tl, tr;
+        const float tmaxf = t_hi32(closest);
+        const bool hl = box_hit32(L, r32, tminf, tmaxf, tl), hr = box_hit32(R, r32, tminf, tmaxf, tr);
         if (hl || hr) {
           const bool lfirst = hl && (!hr || tl <= tr);
           if (hl && hr) {
@@ -436,14 +455,16 @@ __device__ __forceinline__ bool any_hit(const Geo& p, d3 o, d3 d, double tmax, i
     cnt<kCount>(c, C_BOX);
     const DBVHNode root = p.bvh[0];
     if (!box_hit(root, o, id, tmin, tmax)) return false;
+    const Ray32 r32 = ray32(o, id);
+    const float tminf = t_lo32(tmin), tmaxf = t_hi32(tmax);
     int cur = bvh_code(root);  // while-while, as in closest_hit
     while (cur != -1) {
       while ((cur & 7) == 0) {
         const int first = cur >> 3;
         const DBVHNode L = p.bvh[first], R = p.bvh[first + 1];
         cnt<kCount>(c, C_BOX, 2);
-        double tl, tr;
-        const bool hl = box_hit_t(L, o, id, tmin, tmax, tl), hr = box_hit_t(R, o, id, tmin, tmax, tr);
+        float tl, tr;
+        const bool hl = box_hit32(L, r32, tminf, tmaxf, tl), hr = box_hit32(R, r32, tminf, tmaxf, tr);
         if (hl || hr) {
           const bool lfirst = hl && (!hr || tl <= tr);
           if (hl && hr) {
