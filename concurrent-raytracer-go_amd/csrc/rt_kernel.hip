@@ -597,6 +597,115 @@ __device__ __forceinline__ bool shadow_blocked(const Geo& p, bool masks, d3 o, d
   return any_hit<kCount>(p, o, d, tmax, stack, c);
 }
 
+// ------------------------------------------------------------ wide mode
+// When few lanes of a wave still run paths (the end of a block, where one
+// long path sets the launch's critical path), the idle lanes help: every
+// lane that needs a query (an "owner", at most 16) gets a group of
+// S = 64 / next_pow2(owners) helper lanes, which split the primitive scan
+// (primitive i goes to helper i mod S) and merge their results.  Only for
+// sphere-only linear-scan scenes (no triangles): the merges below are exact
+// for spheres.  wide_groups: the owner table (LDS), this lane's owner and its
+// index within the group; S is returned.
+__device__ __forceinline__ int wide_groups(bool need, unsigned long long qmask, int nq, int* owner_tab, int& ow,
+                                           int& k, bool& helper) {
+  const int lane = (int)(threadIdx.x & 63);
+  const int S = nq <= 4 ? 16 : (nq <= 8 ? 8 : 4);
+  if (need) owner_tab[__popcll(qmask & ((1ull << lane) - 1ull))] = lane;
+  __syncthreads();
+  const int grp = lane / S;
+  k = lane - grp * S;
+  helper = grp < nq;
+  ow = helper ? owner_tab[grp] : lane;
+  __syncthreads();  // the table is reused by the next call
+  return S;
+}
+
+// hitWorld's closest hit over the spheres (the scene has no triangles), with
+// helpers.  Each helper scans its spheres in hittable order with the
+// sequential rule; the group then keeps the smallest t, and of equal t the
+// larger hittable index (what the sequential scan ends with: a tie replaces
+// the current hit unless its index is larger).  Exact for finite rays; an
+// owner with a non-finite ray (or a = 0) is flagged in `fallback` and scans
+// on its own.  Returns found for owner lanes.
+template <bool kCount>
+__device__ __forceinline__ bool closest_wide(const Geo& g, bool need, unsigned long long qmask, int nq, d3 o, d3 d,
+                                             HitSel& hs, bool& fallback, Counters& c) {
+  __shared__ int owner_tab[16];
+  const int lane = (int)(threadIdx.x & 63);
+  int ow, k;
+  bool helper;
+  const int S = wide_groups(need, qmask, nq, owner_tab, ow, k, helper);
+  const d3 ro = mk(__shfl(o.x, ow), __shfl(o.y, ow), __shfl(o.z, ow));
+  const d3 rd = mk(__shfl(d.x, ow), __shfl(d.y, ow), __shfl(d.z, ow));
+  const double a = len2(rd);
+  const double inv_a = approx_rcp(a);
+  double bt = __builtin_inf(), bnum = 0;
+  int bobj = -1, bidx = -1;
+  bool found = false;
+  if (helper) {
+    for (int i = k; i < g.ns; i += S) {
+      cnt<kCount>(c, C_SPH);
+      const DSphere& Sp = g.spheres[i];
+      double num;
+      if (sphere_query(Sp, ro, rd, a, inv_a, 0.001, bt, num)) {
+        const double t = num / a;
+        if (t == bt && bobj > Sp.obj) continue;
+        bt = t;
+        bnum = num;
+        bidx = i;
+        bobj = Sp.obj;
+        found = true;
+      }
+    }
+  }
+  for (int off = S >> 1; off >= 1; off >>= 1) {  // within the group (aligned to S)
+    const double t2 = __shfl_xor(bt, off), n2 = __shfl_xor(bnum, off);
+    const int o2 = __shfl_xor(bobj, off), i2 = __shfl_xor(bidx, off), f2 = __shfl_xor((int)found, off);
+    if (f2 && (!found || t2 < bt || (t2 == bt && o2 > bobj))) {
+      bt = t2;
+      bnum = n2;
+      bobj = o2;
+      bidx = i2;
+      found = true;
+    }
+  }
+  const int lead = need ? __popcll(qmask & ((1ull << lane) - 1ull)) * S : lane;
+  const double fnum = __shfl(bnum, lead);
+  const int fidx = __shfl(bidx, lead), ffound = __shfl((int)found, lead);
+  fallback = need && !(__builtin_isfinite(o.x + o.y + o.z) && a > 0 && __builtin_isfinite(__shfl(a, lead)));
+  hs.num = fnum;
+  hs.idx = fidx;
+  hs.is_tri = 0;
+  return ffound != 0;
+}
+
+// cone_candidates (spheres only) with helpers: each helper tests its
+// spheres, the group ORs the bits.  Same tests, same mask.
+__device__ __forceinline__ unsigned long long cone_wide(const Geo& g, bool need, unsigned long long qmask, int nq,
+                                                        d3 P, d3 N, bool front, int self, d3 ldir, double ldist) {
+  __shared__ int owner_tab2[16];
+  const int lane = (int)(threadIdx.x & 63);
+  int ow, k;
+  bool helper;
+  const int S = wide_groups(need, qmask, nq, owner_tab2, ow, k, helper);
+  const d3 Po = mk(__shfl(P.x, ow), __shfl(P.y, ow), __shfl(P.z, ow));
+  const d3 Lo = mk(__shfl(ldir.x, ow), __shfl(ldir.y, ow), __shfl(ldir.z, ow));
+  const double dist = __shfl(ldist, ow);
+  const bool self_out = __shfl((int)(front && dot(N, ldir) >= KC(0.1015)), ow) != 0;
+  const int selfo = __shfl(self, ow);
+  unsigned long long m = 0;
+  if (helper) {
+    for (int i = k; i < g.ns; i += S) {
+      const DSphere& Sp = g.spheres[i];
+      if (self_out && Sp.obj == selfo && Sp.r > 0) continue;
+      if (in_cone(Sp.c, Sp.r, Po, Lo, dist)) m |= 1ull << i;
+    }
+  }
+  for (int off = S >> 1; off >= 1; off >>= 1) m |= __shfl_xor(m, off);
+  const int lead = need ? __popcll(qmask & ((1ull << lane) - 1ull)) * S : lane;
+  return __shfl(m, lead);
+}
+
 // ------------------------------------------------------------ soft shadows
 // Sequential form (every lane its own): ONE loop over rejection tries (3
 // draws each — the same draws, in the same order, as 16 calls of
@@ -1226,18 +1335,35 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       bool shade = false, front = false, fin = false;
       d3 P = mk(0, 0, 0), N = mk(0, 0, 0);
       int mi = 0, self = -1;
+      HitSel hs;
+      bool wide_q = false, wide_found = false, wide_fb = false;
+#ifndef RT_NO_WIDE
+      if constexpr (kStage) {  // wave-uniform: few paths left -> helpers
+        const Hot h = hot<kStage>();
+        const bool need = alive && depth < h.max_depth;
+        const unsigned long long qm = __ballot(need);
+        const int nq = __popcll(qm);
+        // (from 16 spheres on: below that the group set-up and merge cost more
+        // than the short scan they split; measured on the 5-sphere scene)
+        if (h.g.nt == 0 && h.g.ns >= 16 && nq > 0 && nq <= 16) {
+          // (kCount: helpers count their sphere tests, primary queries included)
+          wide_found = closest_wide<kCount>(h.g, need, qm, nq, o, d, hs, wide_fb, c);
+          wide_q = true;
+        }
+      }
+#endif
       if (alive) {
         const Hot h = hot<kStage>();
         const Geo& gg = h.g;
         bool done = depth >= h.max_depth;  // traceRay depth cut-off: contributes 0
-        HitSel hs;
         if (!done) {
           if (kCount && depth == 0) {  // phase 1 counted the primary query
             Counters nc;
-            done = !closest_hit<false>(gg, o, d, hs, stack, all, nc);
+            done = (wide_q && !wide_fb) ? !wide_found : !closest_hit<false>(gg, o, d, hs, stack, all, nc);
           } else {
             cnt<kCount>(c, C_BOUNCE);
-            done = !closest_hit<kCount>(gg, o, d, hs, stack, all, c);  // miss -> black
+            done = (wide_q && !wide_fb) ? !wide_found
+                                        : !closest_hit<kCount>(gg, o, d, hs, stack, all, c);  // miss -> black
           }
         }
         if (done) {
@@ -1298,9 +1424,25 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
             if (lit) {
               cnt<kCount>(c, C_LIGHT);
               cnt<kCount>(c, C_SHADOW);
-              if (masks) cm = cone_candidates(gg, P, N, front, self, ldir, ldist);
-              occl = shadow_blocked<kCount>(gg, masks, P, ldir, ldist, cm, stack, c);  // hard shadow ray
             }
+          }
+          bool wide_c = false;
+#ifndef RT_NO_WIDE
+          if constexpr (kStage) {  // few lit hit points: the cone tests with helpers
+            if (masks && gg.nt == 0) {
+              const unsigned long long cq = __ballot(shade && lit);
+              const int ncq = __popcll(cq);
+              if (ncq > 0 && ncq <= 16) {
+                const unsigned long long ms = cone_wide(gg, shade && lit, cq, ncq, P, N, front, self, ldir, ldist);
+                if (shade && lit) cm = Cand{ms, 0ull};
+                wide_c = true;
+              }
+            }
+          }
+#endif
+          if (shade && lit) {
+            if (masks && !wide_c) cm = cone_candidates(gg, P, N, front, self, ldir, ldist);
+            occl = shadow_blocked<kCount>(gg, masks, P, ldir, ldist, cm, stack, c);  // hard shadow ray
           }
 #ifdef RT_WG_TIMING
           dbg_hard += __builtin_amdgcn_s_memtime() - th0;
