@@ -193,8 +193,9 @@ void build_sphere_bvh(FlatScene* fs) {
     stack.push_back({left + 1, mid, t.first + t.count - mid});
     stack.push_back({left, t.first, mid - t.first});
   }
-  // depth check: traversal keeps at most depth-1 pending right children on
-  // its per-lane LDS stack (rt_kernel.hip kStack = 40)
+  // depth check: traversal keeps at most depth-1 pending children on its
+  // per-lane LDS stack, which the kernels size to the tree's depth (at most
+  // kStack = 40 entries)
   {
     std::vector<std::pair<int, int>> st = {{0, 1}};
     int maxd = 0;
@@ -207,10 +208,11 @@ void build_sphere_bvh(FlatScene* fs) {
         st.push_back({nodes[ni].left_or_first + 1, dep + 1});
       }
     }
-    if (maxd > 38) {
+    if (maxd > kStack) {
       fs->bvh.clear();  // too deep for the stack: keep the linear scan
       return;
     }
+    fs->bvh_depth = maxd;
   }
   std::vector<DSphere> reordered(n);
   for (int i = 0; i < n; ++i) reordered[i] = fs->spheres[idx[i]];

@@ -686,6 +686,7 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
     p.stage_src = c->d_scene;
     p.stage_bytes = getenv("RTGO_NO_STAGE") ? 0 : c->stage_bytes;
     p.stack_off = (p.stage_bytes + 15) & ~15;
+    p.stack_depth = std::max(1, f.bvh_depth);
   }
   rc = prepare_schedule(c, &p, st);
   if (rc) return rc;

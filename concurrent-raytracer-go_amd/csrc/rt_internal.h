@@ -22,6 +22,7 @@ struct FlatScene {
   std::vector<DMat> mats;
   std::vector<DLight> lights;
   std::vector<DBVHNode> bvh;  // empty => linear scan
+  int32_t bvh_depth = 0;      // levels of the BVH (root = 1): the traversal stack holds fewer entries
   double cam_pos[3] = {0, 0, 0};
   double aspect = 0;
   int32_t objects = 0;        // len(hittables)
@@ -57,6 +58,10 @@ constexpr int kJump = 64 + 1;
 // radiance slots live in LDS: 24 KB); the host picks P = floor(1024 / spp)
 // pixels per block (at most 64), so spp <= 1024.
 constexpr int kMaxBlockSamples = 1024;
+// Deepest BVH the kernels accept (per-lane LDS stack entries; bvh.cpp keeps
+// the linear scan for deeper trees).  The stacks are allocated per launch for
+// the scene's actual depth (10k spheres: 15 levels).
+constexpr int kStack = 40;
 
 struct KParams {
   const DSphere* spheres;
@@ -80,6 +85,7 @@ struct KParams {
   const void* stage_src;       // start of the scene prefix staged into LDS (spheres..lights)
   int32_t stage_bytes;         // bytes to stage (multiple of 16); 0 = read the scene from global memory
   int32_t stack_off;           // byte offset of the BVH stacks in dynamic LDS
+  int32_t stack_depth;         // entries per lane of a BVH stack (the tree's depth)
   double cam[3];
   double aspect;
   uint64_t seed_key;
