@@ -334,6 +334,14 @@ struct rt_context {
   unsigned long long* d_masks = nullptr;
   size_t d_masks_cap = 0;
   int32_t stage_bytes = 0;  // scene prefix staged into LDS per workgroup (0 = none)
+  // wavefront path (BVH scenes): path arrays + queues, per-chunk radiance, loop control
+  void* wf_mem = nullptr;
+  size_t wf_mem_bytes = 0;
+  void* wf_rad = nullptr;
+  size_t wf_rad_bytes = 0;
+  WfCtl* wf_ctl = nullptr;   // device
+  WfCtl* wf_host = nullptr;  // pinned ring of kWfRing snapshots
+  hipEvent_t wf_ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 extern "C" {
@@ -407,6 +415,12 @@ void rt_context_destroy(rt_context* c) {
   if (c->d_pilot) (void)hipFree(c->d_pilot);
   if (c->d_split) (void)hipFree(c->d_split);
   if (c->d_masks) (void)hipFree(c->d_masks);
+  if (c->wf_mem) (void)hipFree(c->wf_mem);
+  if (c->wf_rad) (void)hipFree(c->wf_rad);
+  if (c->wf_ctl) (void)hipFree(c->wf_ctl);
+  if (c->wf_host) (void)hipHostFree(c->wf_host);
+  for (hipEvent_t& e : c->wf_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -631,6 +645,162 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st) {
   return RT_OK;
 }
 
+// ---------------------------------------------------------------- wavefront path
+// BVH scenes render through the staged kernels of rt_wavefront.hip (DESIGN.md
+// §4.2).  Buffers live in the context and grow on demand; a frame is cut into
+// chunks of whole pixels (all their samples) so the per-sample radiance
+// buffer stays below kWfMaxChunkSamples entries (24 B each).
+constexpr int kWfRing = 4;
+constexpr uint64_t kWfMaxChunkSamples = 1ull << 28;  // 6 GB of radiance (HBM: 288 GB)
+
+static bool use_wavefront(const FlatScene& f) { return !f.bvh.empty() && !getenv("RTGO_MEGAKERNEL"); }
+
+static int wf_capacity(int nl) {
+  int cap = 1 << 21;
+  if (const char* e = getenv("RTGO_WF_PATHS")) cap = std::max(64, std::min(1 << 24, atoi(e)));  // experiments only
+  // soft queue: capacity * nl * 16 entries of 16 B, at most 2 GB; keys path * nl + light fit 32 bits
+  const long long lim = (1ll << 27) / (16ll * std::max(nl, 1));
+  cap = (int)std::min<long long>(cap, lim);
+  return std::max(64, cap & ~63);
+}
+
+static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings* st, hipStream_t s, bool count) {
+  const FlatScene& f = c->flat;
+  const int nl = (int)f.lights.size();
+  const int cap = wf_capacity(nl);
+  const size_t nlk = (size_t)std::max(nl, 1);
+  // one allocation: two path arrays | hit records | per-light state | queues
+  const size_t path_bytes = (size_t)cap * (12 * sizeof(double) + sizeof(uint64_t) + 2 * sizeof(uint32_t));
+  const size_t hit_bytes = (size_t)cap * (7 * sizeof(double) + 2 * sizeof(int32_t));
+  const size_t light_bytes = (size_t)cap * nlk * (2 * sizeof(uint32_t) + 16 * 4 * sizeof(uint32_t));
+  const size_t need = 2 * path_bytes + hit_bytes + light_bytes + 4096;
+  if (need > c->wf_mem_bytes) {
+    if (c->wf_mem) HIP_TRY(hipFree(c->wf_mem));
+    c->wf_mem = nullptr;
+    c->wf_mem_bytes = 0;
+    HIP_TRY(hipMalloc(&c->wf_mem, need));
+    c->wf_mem_bytes = need;
+  }
+  if (!c->wf_ctl) {
+    HIP_TRY(hipMalloc((void**)&c->wf_ctl, sizeof(WfCtl)));
+    HIP_TRY(hipHostMalloc((void**)&c->wf_host, kWfRing * sizeof(WfCtl), hipHostMallocDefault));
+    for (hipEvent_t& e : c->wf_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  const int local = rt_tiles_for_rank(kp.W, kp.H, kp.rank, kp.world);
+  const uint64_t local_px = (uint64_t)local * 1024;
+  const uint64_t spp = (uint64_t)std::max(st->samples, 1);
+  uint64_t max_chunk = kWfMaxChunkSamples;
+  if (const char* e = getenv("RTGO_WF_CHUNK")) max_chunk = std::max(1ll, std::min(atoll(e), (long long)max_chunk));  // tests
+  const uint64_t chunk_px = std::max<uint64_t>(1, std::min<uint64_t>(local_px, max_chunk / spp));
+  const size_t rad_need = (size_t)(chunk_px * spp * 3 * sizeof(double));
+  if (rad_need > c->wf_rad_bytes) {
+    if (c->wf_rad) HIP_TRY(hipFree(c->wf_rad));
+    c->wf_rad = nullptr;
+    c->wf_rad_bytes = 0;
+    HIP_TRY(hipMalloc(&c->wf_rad, rad_need));
+    c->wf_rad_bytes = rad_need;
+  }
+  WfParams p;
+  memset(&p, 0, sizeof p);
+  p.g = Geo{kp.spheres, kp.tris, kp.boxes, kp.bvh, kp.ns, kp.nt, kp.use_bvh, kp.nb};
+  p.mats = kp.mats;
+  p.lights = kp.lights;
+  p.nl = nl;
+  p.max_depth = kp.max_depth;
+  p.recursive = kp.recursive;
+  p.soft = kp.soft;
+  p.spp = st->samples;  // (0: the mean is 0/0 = NaN, as DivScalar(0) in Go)
+  p.W = kp.W;
+  p.H = kp.H;
+  p.rank = kp.rank;
+  p.world = kp.world;
+  p.tiles_x = kp.tiles_x;
+  p.ntiles = kp.ntiles;
+  p.layout = kp.layout;
+  p.stack_depth = kp.stack_depth;
+  p.capacity = cap;
+  memcpy(p.cam, kp.cam, sizeof p.cam);
+  p.aspect = kp.aspect;
+  p.seed_key = kp.seed_key;
+  p.ctl = c->wf_ctl;
+  p.counts = kp.counts;
+  p.out_linear = kp.out_linear;
+  p.out_rgba = kp.out_rgba;
+  p.rad = (double*)c->wf_rad;
+  {
+    char* m = (char*)c->wf_mem;
+    auto take = [&](size_t bytes) {
+      char* r = m;
+      m += (bytes + 255) & ~size_t(255);
+      return (void*)r;
+    };
+    for (WfPaths* a : {&p.cur, &p.next}) {
+      double** dd[12] = {&a->ox, &a->oy, &a->oz, &a->dx, &a->dy, &a->dz,
+                         &a->tx, &a->ty, &a->tz, &a->lx, &a->ly, &a->lz};
+      for (double** q : dd) *q = (double*)take(cap * sizeof(double));
+      a->rng = (uint64_t*)take(cap * sizeof(uint64_t));
+      a->sid = (uint32_t*)take(cap * sizeof(uint32_t));
+      a->depth = (int32_t*)take(cap * sizeof(int32_t));
+    }
+    p.hidx = (int32_t*)take(cap * sizeof(int32_t));
+    p.hnum = (double*)take(cap * sizeof(double));
+    double** hh[6] = {&p.px, &p.py, &p.pz, &p.nx, &p.ny, &p.nz};
+    for (double** q : hh) *q = (double*)take(cap * sizeof(double));
+    p.hinfo = (int32_t*)take(cap * sizeof(int32_t));
+    p.lstate = (uint32_t*)take(cap * nlk * sizeof(uint32_t));
+    p.hardq = (uint32_t*)take(cap * nlk * sizeof(uint32_t));
+    p.softq = (uint32_t*)take(cap * nlk * 16 * 4 * sizeof(uint32_t));
+    if ((size_t)(m - (char*)c->wf_mem) > c->wf_mem_bytes) {
+      set_error("wavefront buffer layout overflow");
+      return RT_E_NOMEM;
+    }
+  }
+  auto fail = [&](int e, const char* what) {
+    set_error(std::string("wavefront ") + what + " failed: " + hipGetErrorString((hipError_t)e));
+    return RT_E_DEVICE;
+  };
+  for (uint64_t lp0 = 0; lp0 < local_px; lp0 += chunk_px) {
+    const uint64_t npx = std::min(chunk_px, local_px - lp0);
+    p.lp0 = (uint32_t)lp0;
+    WfCtl init;
+    memset(&init, 0, sizeof init);
+    init.total = npx * spp;
+    HIP_TRY(hipMemcpyAsync(c->wf_ctl, &init, sizeof init, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(p.rad, 0, (size_t)(npx * spp * 3 * sizeof(double)), s));
+    if (st->samples > 0) {
+      // initial fill, then iterations until every sample has finished; the
+      // host reads the loop state one iteration behind the GPU
+      int e = wf_launch_regen(p, count, s);
+      if (e) return fail(e, "regen launch");
+      std::swap(p.cur, p.next);
+      const long long max_iter = (long long)init.total + std::max(kp.max_depth, 0) + 8;
+      for (long long it = 0;; ++it) {
+        if (it > max_iter) {
+          set_error("wavefront loop did not terminate");
+          return RT_E_DEVICE;
+        }
+        e = wf_launch_iteration(p, count, s);
+        if (e) return fail(e, "iteration launch");
+        e = wf_launch_regen(p, count, s);
+        if (e) return fail(e, "regen launch");
+        std::swap(p.cur, p.next);
+        const int r = (int)(it % kWfRing);
+        HIP_TRY(hipMemcpyAsync(c->wf_host + r, c->wf_ctl, sizeof(WfCtl), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipEventRecord(c->wf_ev[r], s));
+        if (it >= 1) {
+          const int pr = (int)((it - 1) % kWfRing);
+          HIP_TRY(hipEventSynchronize(c->wf_ev[pr]));
+          const WfCtl& h = c->wf_host[pr];
+          if (h.n_cur == 0 && h.next_sample >= h.total) break;  // iteration `it` had nothing to do
+        }
+      }
+    }
+    int e = wf_launch_resolve(p, (int)npx, s);
+    if (e) return fail(e, "resolve launch");
+  }
+  return RT_OK;
+}
+
 int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settings* st, int32_t rank,
                             int32_t world, int32_t layout, float* d_linear, uint8_t* d_rgba, void* stream,
                             rt_counts* counts) {
@@ -688,8 +858,11 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
     p.stack_off = (p.stage_bytes + 15) & ~15;
     p.stack_depth = std::max(1, f.bvh_depth);
   }
-  rc = prepare_schedule(c, &p, st);
-  if (rc) return rc;
+  const bool wf = use_wavefront(f);
+  if (!wf) {
+    rc = prepare_schedule(c, &p, st);
+    if (rc) return rc;
+  }
   p.num_wgs = p.num_blocks;
   if (const char* e = getenv("RTGO_PRIO")) p.prio_blocks = atoi(e);  // experiments only
   if (const char* e = getenv("RTGO_MAX_BLOCKS"))  // experiments only: the first N blocks (partial image)
@@ -697,13 +870,18 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   // the caller's stream, as given (NULL = the legacy default stream)
   hipStream_t s = (hipStream_t)stream;
   if (counts) HIP_TRY(hipMemsetAsync(c->d_counts, 0, 16 * sizeof(unsigned long long), s));
-  if (c->nsplit)  // split pixels: hit bits and sub-block counters start at zero
+  if (!wf && c->nsplit)  // split pixels: hit bits and sub-block counters start at zero
     HIP_TRY(hipMemsetAsync(p.split_hits, 0, split_flags_bytes(c->nsplit, st->samples), s));
   HIP_TRY(hipEventRecord(c->ev0, s));
-  int e = launch_render(p, counts != nullptr, s);
-  if (e != hipSuccess) {
-    set_error(std::string("render launch failed: ") + hipGetErrorString((hipError_t)e));
-    return RT_E_DEVICE;
+  if (wf) {
+    rc = render_wavefront(c, p, st, s, counts != nullptr);
+    if (rc) return rc;
+  } else {
+    int e = launch_render(p, counts != nullptr, s);
+    if (e != hipSuccess) {
+      set_error(std::string("render launch failed: ") + hipGetErrorString((hipError_t)e));
+      return RT_E_DEVICE;
+    }
   }
   HIP_TRY(hipEventRecord(c->ev1, s));
   c->last_stream = s;

@@ -268,14 +268,6 @@ __device__ __forceinline__ d3 inv_dir(d3 d) {
   return mk(1.0 / (d.x != 0 ? d.x : 1e-300), 1.0 / (d.y != 0 ? d.y : 1e-300), 1.0 / (d.z != 0 ? d.z : 1e-300));
 }
 
-// The geometry an occlusion query needs (a small by-value subset of KParams).
-struct Geo {
-  const DSphere* spheres;
-  const DTri* tris;
-  const DBox* boxes;  // one per cube: its 12 consecutive triangles
-  const DBVHNode* bvh;
-  int32_t ns, nt, use_bvh, nb;
-};
 
 // Can the ray meet the (padded) box within [tmin, tmax]?  Conservative:
 // slab test with the same slack as box_hit; `id` from inv_dir().
@@ -536,6 +528,75 @@ __device__ __forceinline__ Scat scatter(const DMat* __restrict__ m, d3 d, d3 N, 
     r.nd = refl;
   }
   return r;
+}
+
+// ------------------------------------------------------------ camera
+// Launch-uniform inputs of the camera rays (getRay, renderer.go:377-390).
+struct CamK {
+  uint64_t key;
+  uint32_t W;
+  double dW, dH, vw, llcx, llcy, llcz, ox, oy, oz;
+  double rW, rH;  // refined reciprocals of dW, dH (div_by)
+};
+// The compiler's binary64 division n / d is v_div_scale (n and d), v_rcp_f64,
+// two Newton steps on the reciprocal, q = n*r, the residual fma, v_div_fmas
+// and v_div_fixup.  For the camera jitter n = x + rand is in [0, W) with
+// rand a multiple of 2^-32 (so n is 0 or at least 2^-32) and d = W or H is
+// an integer in [1, 2^16]: v_div_scale scales nothing, v_div_fmas is a plain
+// fma and v_div_fixup returns its input, so the sequence is the three
+// operations below with the reciprocal refinement done once per block, and
+// the quotient is the IEEE one bit for bit (validate_settings bounds W, H).
+__device__ __forceinline__ double refined_rcp(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+__device__ __forceinline__ double div_by(double n, double d, double r) {
+  const double q = n * r;
+  return __builtin_fma(__builtin_fma(-d, q, n), r, q);
+}
+template <bool kCount>
+__device__ __forceinline__ void camera_ray_c(const CamK& ck, int x, int y, int s, rt_rng& rng, d3& o, d3& d,
+                                             Counters& c) {
+  rt_rng_init(&rng, ck.key, (uint32_t)y * ck.W + (uint32_t)x, (uint32_t)s);
+  const double u = div_by((double)x + draw<kCount>(rng, c), ck.dW, ck.rW);
+  const double v = div_by((double)y + draw<kCount>(rng, c), ck.dH, ck.rH);
+  o = mk(ck.ox, ck.oy, ck.oz);
+  d = mk(((ck.llcx + ck.vw * u) + 0.0) - o.x, ((ck.llcy + 0.0) + 2.0 * v) - o.y, ((ck.llcz + 0.0) + 0.0) - o.z);
+}
+
+__device__ __forceinline__ CamK make_cam(uint64_t seed_key, int W, int H, double aspect, double cx, double cy,
+                                         double cz) {
+  CamK r;
+  r.key = seed_key;
+  r.W = (uint32_t)W;
+  r.dW = (double)W;
+  r.dH = (double)H;
+  r.rW = refined_rcp(r.dW);
+  r.rH = refined_rcp(r.dH);
+  // lowerLeftCorner = origin - horizontal/2 - vertical/2 - (0,0,focal)
+  r.vw = 2.0 * aspect;
+  r.llcx = cx - r.vw / 2;
+  r.llcy = cy - 1.0;
+  r.llcz = cz - 1.0;
+  r.ox = cx;
+  r.oy = cy;
+  r.oz = cz;
+  return r;
+}
+
+// ------------------------------------------------------------ pixel output
+// toneMap (renderer.go:348-367) then Vec3.ToRGB (vector.go:106-109) of a
+// pixel's mean radiance: opaque RGBA8.
+__device__ __forceinline__ uint32_t tonemap_rgba8(double mx, double my, double mz) {
+  const double g = 1.0 / 2.2;
+  const double tx_ = clamp01(pow_gamma(1.0 - exp(-(mx * 1.0)), g));
+  const double ty_ = clamp01(pow_gamma(1.0 - exp(-(my * 1.0)), g));
+  const double tz_ = clamp01(pow_gamma(1.0 - exp(-(mz * 1.0)), g));
+  return go_u8(clamp01(tx_) * 255) | (go_u8(clamp01(ty_) * 255) << 8) | (go_u8(clamp01(tz_) * 255) << 16) |
+         (255u << 24);
 }
 
 }  // namespace rtgo

@@ -107,6 +107,64 @@ size_t render_shmem(const KParams& p);
 int launch_unpack(int32_t W, int32_t H, int32_t world, int32_t max_local, const float* pl, const uint8_t* pr,
                   float* ol, uint8_t* orgba, void* stream);
 
+// The geometry an occlusion / closest-hit query needs (device pointers).
+struct Geo {
+  const DSphere* spheres;
+  const DTri* tris;
+  const DBox* boxes;  // one per cube: its 12 consecutive triangles
+  const DBVHNode* bvh;
+  int32_t ns, nt, use_bvh, nb;
+};
+
+// ---------------------------------------------------------------- wavefront path
+// (rt_wavefront.hip: BVH scenes)
+struct WfCtl {               // device-resident loop state
+  int32_t n_cur;             // live paths in the current array
+  int32_t n_next;            // paths appended to the next array (shade2, then regen)
+  int32_t n_hard;            // hard shadow jobs queued
+  int32_t n_soft;            // soft shadow jobs queued (16 per owner)
+  int32_t regen_cnt;         // samples the coming regen starts
+  int32_t iter;              // completed iterations
+  uint64_t next_sample;      // first sample id of the chunk not started yet
+  uint64_t total;            // sample ids in the chunk
+};
+struct WfPaths {             // structure of arrays, `capacity` entries
+  double *ox, *oy, *oz, *dx, *dy, *dz;  // ray
+  double *tx, *ty, *tz, *lx, *ly, *lz;  // throughput, radiance so far
+  uint64_t* rng;             // stream state
+  uint32_t* sid;             // sample id within the chunk (local pixel * spp + sample)
+  int32_t* depth;
+};
+struct WfParams {
+  Geo g;
+  const DMat* mats;
+  const DLight* lights;
+  int32_t nl, max_depth, recursive, soft, spp;
+  int32_t W, H, rank, world, tiles_x, ntiles, layout;
+  int32_t stack_depth;       // BVH stack entries per lane (the tree's depth)
+  int32_t capacity;          // path slots per array
+  uint32_t lp0;              // first local pixel of the chunk (local tile * 1024 + pixel in tile)
+  double cam[3];
+  double aspect;
+  uint64_t seed_key;
+  WfPaths cur, next;
+  WfCtl* ctl;
+  int32_t* hidx;             // per current path: sphere hit (-1: none)
+  double* hnum;              // ... and its root numerator
+  double *px, *py, *pz, *nx, *ny, *nz;  // hit point and normal
+  int32_t* hinfo;            // material << 1 | front face
+  uint32_t* lstate;          // [path][light]: kHardBit | blocked soft rays
+  uint32_t* hardq;           // path * nl + light
+  uint32_t* softq;           // 4 words per entry: {path * nl + light, raw draws x, y, z}
+  double* rad;               // [sample id][3] radiance
+  unsigned long long* counts;
+  float* out_linear;
+  uint8_t* out_rgba;
+};
+int wf_launch_regen(const WfParams& p, bool count, void* stream);
+int wf_launch_iteration(const WfParams& p, bool count, void* stream);
+int wf_launch_resolve(const WfParams& p, int npix, void* stream);
+
 // ---------------------------------------------------------------- output
 double go_pow_tonemap(double x);  // Pow(x, 1/2.2) with Go's special cases
 void tonemap_to_rgba(const double c[3], uint8_t out[4]);

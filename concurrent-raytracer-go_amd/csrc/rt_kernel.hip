@@ -474,57 +474,8 @@ __device__ __forceinline__ Hot hot() {
 // (renderer.go:377-390).  Leaves `rng` after those two draws.  CamK holds
 // the launch-uniform inputs; phase 1 loads it once per block (SGPRs), the
 // shading loop rebuilds it from the kernarg segment where it needs it.
-struct CamK {
-  uint64_t key;
-  uint32_t W;
-  double dW, dH, vw, llcx, llcy, llcz, ox, oy, oz;
-  double rW, rH;  // refined reciprocals of dW, dH (div_by)
-};
-// The compiler's binary64 division n / d is v_div_scale (n and d), v_rcp_f64,
-// two Newton steps on the reciprocal, q = n*r, the residual fma, v_div_fmas
-// and v_div_fixup.  For the camera jitter n = x + rand is in [0, W) with
-// rand a multiple of 2^-32 (so n is 0 or at least 2^-32) and d = W or H is
-// an integer in [1, 2^16]: v_div_scale scales nothing, v_div_fmas is a plain
-// fma and v_div_fixup returns its input, so the sequence is the three
-// operations below with the reciprocal refinement done once per block, and
-// the quotient is the IEEE one bit for bit (validate_settings bounds W, H).
-__device__ __forceinline__ double refined_rcp(double d) {
-  double r = __builtin_amdgcn_rcp(d);
-  double e = __builtin_fma(-d, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  e = __builtin_fma(-d, r, 1.0);
-  return __builtin_fma(r, e, r);
-}
-__device__ __forceinline__ double div_by(double n, double d, double r) {
-  const double q = n * r;
-  return __builtin_fma(__builtin_fma(-d, q, n), r, q);
-}
 __device__ __forceinline__ CamK cam_k(KArg k) {
-  CamK r;
-  r.key = k->seed_key;
-  r.W = (uint32_t)k->W;
-  r.dW = (double)k->W;
-  r.dH = (double)k->H;
-  r.rW = refined_rcp(r.dW);
-  r.rH = refined_rcp(r.dH);
-  // lowerLeftCorner = origin - horizontal/2 - vertical/2 - (0,0,focal)
-  r.vw = 2.0 * k->aspect;
-  r.llcx = k->cam[0] - r.vw / 2;
-  r.llcy = k->cam[1] - 1.0;
-  r.llcz = k->cam[2] - 1.0;
-  r.ox = k->cam[0];
-  r.oy = k->cam[1];
-  r.oz = k->cam[2];
-  return r;
-}
-template <bool kCount>
-__device__ __forceinline__ void camera_ray_c(const CamK& ck, int x, int y, int s, rt_rng& rng, d3& o, d3& d,
-                                             Counters& c) {
-  rt_rng_init(&rng, ck.key, (uint32_t)y * ck.W + (uint32_t)x, (uint32_t)s);
-  const double u = div_by((double)x + draw<kCount>(rng, c), ck.dW, ck.rW);
-  const double v = div_by((double)y + draw<kCount>(rng, c), ck.dH, ck.rH);
-  o = mk(ck.ox, ck.oy, ck.oz);
-  d = mk(((ck.llcx + ck.vw * u) + 0.0) - o.x, ((ck.llcy + 0.0) + 2.0 * v) - o.y, ((ck.llcz + 0.0) + 0.0) - o.z);
+  return make_cam(k->seed_key, k->W, k->H, k->aspect, k->cam[0], k->cam[1], k->cam[2]);
 }
 template <bool kCount>
 __device__ __forceinline__ void camera_ray(KArg k, int x, int y, int s, rt_rng& rng, d3& o, d3& d, Counters& c) {
@@ -1091,14 +1042,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
         k->out_linear[oi * 3 + 2] = (float)mz;
       }
       if (k->out_rgba) {
-        // toneMap (renderer.go:348-367) then Vec3.ToRGB (vector.go:106-109)
-        const double g = 1.0 / 2.2;
-        const double tx_ = clamp01(pow_gamma(1.0 - exp(-(mx * 1.0)), g));
-        const double ty_ = clamp01(pow_gamma(1.0 - exp(-(my * 1.0)), g));
-        const double tz_ = clamp01(pow_gamma(1.0 - exp(-(mz * 1.0)), g));
-        const uint32_t px4 = go_u8(clamp01(tx_) * 255) | (go_u8(clamp01(ty_) * 255) << 8) |
-                             (go_u8(clamp01(tz_) * 255) << 16) | (255u << 24);
-        *reinterpret_cast<uint32_t*>(k->out_rgba + oi * 4) = px4;
+        *reinterpret_cast<uint32_t*>(k->out_rgba + oi * 4) = tonemap_rgba8(mx, my, mz);
       }
     }
   }
