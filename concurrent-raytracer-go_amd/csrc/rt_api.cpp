@@ -655,25 +655,32 @@ constexpr uint64_t kWfMaxChunkSamples = 1ull << 28;  // 6 GB of radiance (HBM: 2
 
 static bool use_wavefront(const FlatScene& f) { return !f.bvh.empty() && !getenv("RTGO_MEGAKERNEL"); }
 
-static int wf_capacity(int nl) {
-  int cap = 1 << 21;
-  if (const char* e = getenv("RTGO_WF_PATHS")) cap = std::max(64, std::min(1 << 24, atoi(e)));  // experiments only
-  // soft queue: capacity * nl * 16 entries of 16 B, at most 2 GB; keys path * nl + light fit 32 bits
-  const long long lim = (1ll << 27) / (16ll * std::max(nl, 1));
-  cap = (int)std::min<long long>(cap, lim);
-  return std::max(64, cap & ~63);
+// path slots per shard (a multiple of kWfBlockSlots: every shard receives the
+// survivors of the workgroups b % kWfShards == shard, at most shard_cap);
+// RTGO_WF_PATHS: tests and experiments only
+static int wf_shard_cap(int nl) {
+  long long cap = 1 << 21;
+  if (const char* e = getenv("RTGO_WF_PATHS")) cap = std::max(1ll, std::min(1ll << 24, atoll(e)));
+  // soft queues: cap * nl * 16 entries of 16 B, at most 2 GB; keys slot * nl + light fit 32 bits
+  cap = std::min<long long>(cap, (1ll << 27) / (16ll * std::max(nl, 1)));
+  const long long per = kWfShards * kWfBlockSlots;
+  return (int)(std::max(1ll, cap / per) * kWfBlockSlots);
 }
 
 static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings* st, hipStream_t s, bool count) {
   const FlatScene& f = c->flat;
   const int nl = (int)f.lights.size();
-  const int cap = wf_capacity(nl);
+  const int shard_cap = wf_shard_cap(nl);
+  const size_t cap = (size_t)shard_cap * kWfShards;
   const size_t nlk = (size_t)std::max(nl, 1);
+  const size_t qcap = cap * nlk;  // hard rays per shard: at most every light of every path of its workgroups
   // one allocation: two path arrays | hit records | per-light state | queues
-  const size_t path_bytes = (size_t)cap * (12 * sizeof(double) + sizeof(uint64_t) + 2 * sizeof(uint32_t));
-  const size_t hit_bytes = (size_t)cap * (7 * sizeof(double) + 2 * sizeof(int32_t));
-  const size_t light_bytes = (size_t)cap * nlk * (2 * sizeof(uint32_t) + 16 * 4 * sizeof(uint32_t));
-  const size_t need = 2 * path_bytes + hit_bytes + light_bytes + 4096;
+  const size_t need = 2 * cap * (12 * 8 + 8 + 4 + 4)   // path arrays
+                      + cap * (7 * 8 + 4 + 4)           // hit numerator, point, normal, info, index
+                      + cap * nlk * 4                   // lstate
+                      + (size_t)kWfShards * qcap * 4    // hard queues
+                      + (size_t)kWfShards * qcap * 16 * 16  // soft queues
+                      + 64 * 256;                       // alignment
   if (need > c->wf_mem_bytes) {
     if (c->wf_mem) HIP_TRY(hipFree(c->wf_mem));
     c->wf_mem = nullptr;
@@ -718,7 +725,9 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   p.ntiles = kp.ntiles;
   p.layout = kp.layout;
   p.stack_depth = kp.stack_depth;
-  p.capacity = cap;
+  p.shard_cap = shard_cap;
+  p.hard_cap = (int64_t)qcap;
+  p.soft_cap = (int64_t)qcap * 16;
   memcpy(p.cam, kp.cam, sizeof p.cam);
   p.aspect = kp.aspect;
   p.seed_key = kp.seed_key;
@@ -742,14 +751,14 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
       a->sid = (uint32_t*)take(cap * sizeof(uint32_t));
       a->depth = (int32_t*)take(cap * sizeof(int32_t));
     }
-    p.hidx = (int32_t*)take(cap * sizeof(int32_t));
     p.hnum = (double*)take(cap * sizeof(double));
     double** hh[6] = {&p.px, &p.py, &p.pz, &p.nx, &p.ny, &p.nz};
     for (double** q : hh) *q = (double*)take(cap * sizeof(double));
     p.hinfo = (int32_t*)take(cap * sizeof(int32_t));
+    p.hidx = (int32_t*)take(cap * sizeof(int32_t));
     p.lstate = (uint32_t*)take(cap * nlk * sizeof(uint32_t));
-    p.hardq = (uint32_t*)take(cap * nlk * sizeof(uint32_t));
-    p.softq = (uint32_t*)take(cap * nlk * 16 * 4 * sizeof(uint32_t));
+    p.hardq = (uint32_t*)take((size_t)kWfShards * qcap * sizeof(uint32_t));
+    p.softq = (uint32_t*)take((size_t)kWfShards * qcap * 16 * 4 * sizeof(uint32_t));
     if ((size_t)(m - (char*)c->wf_mem) > c->wf_mem_bytes) {
       set_error("wavefront buffer layout overflow");
       return RT_E_NOMEM;
@@ -762,27 +771,26 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   for (uint64_t lp0 = 0; lp0 < local_px; lp0 += chunk_px) {
     const uint64_t npx = std::min(chunk_px, local_px - lp0);
     p.lp0 = (uint32_t)lp0;
-    WfCtl init;
-    memset(&init, 0, sizeof init);
-    init.total = npx * spp;
-    HIP_TRY(hipMemcpyAsync(c->wf_ctl, &init, sizeof init, hipMemcpyHostToDevice, s));
+    const uint64_t total = npx * (uint64_t)st->samples;
     HIP_TRY(hipMemsetAsync(p.rad, 0, (size_t)(npx * spp * 3 * sizeof(double)), s));
-    if (st->samples > 0) {
-      // initial fill, then iterations until every sample has finished; the
-      // host reads the loop state one iteration behind the GPU
-      int e = wf_launch_regen(p, count, s);
-      if (e) return fail(e, "regen launch");
+    if (total > 0) {
+      WfCtl init;
+      memset(&init, 0, sizeof init);
+      init.total = total;
+      HIP_TRY(hipMemcpyAsync(c->wf_ctl, &init, sizeof init, hipMemcpyHostToDevice, s));
+      // the first samples, then bounces until every sample has finished; the
+      // host reads the loop state one bounce behind the GPU
+      int e = wf_launch_bounce(p, true, count, s);
+      if (e) return fail(e, "launch");
       std::swap(p.cur, p.next);
-      const long long max_iter = (long long)init.total + std::max(kp.max_depth, 0) + 8;
+      const long long max_iter = (long long)total + std::max(kp.max_depth, 0) + 8;
       for (long long it = 0;; ++it) {
         if (it > max_iter) {
           set_error("wavefront loop did not terminate");
           return RT_E_DEVICE;
         }
-        e = wf_launch_iteration(p, count, s);
-        if (e) return fail(e, "iteration launch");
-        e = wf_launch_regen(p, count, s);
-        if (e) return fail(e, "regen launch");
+        e = wf_launch_bounce(p, false, count, s);
+        if (e) return fail(e, "launch");
         std::swap(p.cur, p.next);
         const int r = (int)(it % kWfRing);
         HIP_TRY(hipMemcpyAsync(c->wf_host + r, c->wf_ctl, sizeof(WfCtl), hipMemcpyDeviceToHost, s));
@@ -791,7 +799,7 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
           const int pr = (int)((it - 1) % kWfRing);
           HIP_TRY(hipEventSynchronize(c->wf_ev[pr]));
           const WfCtl& h = c->wf_host[pr];
-          if (h.n_cur == 0 && h.next_sample >= h.total) break;  // iteration `it` had nothing to do
+          if (h.live == 0 && h.dry) break;  // bounce `it` had nothing to do
         }
       }
     }

@@ -118,21 +118,27 @@ struct Geo {
 
 // ---------------------------------------------------------------- wavefront path
 // (rt_wavefront.hip: BVH scenes)
-struct WfCtl {               // device-resident loop state
-  int32_t n_cur;             // live paths in the current array
-  int32_t n_next;            // paths appended to the next array (shade2, then regen)
-  int32_t n_hard;            // hard shadow jobs queued
-  int32_t n_soft;            // soft shadow jobs queued (16 per owner)
-  int32_t regen_cnt;         // samples the coming regen starts
-  int32_t iter;              // completed iterations
-  uint64_t next_sample;      // first sample id of the chunk not started yet
-  uint64_t total;            // sample ids in the chunk
+constexpr int kWfShards = 8;           // queues / path arrays are split in 8 shards (one atomic word each)
+constexpr int kWfBlockSlots = 256;     // threads per workgroup of the wavefront kernels
+constexpr uint32_t kDeadSid = 0xFFFFFFFFu;  // a slot with no sample (out-of-image pixel of an edge tile)
+struct WfCtl {                 // device-resident loop state; counters of shard s at [32 s] (own 128-B line)
+  int32_t cur_cnt[kWfShards * 32];   // live paths per shard of the current array
+  int32_t next_cnt[kWfShards * 32];  // survivors appended per shard of the next array
+  int32_t hard_cnt[kWfShards * 32];  // hard shadow rays queued per shard
+  int32_t soft_cnt[kWfShards * 32];  // soft shadow rays queued per shard
+  int32_t job_head[3][kWfShards * 32];  // persistent kernels (extend, hard, soft): jobs taken per range
+  unsigned long long next_sample;    // first sample id of the chunk not started yet
+  unsigned long long total;          // sample ids in the chunk
+  int32_t live;                // live paths after the last bounce (wf_book)
+  int32_t dry;                 // every sample started
+  int32_t iter;                // bounces done
+  int32_t pad;
 };
-struct WfPaths {             // structure of arrays, `capacity` entries
+struct WfPaths {             // structure of arrays, kWfShards * shard_cap slots
   double *ox, *oy, *oz, *dx, *dy, *dz;  // ray
   double *tx, *ty, *tz, *lx, *ly, *lz;  // throughput, radiance so far
   uint64_t* rng;             // stream state
-  uint32_t* sid;             // sample id within the chunk (local pixel * spp + sample)
+  uint32_t* sid;             // sample id within the chunk (local pixel * spp + sample), kDeadSid: none
   int32_t* depth;
 };
 struct WfParams {
@@ -142,27 +148,27 @@ struct WfParams {
   int32_t nl, max_depth, recursive, soft, spp;
   int32_t W, H, rank, world, tiles_x, ntiles, layout;
   int32_t stack_depth;       // BVH stack entries per lane (the tree's depth)
-  int32_t capacity;          // path slots per array
+  int32_t shard_cap;         // path slots per shard
+  int64_t hard_cap, soft_cap;  // queue entries per shard
   uint32_t lp0;              // first local pixel of the chunk (local tile * 1024 + pixel in tile)
   double cam[3];
   double aspect;
   uint64_t seed_key;
   WfPaths cur, next;
   WfCtl* ctl;
-  int32_t* hidx;             // per current path: sphere hit (-1: none)
-  double* hnum;              // ... and its root numerator
+  int32_t* hidx;             // per slot of the current array: sphere hit (-1: none)
+  double* hnum;              // ... its root numerator
   double *px, *py, *pz, *nx, *ny, *nz;  // hit point and normal
   int32_t* hinfo;            // material << 1 | front face
-  uint32_t* lstate;          // [path][light]: kHardBit | blocked soft rays
-  uint32_t* hardq;           // path * nl + light
-  uint32_t* softq;           // 4 words per entry: {path * nl + light, raw draws x, y, z}
+  uint32_t* lstate;          // [slot][light]: kHardBit | blocked soft rays
+  uint32_t* hardq;           // kWfShards queues of hard_cap entries: slot * nl + light
+  uint32_t* softq;           // kWfShards queues of soft_cap entries, 4 words: {slot * nl + light, draws x, y, z}
   double* rad;               // [sample id][3] radiance
   unsigned long long* counts;
   float* out_linear;
   uint8_t* out_rgba;
 };
-int wf_launch_regen(const WfParams& p, bool count, void* stream);
-int wf_launch_iteration(const WfParams& p, bool count, void* stream);
+int wf_launch_bounce(const WfParams& p, bool first, bool count, void* stream);
 int wf_launch_resolve(const WfParams& p, int npix, void* stream);
 
 // ---------------------------------------------------------------- output

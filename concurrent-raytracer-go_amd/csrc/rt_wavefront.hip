@@ -1,37 +1,43 @@
 // rt_wavefront.hip — the wavefront path for BVH scenes (> 64 spheres, configs
-// C4/C5: 10k spheres).
+// C4/C5: 10k spheres).  DESIGN.md §4.2.
 //
 // The megakernel (rt_kernel.hip) keeps a whole path in one lane: its binary64
 // path state costs 168 VGPRs, so a SIMD holds 3 waves, and on a 10k-sphere
-// scene every BVH traversal is a chain of dependent L2 loads that 3 waves
-// cannot hide (C4: 1.4 s, lanes mostly waiting).  Here the bounce loop of
-// traceRay (internal/renderer/renderer.go:165-227) is cut into stages, each a
-// small kernel over a compacted array of live paths in HBM:
+// scene its lanes spend most of the time masked off while the longest
+// traversal of the wave finishes.  Here traceRay's bounce loop
+// (internal/renderer/renderer.go:165-227) is cut into kernels over dense,
+// sharded arrays of live paths and shadow rays in HBM:
 //
-//   regen    new camera samples fill the free slots (tracePixel's jitter and
-//            getRay, renderer.go:150-163,377-390)
-//   extend   closest hit of every live path (hitWorld, renderer.go:333-346,
-//            through the BVH); a miss or the depth cut-off ends the path
-//   shade1   the HitRecord (sphere.go:42-58) and one hard shadow ray per light
-//            (calculateSmartShadow, renderer.go:299-305) into a queue
-//   hard     any-hit of the hard shadow rays
-//   softgen  per light whose hard ray is clear, in light order, the 16
-//            RandomVec3InUnitSphere points (renderer.go:311-318) into a queue
-//   soft     any-hit of the soft rays, counted per (path, light)
-//   shade2   calculateDirectLighting (renderer.go:229-297) with those counts,
-//            Material.Scatter, the traceRay combination; survivors are
-//            compacted into the next path array (wave ballot + one atomic)
+//   extend    closest hit of every live path (hitWorld, renderer.go:333-346,
+//             through the BVH); a miss or the depth cut-off ends the path
+//   shade1    the HitRecord (sphere.go:42-58); one hard shadow ray per lit
+//             light (calculateSmartShadow, renderer.go:299-305) queued
+//   occlude   any-hit of the hard rays
+//   softgen   per light whose hard ray is clear, in light order, the 16
+//             RandomVec3InUnitSphere points (renderer.go:311-318) queued as
+//             16 consecutive soft rays
+//   occlude   any-hit of the soft rays, blocked ones counted per (path, light)
+//   shade     calculateDirectLighting (renderer.go:229-297) with those counts,
+//             Material.Scatter, the traceRay combination; survivors appended
+//             to the next path array, finished paths write their radiance
+//   regen     free slots of the next array take new camera samples
+//             (tracePixel / getRay, renderer.go:150-163,377-390)
 //
-// The traversal kernels need few registers (8 waves per SIMD instead of 3),
-// every stage runs on full waves, and the 16 soft rays of one point sit in 16
-// adjacent lanes (a coherent packet).  The arithmetic is the megakernel's
-// (rt_device.h), each path consumes its RNG stream in the reference's order
-// (soft-shadow draws light by light, then the scatter draws), and each sample's
-// radiance lands in its own slot; resolve sums a pixel's samples in sample
-// order (tracePixel) — so images are bit-identical to the megakernel's and the
-// oracle's.  The loop is host-driven with device-side counts: every kernel
-// reads its item count from WfCtl, and the host only polls a copy of WfCtl
-// one iteration behind to know when the frame is done.
+// extend and occlude are PERSISTENT traversal kernels: each wave owns a range
+// of jobs and refills idle lanes from it as rays finish (Aila & Laine's
+// persistent while-while traversal with dynamic fetch), so waves stay full
+// instead of waiting for their longest ray.  Appends aggregate per workgroup
+// and go to one of kWfShards queues (a workgroup's shard = its index mod
+// kWfShards): one atomic per workgroup and queue, spread over 8 words.
+//
+// The arithmetic is the megakernel's (rt_device.h).  Each path consumes its
+// RNG stream in the reference's order (hard rays draw nothing; soft-shadow
+// draws light by light, then the scatter draws), and each sample's radiance
+// lands in its own slot of a per-frame buffer; resolve sums every pixel's
+// samples in sample order (tracePixel) — so images are bit-identical to the
+// megakernel's and the oracle's (tests/test_gpu_wavefront.py).  The loop is
+// host-driven: the book kernel publishes the live count, and the host polls
+// a copy of it one bounce behind the GPU to know when the frame is done.
 #include <hip/hip_runtime.h>
 
 #include "../../include/rt_rng.h"
@@ -40,7 +46,9 @@
 
 namespace rtgo {
 
-constexpr int kWfBlock = 256;           // threads per workgroup of every stage
+constexpr int kWfBlock = kWfBlockSlots;  // threads per workgroup of every kernel
+constexpr int kRefill = 16;              // persistent traversal: refill once this many lanes are idle
+constexpr int kChunk = 256;              // persistent traversal: jobs a wave takes per atomic
 constexpr uint32_t kHardBit = 1u << 16;  // lstate: the hard shadow ray is blocked (low bits: blocked soft rays)
 
 extern __shared__ __attribute__((aligned(16))) unsigned char wf_lds[];
@@ -51,17 +59,62 @@ __device__ __forceinline__ int* wf_stack(int depth) {
   return reinterpret_cast<int*>(wf_lds) + (threadIdx.x >> 6) * 64 * depth + (threadIdx.x & 63);
 }
 
-// Append `want` (per lane) items to a queue: one atomic per wave; returns the
-// lane's first index.
-__device__ __forceinline__ int wave_append(int* counter, bool want, int per = 1) {
-  const unsigned long long m = __ballot(want);
-  if (m == 0) return 0;
-  const int lane = (int)(threadIdx.x & 63);
-  const int leader = __builtin_ctzll(m);
-  int base = 0;
-  if (lane == leader) base = atomicAdd(counter, per * __popcll(m));
-  base = __shfl(base, leader);
-  return base + per * __popcll(m & ((1ull << lane) - 1ull));
+// Block-wide exclusive prefix of a per-lane count over the workgroup (wave
+// scans, one LDS word per wave); sets `total`.  Every thread must call it.
+__device__ __forceinline__ int block_prefix(int v, int* s_wave, int& total) {
+  const int lane = (int)(threadIdx.x & 63), w = (int)(threadIdx.x >> 6);
+  int incl = v;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t = __shfl_up(incl, off);
+    if (lane >= off) incl += t;
+  }
+  if (lane == 63) s_wave[w] = incl;
+  __syncthreads();
+  int before = 0;
+  total = 0;
+  for (int k = 0; k < kWfBlock / 64; ++k) {
+    const int x = s_wave[k];
+    before += k < w ? x : 0;
+    total += x;
+  }
+  __syncthreads();  // s_wave is reused by the next call
+  return before + incl - v;
+}
+
+// Append `v` entries per thread to the workgroup's shard of a sharded queue:
+// one atomic per workgroup; returns this thread's first entry index within
+// the shard.  Every thread must call it.
+__device__ __forceinline__ int block_append(int v, int32_t* shard_cnt, int* s_wave, int* s_base) {
+  int total;
+  const int before = block_prefix(v, s_wave, total);
+  if (threadIdx.x == 0 && total > 0) *s_base = atomicAdd(shard_cnt, total);
+  __syncthreads();
+  return *s_base + before;
+}
+
+// Dense index over the kWfShards shards of an array or queue (counts at
+// cnt[32 s]): start[s] = entries before shard s.  Constant indices only, so
+// start[] stays in registers.
+struct Dense {
+  int start[kWfShards + 1];
+};
+__device__ __forceinline__ Dense dense(const int32_t* cnt) {
+  Dense d;
+  d.start[0] = 0;
+#pragma unroll
+  for (int s = 0; s < kWfShards; ++s) d.start[s + 1] = d.start[s] + cnt[s * 32];
+  return d;
+}
+// entry j (< total) -> physical index shard * cap + offset
+__device__ __forceinline__ size_t dense_at(const Dense& d, int j, size_t cap) {
+  int s = 0, off = 0;
+#pragma unroll
+  for (int k = 1; k < kWfShards; ++k)
+    if (j >= d.start[k]) {
+      s = k;
+      off = d.start[k];
+    }
+  return (size_t)s * cap + (size_t)(j - off);
 }
 
 template <bool kCount>
@@ -75,8 +128,8 @@ __device__ __forceinline__ void flush_counts(const WfParams& p, Counters& c) {
   }
 }
 
-__device__ __forceinline__ d3 ld_o(const WfPaths& a, int i) { return mk(a.ox[i], a.oy[i], a.oz[i]); }
-__device__ __forceinline__ d3 ld_d(const WfPaths& a, int i) { return mk(a.dx[i], a.dy[i], a.dz[i]); }
+__device__ __forceinline__ d3 ld_o(const WfPaths& a, size_t i) { return mk(a.ox[i], a.oy[i], a.oz[i]); }
+__device__ __forceinline__ d3 ld_d(const WfPaths& a, size_t i) { return mk(a.dx[i], a.dy[i], a.dz[i]); }
 __device__ __forceinline__ d3 ld_P(const WfParams& p, int i) { return mk(p.px[i], p.py[i], p.pz[i]); }
 
 // the light vector of a hit point: calculateDirectLighting's lightDir and
@@ -87,7 +140,7 @@ __device__ __forceinline__ void light_vec(const DLight& Lt, d3 P, d3& ldir, doub
   ldir = ldist == 0 ? mk(0, 0, 0) : divs(lv, ldist);
 }
 
-__device__ __forceinline__ void store_path(const WfPaths& b, int j, d3 o, d3 d, d3 T, d3 L, uint64_t rng,
+__device__ __forceinline__ void store_path(const WfPaths& b, size_t j, d3 o, d3 d, d3 T, d3 L, uint64_t rng,
                                            uint32_t sid, int depth) {
   b.ox[j] = o.x;
   b.oy[j] = o.y;
@@ -113,298 +166,546 @@ __device__ __forceinline__ void finish(const WfParams& p, uint32_t sid, d3 L) {
   r[2] = L.z;
 }
 
-// ---------------------------------------------------------------- regen
-// Samples [next, next + regen_cnt) of the chunk start as paths appended to
-// the next array.  Sample id = local pixel * spp + sample: a pixel's samples
-// are consecutive, so a wave's camera rays are neighbours.
+// ---------------------------------------------------------------- traversal
+// One step of the while-while traversal of a lane (bvh.cpp layout; the same
+// tests as closest_hit / any_hit in rt_device.h): descend internal nodes,
+// nearer child first, until `cur` is a leaf (count 1..4) or -1 (done).
 template <bool kCount>
-__global__ __launch_bounds__(kWfBlock) void wf_regen(const WfParams p) {
-  const WfCtl* ctl = p.ctl;
-  const long long nnew = ctl->regen_cnt;
-  const long long first = (long long)ctl->next_sample;
-  const CamK ck = make_cam(p.seed_key, p.W, p.H, p.aspect, p.cam[0], p.cam[1], p.cam[2]);
-  Counters c;
-  if constexpr (kCount)
-    for (int i = 0; i < 9; ++i) c.v[i] = 0;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  // (block-uniform trip count: the ballot in wave_append sees whole waves)
-  for (long long b0 = (long long)blockIdx.x * blockDim.x; b0 < nnew; b0 += stride) {
-    const long long t = b0 + threadIdx.x;
-    bool valid = false;
-    const uint32_t sid = (uint32_t)(first + t);
-    int x = 0, y = 0, s = 0;
-    if (t < nnew) {
-      const uint32_t lp = p.lp0 + sid / (uint32_t)p.spp;
-      s = (int)(sid - (sid / (uint32_t)p.spp) * (uint32_t)p.spp);
-      const int lt = (int)(lp >> 10), tp = (int)(lp & 1023);
-      const int tile = p.rank + lt * p.world;
-      const int tx = tile % p.tiles_x, ty = tile / p.tiles_x;
-      x = tx * 32 + (tp & 31);
-      y = ty * 32 + (tp >> 5);
-      valid = tile < p.ntiles && x < p.W && y < p.H;
-    }
-    const int j = wave_append(&p.ctl->n_next, valid);
-    if (valid) {
-      cnt<kCount>(c, C_CAM);
-      rt_rng rng;
-      d3 o, d;
-      camera_ray_c<kCount>(ck, x, y, s, rng, o, d, c);
-      store_path(p.next, j, o, d, mk(1, 1, 1), mk(0, 0, 0), rng.x, sid, 0);
+__device__ __forceinline__ void descend(const DBVHNode* __restrict__ bvh, const Ray32& r, float tminf,
+                                        float tmaxf, int& cur, int& sp, int* stack, Counters& c) {
+  while ((cur & 7) == 0) {
+    const int first = cur >> 3;
+    const DBVHNode L = bvh[first], R = bvh[first + 1];
+    cnt<kCount>(c, C_BOX, 2);
+    float tl, tr;
+    const bool hl = box_hit32(L, r, tminf, tmaxf, tl), hr = box_hit32(R, r, tminf, tmaxf, tr);
+    if (hl || hr) {
+      const bool lfirst = hl && (!hr || tl <= tr);
+      if (hl && hr) {
+        stack[sp * 64] = lfirst ? bvh_code(R) : bvh_code(L);
+        ++sp;
+      }
+      cur = lfirst ? bvh_code(L) : bvh_code(R);
+    } else {
+      cur = sp == 0 ? -1 : stack[--sp * 64];
     }
   }
-  flush_counts<kCount>(p, c);
+}
+
+// Dynamic job distribution of the persistent traversal kernels.  The dense
+// job space [0, n) is cut into kWfShards ranges, each with a head counter
+// (heads[32 s], reset by wf_book); a wave takes chunks of kChunk jobs from
+// its home range (its workgroup index mod kWfShards, i.e. its XCD under the
+// round-robin dispatch), then from the other ranges.  (A static split of the
+// jobs over the waves left the SIMDs idle half the time: traversal lengths
+// vary too much.)  Called by whole waves; wave-uniform state.
+struct JobSrc {
+  int next, hi;  // the current chunk
+  int tried;     // ranges found empty
+};
+__device__ __forceinline__ bool job_refill(JobSrc& js, int32_t* heads, int n) {
+  const int home = blockIdx.x % kWfShards;
+  while (js.tried < kWfShards) {
+    const int s = (home + js.tried) % kWfShards;
+    const int lo_s = (int)((long long)n * s / kWfShards), hi_s = (int)((long long)n * (s + 1) / kWfShards);
+    int got = 0;
+    if ((threadIdx.x & 63) == 0) got = atomicAdd(&heads[s * 32], kChunk);
+    got = __builtin_amdgcn_readfirstlane(got);
+    if (lo_s + got < hi_s) {
+      js.next = lo_s + got;
+      js.hi = min(hi_s, js.next + kChunk);
+      return true;
+    }
+    ++js.tried;
+  }
+  return false;
 }
 
 // ---------------------------------------------------------------- extend
+// Persistent closest-hit traversal of the live paths (hitWorld,
+// renderer.go:333-346, in the BVH form of rt_device.h closest_hit: same
+// tests, same exact-t tie rule).  Wave w owns jobs [n w / W, n (w+1) / W) and
+// refills idle lanes from them.  A hit leaves (sphere, root numerator) for
+// shade1; a miss ends the path with the radiance it has (renderer.go:170-173).
 template <bool kCount>
 __global__ __launch_bounds__(kWfBlock) void wf_extend(const WfParams p) {
-  const int n = p.ctl->n_cur;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if ((int)(blockIdx.x * blockDim.x) >= n) return;
+  const Dense dn = dense(p.ctl->cur_cnt);
+  const int n = dn.start[kWfShards];
+  if (n == 0) return;
+  JobSrc js{0, 0, 0};
+  bool more = true;  // wave-uniform: jobs may remain
   Counters c;
   if constexpr (kCount)
     for (int k = 0; k < 9; ++k) c.v[k] = 0;
-  if (i < n) {
-    const WfPaths& a = p.cur;
-    bool found = false;
-    HitSel hs;
-    if (a.depth[i] < p.max_depth) {  // traceRay's depth cut-off comes first
-      cnt<kCount>(c, C_BOUNCE);
-      const Cand all{~0ull, ~0ull};
-      found = closest_hit<kCount>(p.g, ld_o(a, i), ld_d(a, i), hs, wf_stack(p.stack_depth), all, c);
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int* stack = wf_stack(p.stack_depth);
+  const WfPaths& a = p.cur;
+  const double tmin = 0.001;
+  bool busy = false;
+  size_t slot = 0;
+  d3 o = mk(0, 0, 0), d = mk(0, 0, 0);
+  double av = 0, inv_a = 0, closest = 0, bnum = 0;
+  Ray32 r32{};
+  float tminf = 0;
+  int cur = -1, sp = 0, best_obj = -1, bidx = -1;
+  for (;;) {
+    const unsigned long long idle = __ballot(!busy);
+    if (more && (__popcll(idle) >= kRefill || idle == ~0ull) && js.next >= js.hi)
+      more = job_refill(js, p.ctl->job_head[0], n);
+    if (more && (__popcll(idle) >= kRefill || idle == ~0ull)) {
+      const int j = js.next + __popcll(idle & below), hi = js.hi;
+      js.next = min(hi, js.next + __popcll(idle));
+      if (!busy && j < hi) {
+        slot = dense_at(dn, j, p.shard_cap);
+        const uint32_t sid = a.sid[slot];
+        bool miss = true;
+        if (sid != kDeadSid && a.depth[slot] < p.max_depth) {  // traceRay's depth cut-off comes first
+          cnt<kCount>(c, C_BOUNCE);
+          o = ld_o(a, slot);
+          d = ld_d(a, slot);
+          av = len2(d);
+          inv_a = approx_rcp(av);
+          closest = __builtin_inf();
+          best_obj = -1;
+          const d3 id = inv_dir(d);
+          cnt<kCount>(c, C_BOX);
+          if (box_hit(p.g.bvh[0], o, id, tmin, closest)) {
+            r32 = ray32(o, id);
+            tminf = t_lo32(tmin);
+            cur = bvh_code(p.g.bvh[0]);
+            sp = 0;
+            busy = true;
+            miss = false;
+          }
+        }
+        if (miss) {
+          p.hidx[slot] = -1;
+          if (sid != kDeadSid) finish(p, sid, mk(a.lx[slot], a.ly[slot], a.lz[slot]));
+        }
+      }
     }
-    if (found) {
-      p.hidx[i] = hs.idx;
-      p.hnum[i] = hs.num;
-    } else {  // miss: black (renderer.go:170-173); the path ends with what it has
-      p.hidx[i] = -1;
-      finish(p, a.sid[i], mk(a.lx[i], a.ly[i], a.lz[i]));
+    if (__ballot(busy) == 0) {
+      if (!more) break;
+      continue;
+    }
+    if (busy) {
+      descend<kCount>(p.g.bvh, r32, tminf, t_hi32(closest), cur, sp, stack, c);
+      if (cur != -1) {  // a leaf: the exact Sphere.Hit tests, in hittable order
+        const int first = cur >> 3, count = cur & 7;
+        for (int i = first; i < first + count; ++i) {
+          cnt<kCount>(c, C_SPH);
+          const DSphere& S = p.g.spheres[i];
+          double num;
+          if (sphere_query(S, o, d, av, inv_a, tmin, closest, num)) {
+            const double t = num / av;
+            if (t == closest && best_obj > S.obj) continue;
+            closest = t;
+            bnum = num;
+            bidx = i;
+            best_obj = S.obj;
+          }
+        }
+        cur = sp == 0 ? -1 : stack[--sp * 64];
+      }
+      if (cur == -1) {  // traversal done
+        busy = false;
+        if (best_obj >= 0) {
+          p.hidx[slot] = bidx;
+          p.hnum[slot] = bnum;
+        } else {
+          p.hidx[slot] = -1;
+          finish(p, a.sid[slot], mk(a.lx[slot], a.ly[slot], a.lz[slot]));
+        }
+      }
     }
   }
   flush_counts<kCount>(p, c);
 }
 
 // ---------------------------------------------------------------- shade1
+// HitRecord of every hit (sphere.go:42-58, as in the megakernel) and one hard
+// shadow ray per lit light (renderer.go:249-256,299-305) into the hard queue.
 template <bool kCount>
 __global__ __launch_bounds__(kWfBlock) void wf_shade1(const WfParams p) {
-  const int n = p.ctl->n_cur;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if ((int)(blockIdx.x * blockDim.x) >= n) return;
+  __shared__ int s_wave[kWfBlock / 64];
+  __shared__ int s_base;
+  const Dense dn = dense(p.ctl->cur_cnt);
+  const int n = dn.start[kWfShards];
+  if ((int)(blockIdx.x * kWfBlock) >= n) return;
   Counters c;
   if constexpr (kCount)
     for (int k = 0; k < 9; ++k) c.v[k] = 0;
-  const bool hit = i < n && p.hidx[i] >= 0;
-  d3 P = mk(0, 0, 0);
-  if (hit) {
-    // HitRecord of the sphere (sphere.go:42-58), as in the megakernel
-    const WfPaths& a = p.cur;
-    cnt<kCount>(c, C_SHADE);
-    const d3 o = ld_o(a, i), d = ld_d(a, i);
-    const DSphere& S0 = p.g.spheres[p.hidx[i]];
-    const double t = p.hnum[i] / len2(d);
-    P = o + muls(d, t);
-    const d3 outward = divs(P - ld3(S0.c), S0.r);
-    const bool front = dot(d, outward) < 0;
-    const d3 N = front ? outward : neg(outward);
-    p.px[i] = P.x;
-    p.py[i] = P.y;
-    p.pz[i] = P.z;
-    p.nx[i] = N.x;
-    p.ny[i] = N.y;
-    p.nz[i] = N.z;
-    p.hinfo[i] = (S0.mat << 1) | (front ? 1 : 0);
-  }
-  for (int li = 0; li < p.nl; ++li) {
-    bool lit = false;
+  const int j = blockIdx.x * kWfBlock + threadIdx.x;
+  size_t slot = 0;
+  bool hit = false;
+  uint32_t lit = 0;
+  if (j < n) {
+    slot = dense_at(dn, j, p.shard_cap);
+    const int hi = p.hidx[slot];
+    hit = hi >= 0;
     if (hit) {
-      d3 ldir;
-      double ldist;
-      light_vec(p.lights[li], P, ldir, ldist);
-      lit = !(ldist < 0.001);
-      p.lstate[(size_t)i * p.nl + li] = 0;
-      if (lit) {
-        cnt<kCount>(c, C_LIGHT);
-        cnt<kCount>(c, C_SHADOW);
+      cnt<kCount>(c, C_SHADE);
+      const WfPaths& a = p.cur;
+      const d3 o = ld_o(a, slot), d = ld_d(a, slot);
+      const DSphere& S0 = p.g.spheres[hi];
+      const double t = p.hnum[slot] / len2(d);
+      const d3 P = o + muls(d, t);
+      const d3 outward = divs(P - ld3(S0.c), S0.r);
+      const bool front = dot(d, outward) < 0;
+      const d3 N = front ? outward : neg(outward);
+      p.px[slot] = P.x;
+      p.py[slot] = P.y;
+      p.pz[slot] = P.z;
+      p.nx[slot] = N.x;
+      p.ny[slot] = N.y;
+      p.nz[slot] = N.z;
+      p.hinfo[slot] = (S0.mat << 1) | (front ? 1 : 0);
+      for (int li = 0; li < p.nl; ++li) {
+        d3 ldir;
+        double ldist;
+        light_vec(p.lights[li], P, ldir, ldist);
+        p.lstate[slot * p.nl + li] = 0;
+        if (!(ldist < 0.001)) {
+          cnt<kCount>(c, C_LIGHT);
+          cnt<kCount>(c, C_SHADOW);
+          lit |= 1u << li;
+        }
       }
     }
-    const int j = wave_append(&p.ctl->n_hard, lit);
-    if (lit) p.hardq[j] = (uint32_t)i * (uint32_t)p.nl + (uint32_t)li;
   }
+  const int shard = blockIdx.x % kWfShards;
+  int q = block_append(__popc(lit), &p.ctl->hard_cnt[shard * 32], s_wave, &s_base);
+  uint32_t* hq = p.hardq + (size_t)shard * p.hard_cap;
+  for (uint32_t m = lit; m; m &= m - 1) hq[q++] = (uint32_t)(slot * p.nl) + (uint32_t)__builtin_ctz(m);
   flush_counts<kCount>(p, c);
 }
 
-// ---------------------------------------------------------------- hard
-template <bool kCount>
-__global__ __launch_bounds__(kWfBlock) void wf_hard(const WfParams p) {
-  const int n = p.ctl->n_hard;
+// ---------------------------------------------------------------- occlude
+// Persistent any-hit traversal of the queued shadow rays (hitWorld as used by
+// calculateSmartShadow, renderer.go:305,320: is anything hit in
+// [0.001, distance)?).  kSoft: the ray is normalize(lightDir + 0.1 p) of a
+// queued point p (renderer.go:316-318) and a blocked ray adds 1 to its
+// (path, light) count; hard: the ray is lightDir and a blocked ray sets
+// kHardBit.
+template <bool kCount, bool kSoft>
+__global__ __launch_bounds__(kWfBlock) void wf_occlude(const WfParams p) {
+  const Dense dn = dense(kSoft ? p.ctl->soft_cnt : p.ctl->hard_cnt);
+  const int n = dn.start[kWfShards];
+  if (n == 0) return;
+  JobSrc js{0, 0, 0};
+  bool more = true;  // wave-uniform: jobs may remain
   Counters c;
   if constexpr (kCount)
     for (int k = 0; k < 9; ++k) c.v[k] = 0;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
   int* stack = wf_stack(p.stack_depth);
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-    const uint32_t key = p.hardq[j];
-    const int i = (int)(key / (uint32_t)p.nl), li = (int)(key - (uint32_t)i * (uint32_t)p.nl);
-    const d3 P = ld_P(p, i);
-    d3 ldir;
-    double ldist;
-    light_vec(p.lights[li], P, ldir, ldist);
-    if (any_hit<kCount>(p.g, P, ldir, ldist, stack, c)) p.lstate[key] = kHardBit;
+  const double tmin = 0.001;
+  bool busy = false;
+  uint32_t key = 0;
+  d3 o = mk(0, 0, 0), d = mk(0, 0, 0);
+  double av = 0, inv_a = 0, tmax = 0;
+  Ray32 r32{};
+  float tminf = 0, tmaxf = 0;
+  int cur = -1, sp = 0;
+  for (;;) {
+    const unsigned long long idle = __ballot(!busy);
+    if (more && (__popcll(idle) >= kRefill || idle == ~0ull) && js.next >= js.hi)
+      more = job_refill(js, p.ctl->job_head[kSoft ? 2 : 1], n);
+    if (more && (__popcll(idle) >= kRefill || idle == ~0ull)) {
+      const int j = js.next + __popcll(idle & below), hi = js.hi;
+      js.next = min(hi, js.next + __popcll(idle));
+      if (!busy && j < hi) {
+        const size_t at = dense_at(dn, j, kSoft ? p.soft_cap : p.hard_cap);
+        uint4 e;
+        if constexpr (kSoft)
+          e = reinterpret_cast<const uint4*>(p.softq)[at];
+        else
+          e = make_uint4(p.hardq[at], 0, 0, 0);
+        key = e.x;
+        const uint32_t slot = key / (uint32_t)p.nl, li = key - slot * (uint32_t)p.nl;
+        o = mk(p.px[slot], p.py[slot], p.pz[slot]);
+        d3 ldir;
+        light_vec(p.lights[li], o, ldir, tmax);
+        if constexpr (kSoft) {
+          const d3 pt =
+              mk(rt_bits_to_unit(e.y) * 2 - 1, rt_bits_to_unit(e.z) * 2 - 1, rt_bits_to_unit(e.w) * 2 - 1);
+          d = normalize(ldir + muls(pt, 0.1));
+        } else {
+          d = ldir;
+        }
+        av = len2(d);
+        inv_a = approx_rcp(av);
+        const d3 id = inv_dir(d);
+        cnt<kCount>(c, C_BOX);
+        if (box_hit(p.g.bvh[0], o, id, tmin, tmax)) {
+          r32 = ray32(o, id);
+          tminf = t_lo32(tmin);
+          tmaxf = t_hi32(tmax);
+          cur = bvh_code(p.g.bvh[0]);
+          sp = 0;
+          busy = true;
+        }
+      }
+    }
+    if (__ballot(busy) == 0) {
+      if (!more) break;
+      continue;
+    }
+    if (busy) {
+      descend<kCount>(p.g.bvh, r32, tminf, tmaxf, cur, sp, stack, c);
+      bool blocked = false;
+      if (cur != -1) {
+        const int first = cur >> 3, count = cur & 7;
+        for (int i = first; i < first + count && !blocked; ++i) {
+          cnt<kCount>(c, C_SPH);
+          double num;
+          blocked = sphere_query(p.g.spheres[i], o, d, av, inv_a, tmin, tmax, num) != 0;
+        }
+        cur = sp == 0 ? -1 : stack[--sp * 64];
+      }
+      if (blocked) {
+        if constexpr (kSoft)
+          atomicAdd(&p.lstate[key], 1u);
+        else
+          p.lstate[key] = kHardBit;
+      }
+      if (blocked || cur == -1) busy = false;
+    }
   }
   flush_counts<kCount>(p, c);
 }
 
 // ---------------------------------------------------------------- softgen
-// The 16 jittered points of every (path, light) whose hard ray is clear, in
-// light order from the path's stream (rejection sampling, vector.go:132-139).
-// An owner reserves 16 consecutive queue entries, so its rays are adjacent.
+// For every light whose hard ray is clear, in light order, the 16 points of
+// calculateSmartShadow's soft rays from the path's stream (rejection
+// sampling, vector.go:132-139), as 16 consecutive soft-queue entries.
 template <bool kCount>
 __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
-  const int n = p.ctl->n_cur;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if ((int)(blockIdx.x * blockDim.x) >= n) return;
+  __shared__ int s_wave[kWfBlock / 64];
+  __shared__ int s_base;
+  const Dense dn = dense(p.ctl->cur_cnt);
+  const int n = dn.start[kWfShards];
+  if ((int)(blockIdx.x * kWfBlock) >= n) return;
   Counters c;
   if constexpr (kCount)
     for (int k = 0; k < 9; ++k) c.v[k] = 0;
-  const bool hit = i < n && p.hidx[i] >= 0;
-  rt_rng rng{hit ? p.cur.rng[i] : 0};
-  const d3 P = hit ? ld_P(p, i) : mk(0, 0, 0);
-  for (int li = 0; li < p.nl; ++li) {
-    bool own = false;
-    const uint32_t key = (uint32_t)i * (uint32_t)p.nl + (uint32_t)li;
-    if (hit) {
-      d3 ldir;
-      double ldist;
-      light_vec(p.lights[li], P, ldir, ldist);
-      own = !(ldist < 0.001) && !(p.lstate[key] & kHardBit);
+  const int j = blockIdx.x * kWfBlock + threadIdx.x;
+  size_t slot = 0;
+  uint32_t own = 0;
+  if (j < n) {
+    slot = dense_at(dn, j, p.shard_cap);
+    if (p.hidx[slot] >= 0) {
+      const d3 P = mk(p.px[slot], p.py[slot], p.pz[slot]);
+      for (int li = 0; li < p.nl; ++li) {
+        d3 ldir;
+        double ldist;
+        light_vec(p.lights[li], P, ldir, ldist);
+        if (!(ldist < 0.001) && !(p.lstate[slot * p.nl + li] & kHardBit)) own |= 1u << li;
+      }
     }
-    const int q = wave_append(&p.ctl->n_soft, own, 16);
-    if (own) {
+  }
+  const int shard = blockIdx.x % kWfShards;
+  const int q = block_append(16 * __popc(own), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
+  if (own) {
+    uint4* sq = reinterpret_cast<uint4*>(p.softq) + (size_t)shard * p.soft_cap + q;
+    rt_rng rng{p.cur.rng[slot]};
+    for (uint32_t m = own; m; m &= m - 1) {
+      const uint32_t key = (uint32_t)(slot * p.nl) + (uint32_t)__builtin_ctz(m);
       cnt<kCount>(c, C_SHADOW, 16);
       for (int k = 0; k < 16;) {
         const uint32_t ux = rt_rng_next(&rng), uy = rt_rng_next(&rng), uz = rt_rng_next(&rng);
         cnt<kCount>(c, C_RNG, 3);
         const d3 pt = mk(rt_bits_to_unit(ux) * 2 - 1, rt_bits_to_unit(uy) * 2 - 1, rt_bits_to_unit(uz) * 2 - 1);
-        if (len2(pt) < 1) reinterpret_cast<uint4*>(p.softq)[q + k++] = make_uint4(key, ux, uy, uz);
+        if (len2(pt) < 1) {
+          *sq++ = make_uint4(key, ux, uy, uz);
+          ++k;
+        }
       }
     }
-  }
-  if (hit) p.cur.rng[i] = rng.x;
-  flush_counts<kCount>(p, c);
-}
-
-// ---------------------------------------------------------------- soft
-template <bool kCount>
-__global__ __launch_bounds__(kWfBlock) void wf_soft(const WfParams p) {
-  const int n = p.ctl->n_soft;
-  Counters c;
-  if constexpr (kCount)
-    for (int k = 0; k < 9; ++k) c.v[k] = 0;
-  int* stack = wf_stack(p.stack_depth);
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-    const uint4 e = reinterpret_cast<const uint4*>(p.softq)[j];
-    const int i = (int)(e.x / (uint32_t)p.nl), li = (int)(e.x - (uint32_t)i * (uint32_t)p.nl);
-    const d3 P = ld_P(p, i);
-    d3 ldir;
-    double ldist;
-    light_vec(p.lights[li], P, ldir, ldist);
-    const d3 pt = mk(rt_bits_to_unit(e.y) * 2 - 1, rt_bits_to_unit(e.z) * 2 - 1, rt_bits_to_unit(e.w) * 2 - 1);
-    if (any_hit<kCount>(p.g, P, normalize(ldir + muls(pt, 0.1)), ldist, stack, c)) atomicAdd(&p.lstate[e.x], 1u);
+    p.cur.rng[slot] = rng.x;
   }
   flush_counts<kCount>(p, c);
 }
 
-// ---------------------------------------------------------------- shade2
+// ---------------------------------------------------------------- shade
+// calculateDirectLighting (renderer.go:229-297) with the shadow results,
+// Material.Scatter and the traceRay combination (renderer.go:181-226).
+// Finished paths write their sample's radiance; survivors are appended to the
+// workgroup's shard of the next path array.
 template <bool kCount>
-__global__ __launch_bounds__(kWfBlock) void wf_shade2(const WfParams p) {
-  const int n = p.ctl->n_cur;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if ((int)(blockIdx.x * blockDim.x) >= n) return;
+__global__ __launch_bounds__(kWfBlock) void wf_shade(const WfParams p) {
+  __shared__ int s_wave[kWfBlock / 64];
+  __shared__ int s_base;
+  const Dense dn = dense(p.ctl->cur_cnt);
+  const int n = dn.start[kWfShards];
+  if ((int)(blockIdx.x * kWfBlock) >= n) return;
   Counters c;
   if constexpr (kCount)
     for (int k = 0; k < 9; ++k) c.v[k] = 0;
-  const bool hit = i < n && p.hidx[i] >= 0;
+  const int j = blockIdx.x * kWfBlock + threadIdx.x;
   bool cont = false;
   d3 P = mk(0, 0, 0), nd = mk(0, 0, 0), T = mk(0, 0, 0), L = mk(0, 0, 0);
   rt_rng rng{0};
   uint32_t sid = 0;
   int depth = 0;
-  if (hit) {
-    const WfPaths& a = p.cur;
-    P = ld_P(p, i);
-    const d3 N = mk(p.nx[i], p.ny[i], p.nz[i]);
-    const int info = p.hinfo[i];
-    const bool front = info & 1;
-    const DMat* __restrict__ m = p.mats + (info >> 1);
-    const d3 d = ld_d(a, i);
-    T = mk(a.tx[i], a.ty[i], a.tz[i]);
-    L = mk(a.lx[i], a.ly[i], a.lz[i]);
-    rng.x = a.rng[i];
-    sid = a.sid[i];
-    depth = a.depth[i];
-    // calculateDirectLighting (renderer.go:229-297), light by light
-    d3 D = mk(m->ambient, m->ambient, m->ambient);
-    for (int li = 0; li < p.nl; ++li) {
-      const DLight& Lt = p.lights[li];
-      d3 ldir;
-      double ldist;
-      light_vec(Lt, P, ldir, ldist);
-      if (!(ldist < 0.001)) {
-        const uint32_t ls = p.lstate[(size_t)i * p.nl + li];
-        const bool occl = ls & kHardBit;
-        const int unocc = 16 - (int)(ls & 0xFFFFu);
-        const double sf = occl ? 0.0 : (p.soft ? (double)unocc / 16.0 : 1.0);  // shadowSum / 16
-        if (sf > 0.0) {
-          const double metallic = m->metallic;
-          double cos_t = gmax0(dot(N, ldir));
-          double intensity = cos_t * Lt.intensity / (ldist * ldist);
-          D = D + muls(ld3(m->albedo), m->diffuse_strength * intensity * sf);
-          if (metallic > 0.5) {
-            d3 view = normalize(neg(P));
-            d3 half = normalize(ldir + view);
-            double hc = gmax0(dot(N, half));
-            const int sp = m->spec_pow;
-            double si = sp == 64 ? pow_n<64>(hc) : (sp == 48 ? pow_n<48>(hc) : pow_n<32>(hc));
-            D = D + muls(ld3(Lt.color), si * intensity * sf * metallic * 3.0);
+  if (j < n) {
+    const size_t slot = dense_at(dn, j, p.shard_cap);
+    if (p.hidx[slot] >= 0) {
+      const WfPaths& a = p.cur;
+      P = mk(p.px[slot], p.py[slot], p.pz[slot]);
+      const d3 N = mk(p.nx[slot], p.ny[slot], p.nz[slot]);
+      const int info = p.hinfo[slot];
+      const bool front = info & 1;
+      const DMat* __restrict__ m = p.mats + (info >> 1);
+      const d3 d = ld_d(a, slot);
+      T = mk(a.tx[slot], a.ty[slot], a.tz[slot]);
+      L = mk(a.lx[slot], a.ly[slot], a.lz[slot]);
+      rng.x = a.rng[slot];
+      sid = a.sid[slot];
+      depth = a.depth[slot];
+      d3 D = mk(m->ambient, m->ambient, m->ambient);
+      for (int li = 0; li < p.nl; ++li) {
+        const DLight& Lt = p.lights[li];
+        d3 ldir;
+        double ldist;
+        light_vec(Lt, P, ldir, ldist);
+        if (!(ldist < 0.001)) {
+          const uint32_t ls = p.lstate[slot * p.nl + li];
+          const bool occl = ls & kHardBit;
+          const int unocc = 16 - (int)(ls & 0xFFFFu);
+          const double sf = occl ? 0.0 : (p.soft ? (double)unocc / 16.0 : 1.0);  // shadowSum / 16
+          if (sf > 0.0) {
+            const double metallic = m->metallic;
+            double cos_t = gmax0(dot(N, ldir));
+            double intensity = cos_t * Lt.intensity / (ldist * ldist);
+            D = D + muls(ld3(m->albedo), m->diffuse_strength * intensity * sf);
+            if (metallic > 0.5) {
+              d3 view = normalize(neg(P));
+              d3 half = normalize(ldir + view);
+              double hc = gmax0(dot(N, half));
+              const int spw = m->spec_pow;
+              double si = spw == 64 ? pow_n<64>(hc) : (spw == 48 ? pow_n<48>(hc) : pow_n<32>(hc));
+              D = D + muls(ld3(Lt.color), si * intensity * sf * metallic * 3.0);
+            }
           }
         }
       }
-    }
-    // Material.Scatter and the traceRay combination (renderer.go:181-226)
-    const d3 E = ld3(m->emit);
-    const Scat sc = scatter<kCount>(m, d, N, front, rng, c);
-    if (!sc.ok) {
-      L = L + mul(T, E + D);
-    } else {
-      L = L + mul(T, E + muls(D, m->dw));
-      cont = p.recursive && depth + 1 < p.max_depth;
-      if (cont) {
-        T = mul(T, muls(sc.A, m->rw));
-        nd = sc.nd;
-        depth += 1;
+      const d3 E = ld3(m->emit);
+      const Scat sc = scatter<kCount>(m, d, N, front, rng, c);
+      if (!sc.ok) {
+        L = L + mul(T, E + D);
+      } else {
+        L = L + mul(T, E + muls(D, m->dw));
+        cont = p.recursive && depth + 1 < p.max_depth;
+        if (cont) {
+          T = mul(T, muls(sc.A, m->rw));
+          nd = sc.nd;
+          depth += 1;
+        }
       }
+      if (!cont) finish(p, sid, L);
     }
-    if (!cont) finish(p, sid, L);
   }
-  const int j = wave_append(&p.ctl->n_next, cont);
-  if (cont) store_path(p.next, j, P, nd, T, L, rng.x, sid, depth);
+  const int shard = blockIdx.x % kWfShards;
+  const int q = block_append(cont ? 1 : 0, &p.ctl->next_cnt[shard * 32], s_wave, &s_base);
+  if (cont) store_path(p.next, (size_t)shard * p.shard_cap + q, P, nd, T, L, rng.x, sid, depth);
   flush_counts<kCount>(p, c);
 }
 
-// ---------------------------------------------------------------- bookkeeping
-// before regen: how many new samples fit (the free slots of the next array)
-__global__ void wf_book_regen(WfCtl* ctl, int capacity) {
-  const long long left = (long long)ctl->total - (long long)ctl->next_sample;
-  const long long room = capacity - ctl->n_next;
-  ctl->regen_cnt = (int)(left < room ? left : room);
+// ---------------------------------------------------------------- regen
+// New samples for the free slots of the next array: shard s takes the
+// samples [next + free_0 + .. + free_{s-1}, ...) into its slots after its
+// survivors, in order (a pixel's samples are consecutive, so neighbouring
+// lanes trace neighbouring camera rays).  Out-of-image pixels of edge tiles
+// become dead slots (kDeadSid).  Deterministic: no atomics.
+struct RegenPlan {
+  long long first[kWfShards];  // first new sample of shard s
+  int take[kWfShards];         // new samples of shard s
+  long long taken;             // all shards
+};
+__device__ __forceinline__ RegenPlan regen_plan(const WfCtl* ctl, int shard_cap) {
+  RegenPlan r;
+  long long pos = (long long)ctl->next_sample;
+  const long long total = (long long)ctl->total;
+#pragma unroll
+  for (int s = 0; s < kWfShards; ++s) {
+    const long long fr = shard_cap - ctl->next_cnt[s * 32];
+    const long long t = min(fr, max(0ll, total - pos));
+    r.first[s] = pos;
+    r.take[s] = (int)t;
+    pos += t;
+  }
+  r.taken = pos - (long long)ctl->next_sample;
+  return r;
 }
-// after regen: the next array becomes current
-__global__ void wf_book_swap(WfCtl* ctl) {
-  ctl->next_sample += ctl->regen_cnt;
-  ctl->n_cur = ctl->n_next;
-  ctl->n_next = 0;
-  ctl->n_hard = 0;
-  ctl->n_soft = 0;
-  ctl->regen_cnt = 0;
+
+template <bool kCount>
+__global__ __launch_bounds__(kWfBlock) void wf_regen(const WfParams p) {
+  const int t = blockIdx.x * kWfBlock + threadIdx.x;  // over kWfShards * shard_cap slots
+  const int s = min(t / p.shard_cap, kWfShards - 1), local = t - s * p.shard_cap;
+  const int have = p.ctl->next_cnt[s * 32];
+  Counters c;
+  if constexpr (kCount)
+    for (int i = 0; i < 9; ++i) c.v[i] = 0;
+  if (local >= have && local < p.shard_cap) {
+    const RegenPlan rp = regen_plan(p.ctl, p.shard_cap);
+    int take = 0;
+    long long first = 0;
+#pragma unroll
+    for (int k = 0; k < kWfShards; ++k)
+      if (k == s) {
+        take = rp.take[k];
+        first = rp.first[k];
+      }
+    const int k = local - have;
+    if (k < take) {
+      const uint32_t sid = (uint32_t)(first + k);
+      const uint32_t q = sid / (uint32_t)p.spp;
+      const uint32_t lp = p.lp0 + q;
+      const int smp = (int)(sid - q * (uint32_t)p.spp);
+      const int lt = (int)(lp >> 10), tp = (int)(lp & 1023);
+      const int tile = p.rank + lt * p.world;
+      const int x = (tile % p.tiles_x) * 32 + (tp & 31), y = (tile / p.tiles_x) * 32 + (tp >> 5);
+      const size_t slot = (size_t)s * p.shard_cap + local;
+      if (tile >= p.ntiles || x >= p.W || y >= p.H) {
+        p.next.sid[slot] = kDeadSid;
+      } else {
+        cnt<kCount>(c, C_CAM);
+        const CamK ck = make_cam(p.seed_key, p.W, p.H, p.aspect, p.cam[0], p.cam[1], p.cam[2]);
+        rt_rng rng;
+        d3 o, d;
+        camera_ray_c<kCount>(ck, x, y, smp, rng, o, d, c);
+        store_path(p.next, slot, o, d, mk(1, 1, 1), mk(0, 0, 0), rng.x, sid, 0);
+      }
+    }
+  }
+  flush_counts<kCount>(p, c);
+}
+
+// ---------------------------------------------------------------- book
+// The next array becomes current; queues reset; the loop state for the host.
+__global__ void wf_book(const WfParams p) {
+  if (threadIdx.x != 0) return;
+  WfCtl* ctl = p.ctl;
+  const RegenPlan rp = regen_plan(ctl, p.shard_cap);
+  int live = 0;
+#pragma unroll
+  for (int s = 0; s < kWfShards; ++s) {
+    const int nc = ctl->next_cnt[s * 32] + rp.take[s];
+    ctl->cur_cnt[s * 32] = nc;
+    ctl->next_cnt[s * 32] = 0;
+    ctl->hard_cnt[s * 32] = 0;
+    ctl->soft_cnt[s * 32] = 0;
+    ctl->job_head[0][s * 32] = 0;
+    ctl->job_head[1][s * 32] = 0;
+    ctl->job_head[2][s * 32] = 0;
+    live += nc;
+  }
+  ctl->next_sample += rp.taken;
+  ctl->live = live;
+  ctl->dry = ctl->next_sample >= ctl->total ? 1 : 0;
   ctl->iter += 1;
 }
 
@@ -438,44 +739,57 @@ __global__ __launch_bounds__(kWfBlock) void wf_resolve(const WfParams p, int npi
 }
 
 // ---------------------------------------------------------------- launches
-size_t wf_stack_bytes(const WfParams& p) { return (size_t)kWfBlock * p.stack_depth * sizeof(int); }
+// persistent kernels: as many workgroups as fit on the device at once
+template <typename K>
+static int resident_grid(K kernel, size_t shmem) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 1024;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kWfBlock, shmem) != hipSuccess || per < 1) per = 1;
+  return cus * per;
+}
 
 template <bool kCount>
-static int enqueue_iteration(const WfParams& p, hipStream_t st) {
-  const int cap = p.capacity;
+static int enqueue_regen_book(const WfParams& p, hipStream_t st) {
+  const int slots = kWfShards * p.shard_cap;
+  hipLaunchKernelGGL((wf_regen<kCount>), dim3((slots + kWfBlock - 1) / kWfBlock), dim3(kWfBlock), 0, st, p);
+  hipLaunchKernelGGL(wf_book, dim3(1), dim3(64), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+template <bool kCount>
+static int enqueue_bounce(const WfParams& p, hipStream_t st) {
   const dim3 b(kWfBlock);
-  const dim3 gp((cap + kWfBlock - 1) / kWfBlock);
-  const size_t sh = wf_stack_bytes(p);
-  // queue kernels: grid-stride over at most this many workgroups
-  const dim3 gq(std::min((cap * std::max(p.nl, 1) + kWfBlock - 1) / kWfBlock, 256 * 32));
-  hipLaunchKernelGGL((wf_extend<kCount>), gp, b, sh, st, p);
-  hipLaunchKernelGGL((wf_shade1<kCount>), gp, b, 0, st, p);
+  const dim3 gd((kWfShards * p.shard_cap + kWfBlock - 1) / kWfBlock);  // dense kernels: one thread per slot
+  const size_t sh = (size_t)kWfBlock * p.stack_depth * sizeof(int);
+  static int g_ext = 0, g_occ_h = 0, g_occ_s = 0;
+  static size_t g_sh = 0;
+  if (g_sh != sh || !g_ext) {
+    g_ext = resident_grid(wf_extend<kCount>, sh);
+    g_occ_h = resident_grid(wf_occlude<kCount, false>, sh);
+    g_occ_s = resident_grid(wf_occlude<kCount, true>, sh);
+    g_sh = sh;
+  }
+  hipLaunchKernelGGL((wf_extend<kCount>), dim3(g_ext), b, sh, st, p);
+  hipLaunchKernelGGL((wf_shade1<kCount>), gd, b, 0, st, p);
   if (p.nl > 0) {
-    hipLaunchKernelGGL((wf_hard<kCount>), gq, b, sh, st, p);
+    hipLaunchKernelGGL((wf_occlude<kCount, false>), dim3(g_occ_h), b, sh, st, p);
     if (p.soft) {
-      hipLaunchKernelGGL((wf_softgen<kCount>), gp, b, 0, st, p);
-      hipLaunchKernelGGL((wf_soft<kCount>), gq, b, sh, st, p);
+      hipLaunchKernelGGL((wf_softgen<kCount>), gd, b, 0, st, p);
+      hipLaunchKernelGGL((wf_occlude<kCount, true>), dim3(g_occ_s), b, sh, st, p);
     }
   }
-  hipLaunchKernelGGL((wf_shade2<kCount>), gp, b, 0, st, p);
-  return (int)hipGetLastError();
+  hipLaunchKernelGGL((wf_shade<kCount>), gd, b, 0, st, p);
+  return enqueue_regen_book<kCount>(p, st);
 }
 
-template <bool kCount>
-static int enqueue_regen(const WfParams& p, hipStream_t st) {
-  hipLaunchKernelGGL(wf_book_regen, dim3(1), dim3(1), 0, st, p.ctl, p.capacity);
-  const dim3 g(std::min((p.capacity + kWfBlock - 1) / kWfBlock, 256 * 32));
-  hipLaunchKernelGGL((wf_regen<kCount>), g, dim3(kWfBlock), 0, st, p);
-  hipLaunchKernelGGL(wf_book_swap, dim3(1), dim3(1), 0, st, p.ctl);
-  return (int)hipGetLastError();
+// first == true: the arrays are empty; only regen + book (the first samples)
+int wf_launch_bounce(const WfParams& p, bool first, bool count, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (first) return count ? enqueue_regen_book<true>(p, st) : enqueue_regen_book<false>(p, st);
+  return count ? enqueue_bounce<true>(p, st) : enqueue_bounce<false>(p, st);
 }
 
-int wf_launch_regen(const WfParams& p, bool count, void* stream) {
-  return count ? enqueue_regen<true>(p, (hipStream_t)stream) : enqueue_regen<false>(p, (hipStream_t)stream);
-}
-int wf_launch_iteration(const WfParams& p, bool count, void* stream) {
-  return count ? enqueue_iteration<true>(p, (hipStream_t)stream) : enqueue_iteration<false>(p, (hipStream_t)stream);
-}
 int wf_launch_resolve(const WfParams& p, int npix, void* stream) {
   if (npix <= 0) return hipSuccess;
   hipLaunchKernelGGL(wf_resolve, dim3((npix + kWfBlock - 1) / kWfBlock), dim3(kWfBlock), 0, (hipStream_t)stream, p,

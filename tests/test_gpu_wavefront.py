@@ -95,9 +95,9 @@ def test_wavefront_all_sphere_materials_matches_oracle(monkeypatch):
     assert rgba.reshape(40, 60, 4).tobytes() == ref_rgba.tobytes()
 
 
-@pytest.mark.parametrize("env", [{"RTGO_WF_PATHS": "64"}, {"RTGO_WF_PATHS": "1000"},
+@pytest.mark.parametrize("env", [{"RTGO_WF_PATHS": "64"}, {"RTGO_WF_PATHS": "4096"},
                                  {"RTGO_WF_CHUNK": "700"}, {"RTGO_WF_PATHS": "128", "RTGO_WF_CHUNK": "3000"}],
-                         ids=["64_paths", "1000_paths", "chunks", "both"])
+                         ids=["64_paths", "4096_paths", "chunks", "both"])
 def test_capacity_and_chunks_do_not_change_the_image(env, monkeypatch):
     scene = rtgo.Scene.from_json_text(json.dumps(_sphere_field(200, seed=9)))
     st = make_settings(rtgo, {"samples": 7})
