@@ -73,6 +73,7 @@ constexpr int kLeafMax = 4;
 
 void build_sphere_bvh(FlatScene* fs) {
   fs->bvh.clear();
+  fs->qbvh.clear();
   const int n = (int)fs->spheres.size();
   if (n == 0) return;
   std::vector<Box> pb(n);
@@ -213,6 +214,40 @@ void build_sphere_bvh(FlatScene* fs) {
       return;
     }
     fs->bvh_depth = maxd;
+  }
+  // quantized copy: a grid of 65000 steps per axis over the root box with 4
+  // steps of margin; lo rounded down, hi up, one more step each way, and the
+  // decoded box checked to contain the float box
+  {
+    const DBVHNode& r = nodes[0];
+    for (int k = 0; k < 3; ++k) {
+      const double ext = (double)r.hi[k] - (double)r.lo[k];
+      fs->qd[k] = ext > 0 ? ext / 65000.0 : 1.0;
+      fs->q0[k] = (double)r.lo[k] - 4 * fs->qd[k];
+    }
+    fs->qbvh.resize(nodes.size());
+    for (size_t i = 0; i < nodes.size(); ++i) {
+      const DBVHNode& nd = nodes[i];
+      uint32_t ql[3], qh[3];
+      for (int k = 0; k < 3; ++k) {
+        double a = floor(((double)nd.lo[k] - fs->q0[k]) / fs->qd[k]) - 1;
+        double b = ceil(((double)nd.hi[k] - fs->q0[k]) / fs->qd[k]) + 1;
+        a = std::min(std::max(a, 0.0), 65535.0);
+        b = std::min(std::max(b, 0.0), 65535.0);
+        if (!(fs->q0[k] + a * fs->qd[k] <= (double)nd.lo[k]) || !(fs->q0[k] + b * fs->qd[k] >= (double)nd.hi[k])) {
+          fs->bvh.clear();  // cannot happen for finite boxes; keep the linear scan rather than cull wrongly
+          fs->qbvh.clear();
+          return;
+        }
+        ql[k] = (uint32_t)a;
+        qh[k] = (uint32_t)b;
+      }
+      DQNode& q = fs->qbvh[i];
+      q.w[0] = ql[0] | (ql[1] << 16);
+      q.w[1] = ql[2] | (qh[0] << 16);
+      q.w[2] = qh[1] | (qh[2] << 16);
+      q.w[3] = (uint32_t)((nd.left_or_first << 3) | nd.count);
+    }
   }
   std::vector<DSphere> reordered(n);
   for (int i = 0; i < n; ++i) reordered[i] = fs->spheres[idx[i]];

@@ -313,6 +313,7 @@ struct rt_context {
   const DMat* d_mats = nullptr;
   const DLight* d_lights = nullptr;
   const DBVHNode* d_bvh = nullptr;
+  const DQNode* d_qbvh = nullptr;
   const uint64_t* d_jump = nullptr;
   unsigned long long* d_counts = nullptr;
   hipStream_t last_stream = nullptr;
@@ -454,7 +455,8 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   size_t off_l = off_m + al(f.mats.size() * sizeof(DMat));
   size_t off_j = off_l + al(f.lights.size() * sizeof(DLight));
   size_t off_b = off_j + al(kJump * 2 * sizeof(uint64_t));
-  size_t total = off_b + al(f.bvh.size() * sizeof(DBVHNode)) + 256;
+  size_t off_q = off_b + al(f.bvh.size() * sizeof(DBVHNode));
+  size_t total = off_q + al(f.qbvh.size() * sizeof(DQNode)) + 256;
   if (c->stream) HIP_TRY(hipStreamSynchronize(c->stream));
   if (c->d_scene && c->d_scene_bytes < total) {
     HIP_TRY(hipFree(c->d_scene));
@@ -484,6 +486,7 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
     }
   }
   memcpy(host.data() + off_b, f.bvh.data(), f.bvh.size() * sizeof(DBVHNode));
+  memcpy(host.data() + off_q, f.qbvh.data(), f.qbvh.size() * sizeof(DQNode));
   HIP_TRY(hipMemcpy(base, host.data(), total, hipMemcpyHostToDevice));
   c->d_spheres = (const DSphere*)(base + off_s);
   c->d_tris = (const DTri*)(base + off_t);
@@ -491,6 +494,7 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   c->d_mats = (const DMat*)(base + off_m);
   c->d_lights = (const DLight*)(base + off_l);
   c->d_bvh = (const DBVHNode*)(base + off_b);
+  c->d_qbvh = (const DQNode*)(base + off_q);
   c->d_jump = (const uint64_t*)(base + off_j);
   // small linear-scan scenes are staged into LDS by every workgroup
   // (the 1 KB PCG jump table stays in global memory, L1-cached: only the
@@ -710,6 +714,9 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   WfParams p;
   memset(&p, 0, sizeof p);
   p.g = Geo{kp.spheres, kp.tris, kp.boxes, kp.bvh, kp.ns, kp.nt, kp.use_bvh, kp.nb};
+  p.qbvh = c->d_qbvh;
+  memcpy(p.q0, f.q0, sizeof p.q0);
+  memcpy(p.qd, f.qd, sizeof p.qd);
   p.mats = kp.mats;
   p.lights = kp.lights;
   p.nl = nl;

@@ -23,6 +23,8 @@ struct FlatScene {
   std::vector<DLight> lights;
   std::vector<DBVHNode> bvh;  // empty => linear scan
   int32_t bvh_depth = 0;      // levels of the BVH (root = 1): the traversal stack holds fewer entries
+  std::vector<DQNode> qbvh;   // the BVH with quantized bounds (same node order)
+  double q0[3] = {0, 0, 0}, qd[3] = {1, 1, 1};  // its grid: coordinate = q0 + q * qd
   double cam_pos[3] = {0, 0, 0};
   double aspect = 0;
   int32_t objects = 0;        // len(hittables)
@@ -143,6 +145,8 @@ struct WfPaths {             // structure of arrays, kWfShards * shard_cap slots
 };
 struct WfParams {
   Geo g;
+  const DQNode* qbvh;        // quantized BVH (FlatScene::qbvh) and its grid
+  double q0[3], qd[3];
   const DMat* mats;
   const DLight* lights;
   int32_t nl, max_depth, recursive, soft, spp;

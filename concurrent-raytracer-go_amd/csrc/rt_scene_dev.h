@@ -89,4 +89,13 @@ struct alignas(16) DBVHNode {  // 32 B
   int32_t count;          // 0 = internal node
 };
 
+// The same BVH with 16-bit quantized bounds (the wavefront kernels,
+// rt_wavefront.hip): bounds are grid indices q (coordinate = q0 + q * qd per
+// axis, FlatScene), rounded outward; 16 B per node, a child pair in one
+// 32-B load.  w[0] = lo.x | lo.y << 16, w[1] = lo.z | hi.x << 16,
+// w[2] = hi.y | hi.z << 16, w[3] = traversal code (first << 3 | count).
+struct alignas(16) DQNode {  // 16 B
+  uint32_t w[4];
+};
+
 }  // namespace rtgo

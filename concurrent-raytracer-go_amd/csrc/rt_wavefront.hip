@@ -47,6 +47,10 @@
 namespace rtgo {
 
 constexpr int kWfBlock = kWfBlockSlots;  // threads per workgroup of every kernel
+#ifndef RT_WF_TRAV_WAVES
+#define RT_WF_TRAV_WAVES 6  // waves per SIMD the traversal kernels are compiled for
+#endif
+#define RT_TRAV_ATTR __launch_bounds__(kWfBlock) __attribute__((amdgpu_waves_per_eu(RT_WF_TRAV_WAVES)))
 constexpr int kRefill = 16;              // persistent traversal: refill once this many lanes are idle
 constexpr int kChunk = 256;              // persistent traversal: jobs a wave takes per atomic
 constexpr uint32_t kHardBit = 1u << 16;  // lstate: the hard shadow ray is blocked (low bits: blocked soft rays)
@@ -167,25 +171,90 @@ __device__ __forceinline__ void finish(const WfParams& p, uint32_t sid, d3 L) {
 }
 
 // ---------------------------------------------------------------- traversal
-// One step of the while-while traversal of a lane (bvh.cpp layout; the same
-// tests as closest_hit / any_hit in rt_device.h): descend internal nodes,
-// nearer child first, until `cur` is a leaf (count 1..4) or -1 (done).
+// Slab tests against the quantized BVH (DQNode: 16-bit grid indices, bounds
+// rounded outward, bvh.cpp).  For a grid index q on axis k the slab distance
+// is t = (q0 + q qd - o) inv = q A + B with A = qd inv, B = (q0 - o) inv
+// (binary64, then rounded).  The kernel builds q as a float exactly (the bits
+// of 2^23 + q by one v_perm_b32, minus 2^23) and evaluates fma(q, A, B) in
+// binary32: error <= 2^-24 (65535 |A| + |B|) + the fma rounding.  The bound
+// e_k = 2^-22 (65536 |A| + |B|) is folded into the B used for the near and
+// for the far bound of axis k (pushed outward: down for the near side, up for
+// the far side), so the interval only ever grows; the fma rounding is covered
+// by the relative slack 2^-20 (|tn| + |tf|).  The origin enters in binary64.
+// A ray whose coefficients are not finite tests every box as hit (A = B = 0,
+// eps = inf): slower, exact.
+typedef float f2 __attribute__((ext_vector_type(2)));
+struct RayQ {
+  f2 a, bx, by, bz;  // a = (A_x, A_y); b*: B biased for the lo and hi bound of the axis
+  float az, eps;
+};
+__device__ __forceinline__ void ray_q_axis(double q0, double qd, double o, double id, float& a, f2& b, bool& ok) {
+  const double ik = fmin(fmax(id, -1e30), 1e30);
+  const double A = qd * ik, B = (q0 - o) * ik;
+  const double e = (65536.0 * fabs(A) + fabs(B)) * 0x1p-22;
+  // lo bound: near side when inv > 0 (push down), far side otherwise (push up)
+  const double blo = ik > 0 ? B - e : B + e, bhi = ik > 0 ? B + e : B - e;
+  a = (float)A;
+  b = f2{(float)blo, (float)bhi};
+  ok = ok && __builtin_isfinite(A) && __builtin_isfinite(blo) && __builtin_isfinite(bhi) && fabs(blo) < 1e30 &&
+       fabs(bhi) < 1e30 && fabs(A) < 1e30;
+}
+__device__ __forceinline__ RayQ ray_q(const WfParams& p, d3 o, d3 id) {
+  RayQ r;
+  bool ok = true;
+  float ax, ay;
+  ray_q_axis(p.q0[0], p.qd[0], o.x, id.x, ax, r.bx, ok);
+  ray_q_axis(p.q0[1], p.qd[1], o.y, id.y, ay, r.by, ok);
+  ray_q_axis(p.q0[2], p.qd[2], o.z, id.z, r.az, r.bz, ok);
+  r.a = f2{ax, ay};
+  r.eps = 0.f;
+  if (!ok) {
+    r.a = f2{0.f, 0.f};
+    r.az = 0.f;
+    r.bx = r.by = r.bz = f2{0.f, 0.f};
+    r.eps = __builtin_inff();
+  }
+  return r;
+}
+// q (16-bit half of w) as an exact float: bits of 2^23 + q, minus 2^23
+__device__ __forceinline__ float q_bits_lo(uint32_t w) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_perm(0x4B000000u, w, 0x070c0100u));
+}
+__device__ __forceinline__ float q_bits_hi(uint32_t w) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_perm(0x4B000000u, w, 0x070c0302u));
+}
+__device__ __forceinline__ bool box_q(const uint4 n, const RayQ& r, float tmin, float tmax, float& tn) {
+  const f2 k23 = f2{8388608.f, 8388608.f};
+  const f2 qx = f2{q_bits_lo(n.x), q_bits_hi(n.y)} - k23;  // (lo.x, hi.x)
+  const f2 qy = f2{q_bits_hi(n.x), q_bits_lo(n.z)} - k23;  // (lo.y, hi.y)
+  const f2 qz = f2{q_bits_lo(n.y), q_bits_hi(n.z)} - k23;  // (lo.z, hi.z)
+  const f2 tx = __builtin_elementwise_fma(qx, f2{r.a.x, r.a.x}, r.bx);
+  const f2 ty = __builtin_elementwise_fma(qy, f2{r.a.y, r.a.y}, r.by);
+  const f2 tz = __builtin_elementwise_fma(qz, f2{r.az, r.az}, r.bz);
+  tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fmaxf(fminf(tz.x, tz.y), tmin));
+  const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fminf(fmaxf(tz.x, tz.y), tmax));
+  return tn <= tf + (fabsf(tn) + fabsf(tf)) * 0x1p-20f + r.eps;
+}
+
+// One step of the while-while traversal of a lane (the closest_hit / any_hit
+// order of rt_device.h over the same tree): descend internal nodes, nearer
+// child first, until `cur` is a leaf (count 1..4) or -1 (done).
 template <bool kCount>
-__device__ __forceinline__ void descend(const DBVHNode* __restrict__ bvh, const Ray32& r, float tminf,
-                                        float tmaxf, int& cur, int& sp, int* stack, Counters& c) {
+__device__ __forceinline__ void descend(const uint4* __restrict__ qb, const RayQ& r, float tminf, float tmaxf,
+                                        int& cur, int& sp, int* stack, Counters& c) {
   while ((cur & 7) == 0) {
     const int first = cur >> 3;
-    const DBVHNode L = bvh[first], R = bvh[first + 1];
+    const uint4 L = qb[first], R = qb[first + 1];
     cnt<kCount>(c, C_BOX, 2);
     float tl, tr;
-    const bool hl = box_hit32(L, r, tminf, tmaxf, tl), hr = box_hit32(R, r, tminf, tmaxf, tr);
+    const bool hl = box_q(L, r, tminf, tmaxf, tl), hr = box_q(R, r, tminf, tmaxf, tr);
     if (hl || hr) {
       const bool lfirst = hl && (!hr || tl <= tr);
       if (hl && hr) {
-        stack[sp * 64] = lfirst ? bvh_code(R) : bvh_code(L);
+        stack[sp * 64] = lfirst ? (int)R.w : (int)L.w;
         ++sp;
       }
-      cur = lfirst ? bvh_code(L) : bvh_code(R);
+      cur = lfirst ? (int)L.w : (int)R.w;
     } else {
       cur = sp == 0 ? -1 : stack[--sp * 64];
     }
@@ -228,7 +297,7 @@ __device__ __forceinline__ bool job_refill(JobSrc& js, int32_t* heads, int n) {
 // refills idle lanes from them.  A hit leaves (sphere, root numerator) for
 // shade1; a miss ends the path with the radiance it has (renderer.go:170-173).
 template <bool kCount>
-__global__ __launch_bounds__(kWfBlock) void wf_extend(const WfParams p) {
+__global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
   const Dense dn = dense(p.ctl->cur_cnt);
   const int n = dn.start[kWfShards];
   if (n == 0) return;
@@ -246,7 +315,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_extend(const WfParams p) {
   size_t slot = 0;
   d3 o = mk(0, 0, 0), d = mk(0, 0, 0);
   double av = 0, inv_a = 0, closest = 0, bnum = 0;
-  Ray32 r32{};
+  RayQ r32{};
   float tminf = 0;
   int cur = -1, sp = 0, best_obj = -1, bidx = -1;
   for (;;) {
@@ -271,7 +340,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_extend(const WfParams p) {
           const d3 id = inv_dir(d);
           cnt<kCount>(c, C_BOX);
           if (box_hit(p.g.bvh[0], o, id, tmin, closest)) {
-            r32 = ray32(o, id);
+            r32 = ray_q(p, o, id);
             tminf = t_lo32(tmin);
             cur = bvh_code(p.g.bvh[0]);
             sp = 0;
@@ -290,7 +359,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_extend(const WfParams p) {
       continue;
     }
     if (busy) {
-      descend<kCount>(p.g.bvh, r32, tminf, t_hi32(closest), cur, sp, stack, c);
+      descend<kCount>(reinterpret_cast<const uint4*>(p.qbvh), r32, tminf, t_hi32(closest), cur, sp, stack, c);
       if (cur != -1) {  // a leaf: the exact Sphere.Hit tests, in hittable order
         const int first = cur >> 3, count = cur & 7;
         for (int i = first; i < first + count; ++i) {
@@ -389,7 +458,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade1(const WfParams p) {
 // (path, light) count; hard: the ray is lightDir and a blocked ray sets
 // kHardBit.
 template <bool kCount, bool kSoft>
-__global__ __launch_bounds__(kWfBlock) void wf_occlude(const WfParams p) {
+__global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
   const Dense dn = dense(kSoft ? p.ctl->soft_cnt : p.ctl->hard_cnt);
   const int n = dn.start[kWfShards];
   if (n == 0) return;
@@ -406,7 +475,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_occlude(const WfParams p) {
   uint32_t key = 0;
   d3 o = mk(0, 0, 0), d = mk(0, 0, 0);
   double av = 0, inv_a = 0, tmax = 0;
-  Ray32 r32{};
+  RayQ r32{};
   float tminf = 0, tmaxf = 0;
   int cur = -1, sp = 0;
   for (;;) {
@@ -440,7 +509,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_occlude(const WfParams p) {
         const d3 id = inv_dir(d);
         cnt<kCount>(c, C_BOX);
         if (box_hit(p.g.bvh[0], o, id, tmin, tmax)) {
-          r32 = ray32(o, id);
+          r32 = ray_q(p, o, id);
           tminf = t_lo32(tmin);
           tmaxf = t_hi32(tmax);
           cur = bvh_code(p.g.bvh[0]);
@@ -454,7 +523,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_occlude(const WfParams p) {
       continue;
     }
     if (busy) {
-      descend<kCount>(p.g.bvh, r32, tminf, tmaxf, cur, sp, stack, c);
+      descend<kCount>(reinterpret_cast<const uint4*>(p.qbvh), r32, tminf, tmaxf, cur, sp, stack, c);
       bool blocked = false;
       if (cur != -1) {
         const int first = cur >> 3, count = cur & 7;
