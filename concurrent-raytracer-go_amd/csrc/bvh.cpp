@@ -8,7 +8,7 @@
 // same closest hit as the linear scan (same Sphere.Hit arithmetic, exact-t
 // ties resolved by hittable index, as in the scan).
 //
-// Layout: nodes in depth-first order with the two children of an internal
+// Layout: nodes in breadth-first order with the two children of an internal
 // node adjacent (left = i, right = i + 1), 32 B each, float bounds rounded
 // outward by one ulp so a box never excludes a point of its spheres.  Every
 // sphere box is also padded by pad = 2^-18 * M, M the largest coordinate
@@ -193,6 +193,22 @@ void build_sphere_bvh(FlatScene* fs) {
     nodes[t.node].count = 0;
     stack.push_back({left + 1, mid, t.first + t.count - mid});
     stack.push_back({left, t.first, mid - t.first});
+  }
+  // breadth-first renumbering (child pairs stay adjacent): the top levels of
+  // the tree become a prefix of the node array, which the wavefront traversal
+  // kernels stage in LDS (rt_wavefront.hip stage_tree)
+  {
+    std::vector<DBVHNode> bfs;
+    bfs.reserve(nodes.size());
+    bfs.push_back(nodes[0]);
+    for (size_t i = 0; i < bfs.size(); ++i) {
+      if (bfs[i].count != 0) continue;
+      const int old = bfs[i].left_or_first;
+      bfs[i].left_or_first = (int)bfs.size();
+      bfs.push_back(nodes[old]);
+      bfs.push_back(nodes[old + 1]);
+    }
+    nodes.swap(bfs);
   }
   // depth check: traversal keeps at most depth-1 pending children on its
   // per-lane LDS stack, which the kernels size to the tree's depth (at most

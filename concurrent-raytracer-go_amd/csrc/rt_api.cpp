@@ -731,7 +731,18 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   p.tiles_x = kp.tiles_x;
   p.ntiles = kp.ntiles;
   p.layout = kp.layout;
-  p.stack_depth = kp.stack_depth;
+  // a lane holds at most one pending child per internal node above its leaf:
+  // depth - 1 entries (leaves at level bvh_depth, the root at level 1)
+  p.stack_depth = std::max(1, f.bvh_depth - 1);
+  // traversal workgroups: RTGO_WF_TRAV_BLOCK threads (64..1024), LDS shared by
+  // RTGO_WF_TRAV_WGS of them per CU (experiments; default one of 1024)
+  p.trav_block = kWfTravBlock;
+  int trav_wgs = 1;
+  if (const char* e = getenv("RTGO_WF_TRAV_BLOCK")) p.trav_block = std::max(1, std::min(16, atoi(e) / 64)) * 64;
+  if (const char* e = getenv("RTGO_WF_TRAV_WGS")) trav_wgs = std::max(1, std::min(32, atoi(e)));
+  p.lds_nodes = wf_lds_nodes(p.stack_depth, (int)f.qbvh.size(), p.trav_block, trav_wgs);
+  if (const char* e = getenv("RTGO_WF_LDS_NODES"))  // tests / experiments: stage fewer nodes
+    p.lds_nodes = std::min(p.lds_nodes, std::max(0, atoi(e)) | 1);
   p.shard_cap = shard_cap;
   p.hard_cap = (int64_t)qcap;
   p.soft_cap = (int64_t)qcap * 16;

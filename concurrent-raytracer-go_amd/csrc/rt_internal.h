@@ -122,6 +122,7 @@ struct Geo {
 // (rt_wavefront.hip: BVH scenes)
 constexpr int kWfShards = 8;           // queues / path arrays are split in 8 shards (one atomic word each)
 constexpr int kWfBlockSlots = 256;     // threads per workgroup of the wavefront kernels
+constexpr int kWfTravBlock = 1024;     // ... of the traversal kernels (extend, occlude): one per CU, BVH in LDS
 constexpr uint32_t kDeadSid = 0xFFFFFFFFu;  // a slot with no sample (out-of-image pixel of an edge tile)
 struct WfCtl {                 // device-resident loop state; counters of shard s at [32 s] (own 128-B line)
   int32_t cur_cnt[kWfShards * 32];   // live paths per shard of the current array
@@ -151,7 +152,9 @@ struct WfParams {
   const DLight* lights;
   int32_t nl, max_depth, recursive, soft, spp;
   int32_t W, H, rank, world, tiles_x, ntiles, layout;
-  int32_t stack_depth;       // BVH stack entries per lane (the tree's depth)
+  int32_t stack_depth;       // BVH stack entries per lane (the tree's depth - 1)
+  int32_t lds_nodes;         // leading quantized nodes (breadth-first: the top levels) staged in LDS
+  int32_t trav_block;        // threads per workgroup of the traversal kernels (<= kWfTravBlock)
   int32_t shard_cap;         // path slots per shard
   int64_t hard_cap, soft_cap;  // queue entries per shard
   uint32_t lp0;              // first local pixel of the chunk (local tile * 1024 + pixel in tile)
@@ -173,6 +176,9 @@ struct WfParams {
   uint8_t* out_rgba;
 };
 int wf_launch_bounce(const WfParams& p, bool first, bool count, void* stream);
+// Quantized nodes the traversal kernels can stage in LDS next to their stacks
+// (all of them when they fit; else an odd count, so no child pair is split).
+int wf_lds_nodes(int stack_depth, int nodes, int block, int wgs_per_cu);
 int wf_launch_resolve(const WfParams& p, int npix, void* stream);
 
 // ---------------------------------------------------------------- output

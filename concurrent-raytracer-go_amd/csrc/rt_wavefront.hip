@@ -40,17 +40,25 @@
 // a copy of it one bounce behind the GPU to know when the frame is done.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "../../include/rt_rng.h"
 #include "rt_device.h"
 #include "rt_internal.h"
 
 namespace rtgo {
 
-constexpr int kWfBlock = kWfBlockSlots;  // threads per workgroup of every kernel
+constexpr int kWfBlock = kWfBlockSlots;  // threads per workgroup of the dense kernels
+// Traversal kernels: by default one 1024-thread workgroup per CU (4 waves per
+// SIMD), whose LDS holds the lanes' stacks and as much of the quantized BVH as
+// fits behind them (10k spheres: all 6,623 nodes, 104 KB).  The launch size
+// (p.trav_block <= kTravBlock) and workgroups per CU are host choices.
+constexpr int kTravBlock = kWfTravBlock;
 #ifndef RT_WF_TRAV_WAVES
-#define RT_WF_TRAV_WAVES 6  // waves per SIMD the traversal kernels are compiled for
+#define RT_WF_TRAV_WAVES 4  // waves per SIMD the traversal kernels are compiled for
 #endif
-#define RT_TRAV_ATTR __launch_bounds__(kWfBlock) __attribute__((amdgpu_waves_per_eu(RT_WF_TRAV_WAVES)))
+#define RT_TRAV_ATTR __launch_bounds__(kTravBlock) __attribute__((amdgpu_waves_per_eu(RT_WF_TRAV_WAVES)))
+constexpr int kLdsBytes = 160 * 1024;    // LDS per CU (MI355X), all of it available to one workgroup
 constexpr int kRefill = 16;              // persistent traversal: refill once this many lanes are idle
 constexpr int kChunk = 256;              // persistent traversal: jobs a wave takes per atomic
 constexpr uint32_t kHardBit = 1u << 16;  // lstate: the hard shadow ray is blocked (low bits: blocked soft rays)
@@ -61,6 +69,25 @@ extern __shared__ __attribute__((aligned(16))) unsigned char wf_lds[];
 // lane-interleaved (closest_hit / any_hit index it with stride 64)
 __device__ __forceinline__ int* wf_stack(int depth) {
   return reinterpret_cast<int*>(wf_lds) + (threadIdx.x >> 6) * 64 * depth + (threadIdx.x & 63);
+}
+
+// The first p.lds_nodes quantized nodes (breadth-first order, bvh.cpp: the
+// top of the tree, or all of it) copied into LDS behind the stacks, once per
+// workgroup of a persistent traversal kernel.  Divergent lanes then read
+// their node pairs as ds_read_b128 (~50 cycles, 256 B/clk per CU) instead of
+// one vector-L1 line per lane.  Every thread must call it.
+// (Typed address spaces keep the two loads of descend apart: through generic
+// pointers the compiler merges them into one select + flat load.)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const u32x4 lds_node;
+typedef __attribute__((address_space(1))) const u32x4 glb_node;
+__device__ __forceinline__ uint4 as_uint4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ lds_node* stage_tree(const WfParams& p) {
+  uint4* t = reinterpret_cast<uint4*>(wf_lds + (size_t)p.trav_block * p.stack_depth * sizeof(int));
+  const uint4* src = reinterpret_cast<const uint4*>(p.qbvh);
+  for (int i = threadIdx.x; i < p.lds_nodes; i += p.trav_block) t[i] = src[i];
+  __syncthreads();
+  return (lds_node*)t;
 }
 
 // Block-wide exclusive prefix of a per-lane count over the workgroup (wave
@@ -239,12 +266,22 @@ __device__ __forceinline__ bool box_q(const uint4 n, const RayQ& r, float tmin, 
 // One step of the while-while traversal of a lane (the closest_hit / any_hit
 // order of rt_device.h over the same tree): descend internal nodes, nearer
 // child first, until `cur` is a leaf (count 1..4) or -1 (done).
+// Node pairs below `nlds` come from the LDS copy `lt` (stage_tree), the rest
+// from global memory.
 template <bool kCount>
-__device__ __forceinline__ void descend(const uint4* __restrict__ qb, const RayQ& r, float tminf, float tmaxf,
-                                        int& cur, int& sp, int* stack, Counters& c) {
+__device__ __forceinline__ void descend(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
+                                        const RayQ& r, float tminf, float tmaxf, int& cur, int& sp, int* stack,
+                                        Counters& c) {
   while ((cur & 7) == 0) {
     const int first = cur >> 3;
-    const uint4 L = qb[first], R = qb[first + 1];
+    uint4 L, R;
+    if (first < nlds) {  // nlds is odd or the whole tree: a staged pair is whole
+      L = as_uint4(lt[first]);
+      R = as_uint4(lt[first + 1]);
+    } else {
+      L = as_uint4(qb[first]);
+      R = as_uint4(qb[first + 1]);
+    }
     cnt<kCount>(c, C_BOX, 2);
     float tl, tr;
     const bool hl = box_q(L, r, tminf, tmaxf, tl), hr = box_q(R, r, tminf, tmaxf, tr);
@@ -301,6 +338,7 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
   const Dense dn = dense(p.ctl->cur_cnt);
   const int n = dn.start[kWfShards];
   if (n == 0) return;
+  lds_node* lt = stage_tree(p);
   JobSrc js{0, 0, 0};
   bool more = true;  // wave-uniform: jobs may remain
   Counters c;
@@ -359,7 +397,7 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
       continue;
     }
     if (busy) {
-      descend<kCount>(reinterpret_cast<const uint4*>(p.qbvh), r32, tminf, t_hi32(closest), cur, sp, stack, c);
+      descend<kCount>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, t_hi32(closest), cur, sp, stack, c);
       if (cur != -1) {  // a leaf: the exact Sphere.Hit tests, in hittable order
         const int first = cur >> 3, count = cur & 7;
         for (int i = first; i < first + count; ++i) {
@@ -462,6 +500,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
   const Dense dn = dense(kSoft ? p.ctl->soft_cnt : p.ctl->hard_cnt);
   const int n = dn.start[kWfShards];
   if (n == 0) return;
+  lds_node* lt = stage_tree(p);
   JobSrc js{0, 0, 0};
   bool more = true;  // wave-uniform: jobs may remain
   Counters c;
@@ -523,7 +562,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
       continue;
     }
     if (busy) {
-      descend<kCount>(reinterpret_cast<const uint4*>(p.qbvh), r32, tminf, tmaxf, cur, sp, stack, c);
+      descend<kCount>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, tmaxf, cur, sp, stack, c);
       bool blocked = false;
       if (cur != -1) {
         const int first = cur >> 3, count = cur & 7;
@@ -810,12 +849,27 @@ __global__ __launch_bounds__(kWfBlock) void wf_resolve(const WfParams p, int npi
 // ---------------------------------------------------------------- launches
 // persistent kernels: as many workgroups as fit on the device at once
 template <typename K>
-static int resident_grid(K kernel, size_t shmem) {
+static int resident_grid(K kernel, int block, size_t shmem) {
   int dev = 0, cus = 0, per = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 1024;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kWfBlock, shmem) != hipSuccess || per < 1) per = 1;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 256;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)shmem);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, shmem) != hipSuccess || per < 1) per = 1;
   return cus * per;
+}
+
+static size_t trav_shmem(const WfParams& p) {
+  return (size_t)p.trav_block * p.stack_depth * sizeof(int) + (size_t)p.lds_nodes * sizeof(uint4);
+}
+
+int wf_lds_nodes(int stack_depth, int nodes, int block, int wgs_per_cu) {
+  const long long room =
+      ((long long)kLdsBytes / std::max(1, wgs_per_cu) - (long long)block * stack_depth * (long long)sizeof(int)) /
+      (long long)sizeof(uint4);
+  if (room >= nodes) return nodes;
+  if (room < 1) return 0;
+  return (int)(room % 2 ? room : room - 1);
 }
 
 template <bool kCount>
@@ -828,24 +882,25 @@ static int enqueue_regen_book(const WfParams& p, hipStream_t st) {
 
 template <bool kCount>
 static int enqueue_bounce(const WfParams& p, hipStream_t st) {
-  const dim3 b(kWfBlock);
+  const dim3 b(kWfBlock), bt(p.trav_block);
   const dim3 gd((kWfShards * p.shard_cap + kWfBlock - 1) / kWfBlock);  // dense kernels: one thread per slot
-  const size_t sh = (size_t)kWfBlock * p.stack_depth * sizeof(int);
-  static int g_ext = 0, g_occ_h = 0, g_occ_s = 0;
+  const size_t sh = trav_shmem(p);
+  static int g_ext = 0, g_occ_h = 0, g_occ_s = 0, g_block = 0;
   static size_t g_sh = 0;
-  if (g_sh != sh || !g_ext) {
-    g_ext = resident_grid(wf_extend<kCount>, sh);
-    g_occ_h = resident_grid(wf_occlude<kCount, false>, sh);
-    g_occ_s = resident_grid(wf_occlude<kCount, true>, sh);
+  if (g_sh != sh || g_block != p.trav_block || !g_ext) {
+    g_ext = resident_grid(wf_extend<kCount>, p.trav_block, sh);
+    g_occ_h = resident_grid(wf_occlude<kCount, false>, p.trav_block, sh);
+    g_occ_s = resident_grid(wf_occlude<kCount, true>, p.trav_block, sh);
     g_sh = sh;
+    g_block = p.trav_block;
   }
-  hipLaunchKernelGGL((wf_extend<kCount>), dim3(g_ext), b, sh, st, p);
+  hipLaunchKernelGGL((wf_extend<kCount>), dim3(g_ext), bt, sh, st, p);
   hipLaunchKernelGGL((wf_shade1<kCount>), gd, b, 0, st, p);
   if (p.nl > 0) {
-    hipLaunchKernelGGL((wf_occlude<kCount, false>), dim3(g_occ_h), b, sh, st, p);
+    hipLaunchKernelGGL((wf_occlude<kCount, false>), dim3(g_occ_h), bt, sh, st, p);
     if (p.soft) {
       hipLaunchKernelGGL((wf_softgen<kCount>), gd, b, 0, st, p);
-      hipLaunchKernelGGL((wf_occlude<kCount, true>), dim3(g_occ_s), b, sh, st, p);
+      hipLaunchKernelGGL((wf_occlude<kCount, true>), dim3(g_occ_s), bt, sh, st, p);
     }
   }
   hipLaunchKernelGGL((wf_shade<kCount>), gd, b, 0, st, p);

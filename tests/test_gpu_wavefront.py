@@ -96,9 +96,12 @@ def test_wavefront_all_sphere_materials_matches_oracle(monkeypatch):
 
 
 @pytest.mark.parametrize("env", [{"RTGO_WF_PATHS": "64"}, {"RTGO_WF_PATHS": "4096"},
-                                 {"RTGO_WF_CHUNK": "700"}, {"RTGO_WF_PATHS": "128", "RTGO_WF_CHUNK": "3000"}],
-                         ids=["64_paths", "4096_paths", "chunks", "both"])
+                                 {"RTGO_WF_CHUNK": "700"}, {"RTGO_WF_PATHS": "128", "RTGO_WF_CHUNK": "3000"},
+                                 {"RTGO_WF_LDS_NODES": "0"}, {"RTGO_WF_LDS_NODES": "31"}],
+                         ids=["64_paths", "4096_paths", "chunks", "both", "bvh_all_global", "bvh_top_in_lds"])
 def test_capacity_and_chunks_do_not_change_the_image(env, monkeypatch):
+    """... nor how much of the BVH the traversal kernels stage in LDS (by
+    default all of it; here none, or only the top 31 nodes)."""
     scene = rtgo.Scene.from_json_text(json.dumps(_sphere_field(200, seed=9)))
     st = make_settings(rtgo, {"samples": 7})
     base = _render(scene, 50, 37, st, monkeypatch, mega=False)
