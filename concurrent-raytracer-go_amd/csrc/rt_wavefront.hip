@@ -201,19 +201,23 @@ __device__ __forceinline__ void finish(const WfParams& p, uint32_t sid, d3 L) {
 // Slab tests against the quantized BVH (DQNode: 16-bit grid indices, bounds
 // rounded outward, bvh.cpp).  For a grid index q on axis k the slab distance
 // is t = (q0 + q qd - o) inv = q A + B with A = qd inv, B = (q0 - o) inv
-// (binary64, then rounded).  The kernel builds q as a float exactly (the bits
-// of 2^23 + q by one v_perm_b32, minus 2^23) and evaluates fma(q, A, B) in
-// binary32: error <= 2^-24 (65535 |A| + |B|) + the fma rounding.  The bound
-// e_k = 2^-22 (65536 |A| + |B|) is folded into the B used for the near and
-// for the far bound of axis k (pushed outward: down for the near side, up for
-// the far side), so the interval only ever grows; the fma rounding is covered
-// by the relative slack 2^-20 (|tn| + |tf|).  The origin enters in binary64.
-// A ray whose coefficients are not finite tests every box as hit (A = B = 0,
-// eps = inf): slower, exact.
+// (binary64, then rounded).  The kernel builds q as a float exactly and
+// evaluates fma(q, A, B) in binary32.  Against the exact slab distance the
+// error is at most 2^-24 * 65535 |A| (A rounded) + 2^-24 |B| (B rounded) +
+// 2^-24 |q A + B| (the fma's rounding) <= 2^-23 (65535 |A| + |B|) (1 + 2^-23),
+// plus binary64 errors of A and B near 2^-52.  The bound
+// e_k = 2^-22 (65536 |A| + |B|), twice that, is folded into the B used for
+// the near and for the far bound of axis k (pushed outward: down for the near
+// side, up for the far side), so every computed near distance is <= the exact
+// one and every far distance >= it; min/max and the final compare are exact,
+// so a box the exact interval meets is never rejected.  tmin / tmax enter
+// rounded outward (t_lo32 / t_hi32).  A ray whose coefficients are not finite
+// or too large tests every box as hit (A = 0, B = -1e30 / +1e30 per axis:
+// the interval becomes [tmin, tmax]): slower, exact.
 typedef float f2 __attribute__((ext_vector_type(2)));
 struct RayQ {
   f2 a, bx, by, bz;  // a = (A_x, A_y); b*: B biased for the lo and hi bound of the axis
-  float az, eps;
+  float az;
 };
 __device__ __forceinline__ void ray_q_axis(double q0, double qd, double o, double id, float& a, f2& b, bool& ok) {
   const double ik = fmin(fmax(id, -1e30), 1e30);
@@ -234,16 +238,18 @@ __device__ __forceinline__ RayQ ray_q(const WfParams& p, d3 o, d3 id) {
   ray_q_axis(p.q0[1], p.qd[1], o.y, id.y, ay, r.by, ok);
   ray_q_axis(p.q0[2], p.qd[2], o.z, id.z, r.az, r.bz, ok);
   r.a = f2{ax, ay};
-  r.eps = 0.f;
   if (!ok) {
     r.a = f2{0.f, 0.f};
     r.az = 0.f;
-    r.bx = r.by = r.bz = f2{0.f, 0.f};
-    r.eps = __builtin_inff();
+    r.bx = r.by = r.bz = f2{-1e30f, 1e30f};
   }
   return r;
 }
-// q (16-bit half of w) as an exact float: bits of 2^23 + q, minus 2^23
+// q (16-bit half of w) as an exact float (one v_cvt_f32_u32 with an SDWA word
+// select each)
+__device__ __forceinline__ float q_lo(uint32_t w) { return (float)(w & 0xFFFFu); }
+__device__ __forceinline__ float q_hi(uint32_t w) { return (float)(w >> 16); }
+// (alternative form: bits of 2^23 + q by one v_perm_b32, minus 2^23)
 __device__ __forceinline__ float q_bits_lo(uint32_t w) {
   return __builtin_bit_cast(float, __builtin_amdgcn_perm(0x4B000000u, w, 0x070c0100u));
 }
@@ -251,16 +257,15 @@ __device__ __forceinline__ float q_bits_hi(uint32_t w) {
   return __builtin_bit_cast(float, __builtin_amdgcn_perm(0x4B000000u, w, 0x070c0302u));
 }
 __device__ __forceinline__ bool box_q(const uint4 n, const RayQ& r, float tmin, float tmax, float& tn) {
-  const f2 k23 = f2{8388608.f, 8388608.f};
-  const f2 qx = f2{q_bits_lo(n.x), q_bits_hi(n.y)} - k23;  // (lo.x, hi.x)
-  const f2 qy = f2{q_bits_hi(n.x), q_bits_lo(n.z)} - k23;  // (lo.y, hi.y)
-  const f2 qz = f2{q_bits_lo(n.y), q_bits_hi(n.z)} - k23;  // (lo.z, hi.z)
+  const f2 qx = f2{q_lo(n.x), q_hi(n.y)};  // (lo.x, hi.x)
+  const f2 qy = f2{q_hi(n.x), q_lo(n.z)};  // (lo.y, hi.y)
+  const f2 qz = f2{q_lo(n.y), q_hi(n.z)};  // (lo.z, hi.z)
   const f2 tx = __builtin_elementwise_fma(qx, f2{r.a.x, r.a.x}, r.bx);
   const f2 ty = __builtin_elementwise_fma(qy, f2{r.a.y, r.a.y}, r.by);
   const f2 tz = __builtin_elementwise_fma(qz, f2{r.az, r.az}, r.bz);
   tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fmaxf(fminf(tz.x, tz.y), tmin));
   const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fminf(fmaxf(tz.x, tz.y), tmax));
-  return tn <= tf + (fabsf(tn) + fabsf(tf)) * 0x1p-20f + r.eps;
+  return tn <= tf;
 }
 
 // One step of the while-while traversal of a lane (the closest_hit / any_hit
