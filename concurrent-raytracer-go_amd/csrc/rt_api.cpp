@@ -321,9 +321,9 @@ struct rt_context {
   unsigned long long* dbg = nullptr;
   // tile dispatch order (schedule.cpp), cached per (scene, W, H, rank, world)
   uint64_t scene_gen = 0;
-  int64_t order_key[12] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+  int64_t order_key[13] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
   std::vector<int32_t> order_host;   // local tiles by projected-primitive count (fallback estimate)
-  std::vector<int32_t> blocks_host;  // work blocks, 4 ints each (schedule.cpp build_blocks)
+  std::vector<int32_t> blocks_host;  // work blocks, kBlockInts ints each (schedule.cpp build_blocks)
   int32_t* d_blocks = nullptr;
   size_t d_blocks_cap = 0;
   int32_t nsplit = 0;       // split pixels of the current schedule
@@ -532,8 +532,10 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st) {
   double block_work = f.bvh.empty() ? 512.0 : 8192.0;
   if (const char* e = getenv("RTGO_BLOCK_WORK")) block_work = std::max(1.0, atof(e));  // experiments only
   const bool pilot = !getenv("RTGO_NO_PILOT");
-  const int64_t key[12] = {(int64_t)c->scene_gen, w, h, rank, world, st->samples, st->max_depth,
-                           st->recursive_reflections, st->soft_shadows, bigP, (int64_t)(block_work * 16), pilot};
+  const bool frustum = !getenv("RTGO_NO_FRUSTUM");
+  const int64_t key[13] = {(int64_t)c->scene_gen, w, h, rank, world, st->samples, st->max_depth,
+                           st->recursive_reflections, st->soft_shadows, bigP, (int64_t)(block_work * 16), pilot,
+                           frustum};
   if (memcmp(key, c->order_key, sizeof key) != 0) {
     // primary-ray candidate masks per local tile
     if (f.bvh.empty() && f.spheres.size() <= 64 && f.tris.size() <= 64) {
@@ -551,6 +553,10 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st) {
       c->masks_host.clear();
     }
     const int local = rt_tiles_for_rank(w, h, rank, world);
+    // per-pixel primary masks (phase 1 traces only the samples of pixels
+    // whose own masks are not empty, against their block's union)
+    std::vector<unsigned long long> pix;
+    if (!c->masks_host.empty()) pixel_primary_masks(f, w, h, rank, world, c->masks_host, &pix);
     // fallback estimate: primitives projected onto the tile
     std::vector<float> tile_cost;
     tile_dispatch_order(f, w, h, rank, world, &c->order_host, &tile_cost);
@@ -576,7 +582,8 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st) {
       // one sample per pixel, blocks of 64 pixels, packed output into scratch
       std::vector<int32_t> pb;
       for (int lt = 0; lt < local; ++lt)
-        for (int p0 = 0; p0 < 1024; p0 += 64) pb.insert(pb.end(), {lt, p0, 64, 0, 1, -1, 1, 0});
+        for (int p0 = 0; p0 < 1024; p0 += 64) pb.insert(pb.end(), {lt, p0, 64, 0, 1, -1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0});
+      if (!c->masks_host.empty()) fill_block_masks(pix, &pb);
       int rc = upload_blocks(pb);
       if (rc) return rc;
       const size_t npx = (size_t)local * 1024;
@@ -592,7 +599,7 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st) {
       KParams q = *p;
       q.spp = 1;
       q.blocks = c->d_blocks;
-      q.num_blocks = (int32_t)(pb.size() / 8);
+      q.num_blocks = (int32_t)(pb.size() / kBlockInts);
       q.num_wgs = q.num_blocks;
       q.layout = RT_LAYOUT_PACKED_TILES;
       q.out_linear = plin;
@@ -627,7 +634,13 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st) {
         }
       }
     }
-    c->nsplit = build_blocks(work, st->samples, bigP, block_work, &c->blocks_host);
+    // tiles whose camera rays provably miss everything (both primary masks
+    // empty): black without tracing
+    std::vector<uint8_t> black;
+    if (frustum && !c->masks_host.empty())
+      for (int lt = 0; lt < local; ++lt) black.push_back((c->masks_host[2 * lt] | c->masks_host[2 * lt + 1]) == 0);
+    c->nsplit = build_blocks(work, st->samples, bigP, block_work, black, &c->blocks_host);
+    if (!c->masks_host.empty()) fill_block_masks(pix, &c->blocks_host);
     int rc = upload_blocks(c->blocks_host);
     if (rc) return rc;
     const size_t need = (size_t)c->nsplit * st->samples * 3 * sizeof(double) + split_flags_bytes(c->nsplit, st->samples);
@@ -640,7 +653,7 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st) {
     memcpy(c->order_key, key, sizeof key);
   }
   p->blocks = c->d_blocks;
-  p->num_blocks = (int32_t)(c->blocks_host.size() / 8);
+  p->num_blocks = (int32_t)(c->blocks_host.size() / kBlockInts);
   p->split_rad = c->nsplit ? (double*)c->d_split : nullptr;
   p->split_hits = c->nsplit ? (uint32_t*)((char*)c->d_split + (size_t)c->nsplit * st->samples * 3 * sizeof(double))
                             : nullptr;

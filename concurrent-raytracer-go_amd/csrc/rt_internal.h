@@ -42,13 +42,24 @@ void tile_dispatch_order(const FlatScene& fs, int32_t W, int32_t H, int32_t rank
 // estimated work per pixel-sample (pixel_work[lt * 1024 + p]), the heaviest
 // pixels split into sample ranges, most expensive first (schedule.cpp).
 // Returns the number of split pixels.
+// black_tiles[lt] != 0: every camera ray of local tile lt provably misses
+// (empty primary masks); its pixels go to kBlockBlack blocks.
+constexpr int32_t kBlockBlack = 1;  // block flag (8th int): black tile, nothing to trace
+constexpr int kBlockInts = 16;      // ints per work block record (KParams::blocks)
 int build_blocks(const std::vector<float>& pixel_work, int spp, int big_pixels, double block_work,
-                 std::vector<int32_t>* blocks);
+                 const std::vector<uint8_t>& black_tiles, std::vector<int32_t>* blocks);
 // Primary-ray candidate masks per local tile (2 x u64: spheres, triangles;
 // scenes with <= 64 of each): bit i set unless primitive i's bounding sphere
 // provably misses the cone of the tile's camera rays.
 void tile_primary_masks(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
                         std::vector<unsigned long long>* masks);
+// The same per pixel of every local tile (2 x u64 per pixel, lt * 1024 + p;
+// only candidates of the pixel's tile are tested; 0 outside the image).
+void pixel_primary_masks(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
+                         const std::vector<unsigned long long>& tile_masks, std::vector<unsigned long long>* pix);
+// Per block record: the union of its pixels' masks (ints 8..11) and the bits
+// of its pixels whose masks are not empty (ints 12..13).
+void fill_block_masks(const std::vector<unsigned long long>& pix, std::vector<int32_t>* blocks);
 
 // ---------------------------------------------------------------- kernels
 // PCG jump-ahead entries: cooperative soft shadows evaluate up to 64
@@ -77,8 +88,9 @@ struct KParams {
   uint8_t* out_rgba;
   unsigned long long* counts;  // 9 counters (rt_counts order) or null
   unsigned long long* dbg;     // per-WG timing records (RT_WG_TIMING builds only) or null
-  const int32_t* blocks;       // per block, 8 ints: {local tile, first pixel, pixel count, first sample,
-                               //   samples, split slot (-1: none), sub-blocks of the split pixel, 0}
+  const int32_t* blocks;       // per block, kBlockInts ints: {local tile, first pixel, pixel count, first sample,
+                               //   samples, split slot (-1: none), sub-blocks of the split pixel, flags,
+                               //   primary masks (spheres u64, tris u64), live pixels u64, 0, 0}
   double* split_rad;           // split pixels: [slot][spp][3] radiance of the hit samples
   uint32_t* split_hits;        // split pixels: [slot][(spp+31)/32] hit-sample bits (zeroed per launch)
   int32_t* split_cnt;          // split pixels: sub-blocks finished (zeroed per launch)

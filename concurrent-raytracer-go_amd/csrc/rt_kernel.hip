@@ -411,11 +411,19 @@ struct BlockLoc {
   int p0, np;            // first pixel (row-major in the tile), pixel count
   int s0, ns;            // samples [s0, s0+ns) of each pixel (all spp unless split)
   int slot, nsub;        // split pixel: its radiance slot row and number of sub-blocks (slot < 0: not split)
+  bool black;            // kBlockBlack: no camera ray of the tile can hit anything
+  unsigned long long ms, mt;  // primary masks: union over the block's pixels (fill_block_masks)
+  unsigned long long live;    // its pixels whose own primary masks are not empty
 };
 __device__ __forceinline__ BlockLoc block_loc(KArg k, int b) {
   BlockLoc r;
-  const int4 e = reinterpret_cast<const int4*>(k->blocks)[2 * b];
-  const int4 f = reinterpret_cast<const int4*>(k->blocks)[2 * b + 1];
+  const int4 e = reinterpret_cast<const int4*>(k->blocks)[4 * b];
+  const int4 f = reinterpret_cast<const int4*>(k->blocks)[4 * b + 1];
+  const int4 g = reinterpret_cast<const int4*>(k->blocks)[4 * b + 2];
+  const int4 l = reinterpret_cast<const int4*>(k->blocks)[4 * b + 3];
+  r.ms = (unsigned long long)(uint32_t)g.x | ((unsigned long long)(uint32_t)g.y << 32);
+  r.mt = (unsigned long long)(uint32_t)g.z | ((unsigned long long)(uint32_t)g.w << 32);
+  r.live = (unsigned long long)(uint32_t)l.x | ((unsigned long long)(uint32_t)l.y << 32);
   r.lt = e.x;
   r.p0 = e.y;
   r.np = e.z;
@@ -423,6 +431,7 @@ __device__ __forceinline__ BlockLoc block_loc(KArg k, int b) {
   r.ns = f.x;
   r.slot = f.y;
   r.nsub = f.z;
+  r.black = (f.w & kBlockBlack) != 0;
   r.tile = k->rank + r.lt * k->world;
   r.tx = r.tile % k->tiles_x;
   r.ty = r.tile / k->tiles_x;
@@ -518,6 +527,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
 #endif
   __shared__ double slot[kRound][3];                 // radiance of the round's entries
   __shared__ double psum[64][3];                     // per pixel: running sum over samples
+  __shared__ uint8_t lpix[64];                       // phase 1: the block's live pixels
   // dynamic LDS (dyn_lds): [staged scene prefix (kStage)][BVH stack (stack_depth x 64 ints)]
 
   const int lane = threadIdx.x;
@@ -525,7 +535,8 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   int* stack = reinterpret_cast<int*>(dyn_lds + pk.stack_off) + lane;
   const BlockLoc blk = block_loc(fresh(), blockIdx.x);
   if ((int)blockIdx.x < fresh()->prio_blocks) __builtin_amdgcn_s_setprio(3);
-  const int nwords = (blk.np * blk.ns + 31) >> 5;
+  // a black block (up to 64 pixels x spp samples) sets no hit bits
+  const int nwords = blk.black ? 0 : (blk.np * blk.ns + 31) >> 5;
   if (lane < nwords) hbits[lane] = 0;
   psum[lane][0] = 0;
   psum[lane][1] = 0;
@@ -564,14 +575,23 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     KArg k = fresh();
     const BlockLoc loc = block_loc(k, blockIdx.x);
     const int NB = loc.np * loc.ns, ns = loc.ns;
-    // primary-ray frustum culling (host-computed per tile, schedule.cpp):
-    // only primitives whose bounding sphere meets the cone of the tile's
-    // camera rays can be hit; every camera ray is still generated and tested
+    // primary-ray frustum culling (host-computed per pixel, schedule.cpp):
+    // only primitives whose bounding sphere meets the cone of a pixel's
+    // camera rays can be hit by them.  A pixel with no candidate is black
+    // (every sample misses, renderer.go:170-173, and adds +0): its samples
+    // are not traced.  The others are tested against the union of the
+    // block's pixel masks.  (The counting variant walks every sample, so the
+    // path counts stay the reference's.)
     Cand prim = all;
+    unsigned long long pxlive = loc.np >= 64 ? ~0ull : (1ull << loc.np) - 1ull;
     if (k->tile_masks) {
-      prim.s = k->tile_masks[2 * loc.lt];
-      prim.t = k->tile_masks[2 * loc.lt + 1];
+      prim = Cand{loc.ms, loc.mt};
+      pxlive = loc.live;
     }
+    // compact list of the live pixels (block-local indices)
+    if (lane < loc.np && ((pxlive >> lane) & 1ull)) lpix[__popcll(pxlive & below)] = (uint8_t)lane;
+    __syncthreads();
+    const int nlive = __popcll(pxlive);
     const CamK ck = cam_k(k);
     const int W = k->W, H = k->H;
     // traceRay's depth cut-off comes first: with max_depth <= 0 every sample is black
@@ -581,11 +601,19 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     // id / ns by a multiply-high with m = floor((2^32 - 1) / ns) + 1: exact
     // for id, ns < 2^16 (NB <= kMaxBlockSamples); ns == 1 has no 32-bit m
     const uint32_t mdiv = ns > 1 ? 0xFFFFFFFFu / (uint32_t)ns + 1u : 0u;
+    // A black block's tile has empty primary masks: every camera ray misses
+    // (renderer.go:170-173), every sample is +0, so nothing is traced.  The
+    // counting variant still walks its samples for the path counts (its
+    // queries have no candidates: no hit bit is ever set).
+    const int NL = kCount ? NB : (loc.black ? 0 : nlive * ns);
 #ifdef RT_VIS_UNROLL
 #pragma unroll RT_VIS_UNROLL
 #endif
-    for (int id = lane; id < NB; id += 64) {
-      const int p = ns > 1 ? (int)__umulhi((uint32_t)id, mdiv) : id, s = s0 + id - p * ns;
+    for (int j = lane; j < NL; j += 64) {
+      // j -> (pixel, sample): every sample of the block (kCount) or of its
+      // live pixels, in order
+      const int pj = ns > 1 ? (int)__umulhi((uint32_t)j, mdiv) : j, sl = j - pj * ns;
+      const int p = kCount ? pj : (int)lpix[pj], s = s0 + sl, id = p * ns + sl;
       const int tp = p0 + p;
       const int x = x0 + (tp & 31), y = y0 + (tp >> 5);
       if (tp >= 1024 || !live || x >= W || y >= H) continue;
