@@ -13,7 +13,15 @@ workload: configs[1]: sphere_reflections_light, 800x600, 100 spp, depth 50,
           materials), which is MORE work.  --with-as-committed also times
           the as-committed scene ("as_committed" in the output).
 step    : one render of the frame with the scene and output buffers resident
-          in HBM.  For N>1 a step also includes the RCCL gather of the packed
+          in HBM.  Frames are rendered with F frames in flight
+          (--frames-in-flight, default 2): step i runs on context/stream
+          i % F with its own output buffers, so a frame's low-occupancy tail
+          (its last few 50-bounce paths) overlaps the next
+          frame's start.  Every step still renders one whole frame; `value`
+          is whole-job throughput over the K steps.  The same K frames are
+          also timed one at a time (F = 1, the reference's synchronous
+          Render): "one_frame_in_flight" reports that rate and the frame
+          latency.  For N>1 a step also includes the RCCL gather of the packed
           tiles to rank 0 and the unpack kernel there.  Like the scene
           upload, the work schedule of a (scene, frame, settings) key is
           built by the first frame (one-sample pilot render + host block
@@ -77,13 +85,16 @@ def parse():
                     help="also time the as-committed (black) scene; off by default so the profiled command's "
                          "render_kernel launches are all of the headline workload")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--frames-in-flight", type=int, default=2,
+                    help="frames rendered concurrently (own context, stream and buffers each)")
     return ap.parse_args()
 
 
 class Frame:
     """Device buffers and one render step of this rank."""
 
-    def __init__(self, rtgo, torch, dist, ctx, w, h, st, rank, world, device):
+    def __init__(self, rtgo, torch, dist, ctx, w, h, st, rank, world, device, stream=None):
+        self.stream = stream
         self.rtgo, self.torch, self.dist = rtgo, torch, dist
         self.ctx, self.w, self.h, self.st = ctx, w, h, st
         self.rank, self.world = rank, world
@@ -129,27 +140,34 @@ class Frame:
                               self.rank, self.world, self.layout)
 
 
-def time_steps(frame, torch, dist, world, steps, warmup, stream_ptr):
+def time_steps(frames, torch, dist, world, steps, warmup):
     """W untimed steps, then K timed steps between barrier + synchronize on
-    both sides; returns (max-over-ranks seconds, per-launch kernel ms).
-    Kernel durations come from HIP events recorded on the render stream."""
-    for _ in range(warmup):
-        frame.render(stream_ptr)
-        frame.gather(stream_ptr)
+    both sides; step i renders frames[i % F] on its own stream (F frames in
+    flight); returns (max-over-ranks seconds, per-launch kernel ms).  Kernel
+    durations come from HIP events recorded on the stream each kernel is
+    launched on."""
+    F = len(frames)
+    for i in range(warmup):
+        fr = frames[i % F]
+        with torch.cuda.stream(fr.stream):
+            fr.render(fr.stream.cuda_stream)
+            fr.gather(fr.stream.cuda_stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     evs = []
     t0 = time.perf_counter()
-    for _ in range(steps):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()  # current stream = the render stream (set in main)
-        frame.render(stream_ptr)
-        e1.record()
-        evs.append((e0, e1))
-        frame.gather(stream_ptr)
+    for i in range(steps):
+        fr = frames[i % F]
+        with torch.cuda.stream(fr.stream):  # events and the gather's stream: this frame's
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fr.render(fr.stream.cuda_stream)
+            e1.record()
+            evs.append((e0, e1))
+            fr.gather(fr.stream.cuda_stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -168,7 +186,7 @@ def first_frame_ms(rtgo, torch, dist, args, W, H, st, rank, world, local, stream
     max over ranks."""
     ctx = rtgo.Context(local)
     ctx.set_scene(rtgo.Scene.load_from_file(args.scene))
-    frame = Frame(rtgo, torch, dist, ctx, W, H, st, rank, world, local)
+    frame = Frame(rtgo, torch, dist, ctx, W, H, st, rank, world, local, torch.cuda.current_stream())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -264,20 +282,31 @@ def main():
     torch.cuda.set_stream(bench_stream)
     stream_ptr = bench_stream.cuda_stream
 
-    ctx = rtgo.Context(local)
-    ctx.set_scene(rtgo.Scene.load_from_file(args.scene))
-    frame = Frame(rtgo, torch, dist, ctx, W, H, st, rank, world, local)
-    counts = frame.counts(stream_ptr)  # algorithmic work of this rank's launch (counting variant, untimed)
+    F = max(1, args.frames_in_flight)
+    scene = rtgo.Scene.load_from_file(args.scene)
+    frames = []
+    for j in range(F):  # F frames in flight: own context (schedule), stream and buffers each
+        ctx = rtgo.Context(local)
+        ctx.set_scene(scene)
+        fr = Frame(rtgo, torch, dist, ctx, W, H, st, rank, world, local,
+                   bench_stream if j == 0 else torch.cuda.Stream())
+        with torch.cuda.stream(fr.stream):  # set-up: builds this context's schedule (like the scene upload)
+            fr.render(fr.stream.cuda_stream)
+            fr.gather(fr.stream.cuda_stream)
+        frames.append(fr)
+    counts = frames[0].counts(stream_ptr)  # algorithmic work of this rank's launch (counting variant, untimed)
     torch.cuda.synchronize()
-    elapsed, kms = time_steps(frame, torch, dist, world, args.steps, args.warmup, stream_ptr)
+    elapsed, kms = time_steps(frames, torch, dist, world, args.steps, args.warmup)
+    # the same frames one at a time (the reference's synchronous Render)
+    elapsed1, kms1 = time_steps(frames[:1], torch, dist, world, args.steps, args.warmup) if F > 1 else (elapsed, kms)
     first_ms = first_frame_ms(rtgo, torch, dist, args, W, H, st, rank, world, local, stream_ptr)
 
     as_committed = None
     if args.with_as_committed:
         ctx2 = rtgo.Context(local)
         ctx2.set_scene(rtgo.Scene.load_from_file(args.as_committed))
-        frame2 = Frame(rtgo, torch, dist, ctx2, W, H, st, rank, world, local)
-        elapsed2, kms2 = time_steps(frame2, torch, dist, world, args.steps, args.warmup, stream_ptr)
+        frame2 = Frame(rtgo, torch, dist, ctx2, W, H, st, rank, world, local, bench_stream)
+        elapsed2, kms2 = time_steps([frame2], torch, dist, world, args.steps, args.warmup)
         as_committed = {
             "scene": "sphere_reflections_light.json as committed (renders black: objects behind the camera)",
             "value": round(W * H * args.spp * args.steps / elapsed2 / 1e6, 3),
@@ -312,6 +341,12 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             # a first frame also builds the schedule that steps reuse (pilot render + host blocks)
             "first_frame_ms": round(first_ms, 4),
+            "frames_in_flight": F,
+            "one_frame_in_flight": {
+                "value": round(rays * args.steps / elapsed1 / 1e6, 3),
+                "ms_per_step": round(elapsed1 / args.steps * 1e3, 4),
+                "kernel_ms": round(sum(kms1) / len(kms1), 4),
+            },
             "higher_is_better": True,
             "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,  # BASELINE.md has no published number on this hardware/config
@@ -322,6 +357,7 @@ def main():
                 "workload": workload + ", soft shadows, recursive reflections",
                 "width": W, "height": H, "spp": args.spp, "max_depth": args.depth,
                 "parallelism": "tiles t%%%d + RCCL gather" % world if world > 1 else "1 GPU",
+                "frames_in_flight": F,
             },
             "roofline": {
                 "bound": "valu",
@@ -335,7 +371,8 @@ def main():
                 "flops_per_launch": flops,
                 "note": "FP64 VALU-bound branchy path (binary64 like the Go reference; no matrix shape, no MFMA). "
                         "achieved = algorithmic FP64 ops of one launch (the kernel's own event counts x "
-                        "DESIGN.md per-event costs) / average launch time (HIP events on the render stream). "
+                        "DESIGN.md per-event costs) / average launch time (HIP events on the stream each launch runs on; "
+                        "with frames in flight a launch shares the GPU with its neighbours' tails). "
                         "traffic = HBM bytes per launch from rocprofv3 FETCH_SIZE+WRITE_SIZE passes.",
             },
             "roofline_hbm": {
