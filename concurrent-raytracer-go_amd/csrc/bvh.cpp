@@ -264,9 +264,9 @@ void build_sphere_bvh(FlatScene* fs) {
         qh[k] = (uint32_t)b;
       }
       DQNode& q = fs->qbvh[i];
-      q.w[0] = ql[0] | (ql[1] << 16);
-      q.w[1] = ql[2] | (qh[0] << 16);
-      q.w[2] = qh[1] | (qh[2] << 16);
+      q.w[0] = ql[0] | (qh[0] << 16);  // per axis (lo, hi): the kernel picks near / far per ray
+      q.w[1] = ql[1] | (qh[1] << 16);
+      q.w[2] = ql[2] | (qh[2] << 16);
       q.w[3] = (uint32_t)((nd.left_or_first << 3) | nd.count);
     }
   }

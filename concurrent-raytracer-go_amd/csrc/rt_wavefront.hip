@@ -214,57 +214,56 @@ __device__ __forceinline__ void finish(const WfParams& p, uint32_t sid, d3 L) {
 // rounded outward (t_lo32 / t_hi32).  A ray whose coefficients are not finite
 // or too large tests every box as hit (A = 0, B = -1e30 / +1e30 per axis:
 // the interval becomes [tmin, tmax]): slower, exact.
+// Node words (bvh.cpp): w[k] = lo_k | hi_k << 16 for axes k = 0..2, w[3] the
+// child code.  Per ray and axis the near bound is lo when the direction is
+// positive, else hi; a per-ray byte selector `s` picks it, so the near and
+// far grid indices of an axis come out of two v_perm_b32 as the float bits
+// of 2^23 + q (exact), one packed subtract of 2^23, and one packed fma gives
+// (t_near, t_far) with no per-box min/max.
 typedef float f2 __attribute__((ext_vector_type(2)));
 struct RayQ {
-  f2 a, bx, by, bz;  // a = (A_x, A_y); b*: B biased for the lo and hi bound of the axis
-  float az;
+  float ax, ay, az;  // A per axis
+  f2 bx, by, bz;     // (B - e, B + e): the near and the far bound's coefficient
+  uint32_t sx, sy, sz;  // v_perm selector of the near half (the far half: s ^ 0x0202)
 };
-__device__ __forceinline__ void ray_q_axis(double q0, double qd, double o, double id, float& a, f2& b, bool& ok) {
+constexpr uint32_t kSelLo = 0x070c0100u, kSelHi = 0x070c0302u;  // bytes {q, q, 0x00, 0x4B}
+__device__ __forceinline__ void ray_q_axis(double q0, double qd, double o, double id, float& a, f2& b, uint32_t& sel,
+                                           bool& ok) {
   const double ik = fmin(fmax(id, -1e30), 1e30);
   const double A = qd * ik, B = (q0 - o) * ik;
   const double e = (65536.0 * fabs(A) + fabs(B)) * 0x1p-22;
-  // lo bound: near side when inv > 0 (push down), far side otherwise (push up)
-  const double blo = ik > 0 ? B - e : B + e, bhi = ik > 0 ? B + e : B - e;
+  // the near side is pushed down, the far side up
+  const double bn = B - e, bf = B + e;
   a = (float)A;
-  b = f2{(float)blo, (float)bhi};
-  ok = ok && __builtin_isfinite(A) && __builtin_isfinite(blo) && __builtin_isfinite(bhi) && fabs(blo) < 1e30 &&
-       fabs(bhi) < 1e30 && fabs(A) < 1e30;
+  b = f2{(float)bn, (float)bf};
+  sel = ik > 0 ? kSelLo : kSelHi;  // t = q A + B grows with q when A > 0: near = lo
+  ok = ok && __builtin_isfinite(A) && __builtin_isfinite(bn) && __builtin_isfinite(bf) && fabs(bn) < 1e30 &&
+       fabs(bf) < 1e30 && fabs(A) < 1e30;
 }
 __device__ __forceinline__ RayQ ray_q(const WfParams& p, d3 o, d3 id) {
   RayQ r;
   bool ok = true;
-  float ax, ay;
-  ray_q_axis(p.q0[0], p.qd[0], o.x, id.x, ax, r.bx, ok);
-  ray_q_axis(p.q0[1], p.qd[1], o.y, id.y, ay, r.by, ok);
-  ray_q_axis(p.q0[2], p.qd[2], o.z, id.z, r.az, r.bz, ok);
-  r.a = f2{ax, ay};
+  ray_q_axis(p.q0[0], p.qd[0], o.x, id.x, r.ax, r.bx, r.sx, ok);
+  ray_q_axis(p.q0[1], p.qd[1], o.y, id.y, r.ay, r.by, r.sy, ok);
+  ray_q_axis(p.q0[2], p.qd[2], o.z, id.z, r.az, r.bz, r.sz, ok);
   if (!ok) {
-    r.a = f2{0.f, 0.f};
-    r.az = 0.f;
+    r.ax = r.ay = r.az = 0.f;
     r.bx = r.by = r.bz = f2{-1e30f, 1e30f};
   }
   return r;
 }
-// q (16-bit half of w) as an exact float (one v_cvt_f32_u32 with an SDWA word
-// select each)
-__device__ __forceinline__ float q_lo(uint32_t w) { return (float)(w & 0xFFFFu); }
-__device__ __forceinline__ float q_hi(uint32_t w) { return (float)(w >> 16); }
-// (alternative form: bits of 2^23 + q by one v_perm_b32, minus 2^23)
-__device__ __forceinline__ float q_bits_lo(uint32_t w) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_perm(0x4B000000u, w, 0x070c0100u));
-}
-__device__ __forceinline__ float q_bits_hi(uint32_t w) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_perm(0x4B000000u, w, 0x070c0302u));
+// (near, far) grid indices of one axis word as exact floats
+__device__ __forceinline__ f2 q_near_far(uint32_t w, uint32_t sel) {
+  const f2 bits = f2{__builtin_bit_cast(float, __builtin_amdgcn_perm(0x4B000000u, w, sel)),
+                     __builtin_bit_cast(float, __builtin_amdgcn_perm(0x4B000000u, w, sel ^ 0x0202u))};
+  return bits - f2{8388608.f, 8388608.f};
 }
 __device__ __forceinline__ bool box_q(const uint4 n, const RayQ& r, float tmin, float tmax, float& tn) {
-  const f2 qx = f2{q_lo(n.x), q_hi(n.y)};  // (lo.x, hi.x)
-  const f2 qy = f2{q_hi(n.x), q_lo(n.z)};  // (lo.y, hi.y)
-  const f2 qz = f2{q_lo(n.y), q_hi(n.z)};  // (lo.z, hi.z)
-  const f2 tx = __builtin_elementwise_fma(qx, f2{r.a.x, r.a.x}, r.bx);
-  const f2 ty = __builtin_elementwise_fma(qy, f2{r.a.y, r.a.y}, r.by);
-  const f2 tz = __builtin_elementwise_fma(qz, f2{r.az, r.az}, r.bz);
-  tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fmaxf(fminf(tz.x, tz.y), tmin));
-  const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fminf(fmaxf(tz.x, tz.y), tmax));
+  const f2 tx = __builtin_elementwise_fma(q_near_far(n.x, r.sx), f2{r.ax, r.ax}, r.bx);
+  const f2 ty = __builtin_elementwise_fma(q_near_far(n.y, r.sy), f2{r.ay, r.ay}, r.by);
+  const f2 tz = __builtin_elementwise_fma(q_near_far(n.z, r.sz), f2{r.az, r.az}, r.bz);
+  tn = fmaxf(fmaxf(tx.x, ty.x), fmaxf(tz.x, tmin));
+  const float tf = fminf(fminf(tx.y, ty.y), fminf(tz.y, tmax));
   return tn <= tf;
 }
 
