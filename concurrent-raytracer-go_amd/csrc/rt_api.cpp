@@ -753,6 +753,7 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   int trav_wgs = 1;
   if (const char* e = getenv("RTGO_WF_TRAV_BLOCK")) p.trav_block = std::max(1, std::min(16, atoi(e) / 64)) * 64;
   if (const char* e = getenv("RTGO_WF_TRAV_WGS")) trav_wgs = std::max(1, std::min(32, atoi(e)));
+  p.bvh_nodes = (int)f.qbvh.size();
   p.lds_nodes = wf_lds_nodes(p.stack_depth, (int)f.qbvh.size(), p.trav_block, trav_wgs);
   if (const char* e = getenv("RTGO_WF_LDS_NODES"))  // tests / experiments: stage fewer nodes
     p.lds_nodes = std::min(p.lds_nodes, std::max(0, atoi(e)) | 1);

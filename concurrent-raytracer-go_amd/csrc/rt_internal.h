@@ -166,6 +166,7 @@ struct WfParams {
   int32_t W, H, rank, world, tiles_x, ntiles, layout;
   int32_t stack_depth;       // BVH stack entries per lane (the tree's depth - 1)
   int32_t lds_nodes;         // leading quantized nodes (breadth-first: the top levels) staged in LDS
+  int32_t bvh_nodes;         // quantized nodes in all
   int32_t trav_block;        // threads per workgroup of the traversal kernels (<= kWfTravBlock)
   int32_t shard_cap;         // path slots per shard
   int64_t hard_cap, soft_cap;  // queue entries per shard

@@ -274,14 +274,15 @@ __device__ __forceinline__ bool box_q(const uint4 n, const RayQ& r, float tmin, 
 // child first, until `cur` is a leaf (count 1..4) or -1 (done).
 // Node pairs below `nlds` come from the LDS copy `lt` (stage_tree), the rest
 // from global memory.
-template <bool kCount>
+// kFull: the whole tree is staged (no global-memory branch).
+template <bool kCount, bool kFull>
 __device__ __forceinline__ void descend(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
                                         const RayQ& r, float tminf, float tmaxf, int& cur, int& sp, int* stack,
                                         Counters& c) {
   while ((cur & 7) == 0) {
     const int first = cur >> 3;
     uint4 L, R;
-    if (first < nlds) {  // nlds is odd or the whole tree: a staged pair is whole
+    if (kFull || first < nlds) {  // nlds is odd or the whole tree: a staged pair is whole
       L = as_uint4(lt[first]);
       R = as_uint4(lt[first + 1]);
     } else {
@@ -339,7 +340,7 @@ __device__ __forceinline__ bool job_refill(JobSrc& js, int32_t* heads, int n) {
 // tests, same exact-t tie rule).  Wave w owns jobs [n w / W, n (w+1) / W) and
 // refills idle lanes from them.  A hit leaves (sphere, root numerator) for
 // shade1; a miss ends the path with the radiance it has (renderer.go:170-173).
-template <bool kCount>
+template <bool kCount, bool kFull>
 __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
   const Dense dn = dense(p.ctl->cur_cnt);
   const int n = dn.start[kWfShards];
@@ -403,7 +404,7 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
       continue;
     }
     if (busy) {
-      descend<kCount>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, t_hi32(closest), cur, sp, stack, c);
+      descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, t_hi32(closest), cur, sp, stack, c);
       if (cur != -1) {  // a leaf: the exact Sphere.Hit tests, in hittable order
         const int first = cur >> 3, count = cur & 7;
         for (int i = first; i < first + count; ++i) {
@@ -501,7 +502,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade1(const WfParams p) {
 // queued point p (renderer.go:316-318) and a blocked ray adds 1 to its
 // (path, light) count; hard: the ray is lightDir and a blocked ray sets
 // kHardBit.
-template <bool kCount, bool kSoft>
+template <bool kCount, bool kSoft, bool kFull>
 __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
   const Dense dn = dense(kSoft ? p.ctl->soft_cnt : p.ctl->hard_cnt);
   const int n = dn.start[kWfShards];
@@ -568,7 +569,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
       continue;
     }
     if (busy) {
-      descend<kCount>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, tmaxf, cur, sp, stack, c);
+      descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, tmaxf, cur, sp, stack, c);
       bool blocked = false;
       if (cur != -1) {
         const int first = cur >> 3, count = cur & 7;
@@ -886,27 +887,43 @@ static int enqueue_regen_book(const WfParams& p, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-template <bool kCount>
-static int enqueue_bounce(const WfParams& p, hipStream_t st) {
-  const dim3 b(kWfBlock), bt(p.trav_block);
-  const dim3 gd((kWfShards * p.shard_cap + kWfBlock - 1) / kWfBlock);  // dense kernels: one thread per slot
+// the traversal kernels of one bounce: closest hit, hard and soft occlusion
+template <bool kCount, bool kFull>
+static void enqueue_trav(const WfParams& p, hipStream_t st, int which) {
+  const dim3 bt(p.trav_block);
   const size_t sh = trav_shmem(p);
   static int g_ext = 0, g_occ_h = 0, g_occ_s = 0, g_block = 0;
   static size_t g_sh = 0;
   if (g_sh != sh || g_block != p.trav_block || !g_ext) {
-    g_ext = resident_grid(wf_extend<kCount>, p.trav_block, sh);
-    g_occ_h = resident_grid(wf_occlude<kCount, false>, p.trav_block, sh);
-    g_occ_s = resident_grid(wf_occlude<kCount, true>, p.trav_block, sh);
+    g_ext = resident_grid(wf_extend<kCount, kFull>, p.trav_block, sh);
+    g_occ_h = resident_grid(wf_occlude<kCount, false, kFull>, p.trav_block, sh);
+    g_occ_s = resident_grid(wf_occlude<kCount, true, kFull>, p.trav_block, sh);
     g_sh = sh;
     g_block = p.trav_block;
   }
-  hipLaunchKernelGGL((wf_extend<kCount>), dim3(g_ext), bt, sh, st, p);
+  if (which == 0) hipLaunchKernelGGL((wf_extend<kCount, kFull>), dim3(g_ext), bt, sh, st, p);
+  if (which == 1) hipLaunchKernelGGL((wf_occlude<kCount, false, kFull>), dim3(g_occ_h), bt, sh, st, p);
+  if (which == 2) hipLaunchKernelGGL((wf_occlude<kCount, true, kFull>), dim3(g_occ_s), bt, sh, st, p);
+}
+
+template <bool kCount>
+static int enqueue_bounce(const WfParams& p, hipStream_t st) {
+  const dim3 b(kWfBlock);
+  const dim3 gd((kWfShards * p.shard_cap + kWfBlock - 1) / kWfBlock);  // dense kernels: one thread per slot
+  const bool full = p.lds_nodes >= p.bvh_nodes;
+  auto trav = [&](int which) {
+    if (full)
+      enqueue_trav<kCount, true>(p, st, which);
+    else
+      enqueue_trav<kCount, false>(p, st, which);
+  };
+  trav(0);
   hipLaunchKernelGGL((wf_shade1<kCount>), gd, b, 0, st, p);
   if (p.nl > 0) {
-    hipLaunchKernelGGL((wf_occlude<kCount, false>), dim3(g_occ_h), bt, sh, st, p);
+    trav(1);
     if (p.soft) {
       hipLaunchKernelGGL((wf_softgen<kCount>), gd, b, 0, st, p);
-      hipLaunchKernelGGL((wf_occlude<kCount, true>), dim3(g_occ_s), bt, sh, st, p);
+      trav(2);
     }
   }
   hipLaunchKernelGGL((wf_shade<kCount>), gd, b, 0, st, p);
