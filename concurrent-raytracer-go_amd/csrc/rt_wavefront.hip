@@ -201,25 +201,21 @@ __device__ __forceinline__ void finish(const WfParams& p, uint32_t sid, d3 L) {
 // Slab tests against the quantized BVH (DQNode: 16-bit grid indices, bounds
 // rounded outward, bvh.cpp).  For a grid index q on axis k the slab distance
 // is t = (q0 + q qd - o) inv = q A + B with A = qd inv, B = (q0 - o) inv
-// (binary64, then rounded).  The kernel builds q as a float exactly and
-// evaluates fma(q, A, B) in binary32.  Against the exact slab distance the
-// error is at most 2^-24 * 65535 |A| (A rounded) + 2^-24 |B| (B rounded) +
-// 2^-24 |q A + B| (the fma's rounding) <= 2^-23 (65535 |A| + |B|) (1 + 2^-23),
-// plus binary64 errors of A and B near 2^-52.  The bound
-// e_k = 2^-22 (65536 |A| + |B|), twice that, is folded into the B used for
+// (binary64).  The kernel evaluates it in binary32 (ray_q_axis: the error
+// bound e_k and its derivation); e_k is folded into the coefficient used for
 // the near and for the far bound of axis k (pushed outward: down for the near
-// side, up for the far side), so every computed near distance is <= the exact
-// one and every far distance >= it; min/max and the final compare are exact,
-// so a box the exact interval meets is never rejected.  tmin / tmax enter
-// rounded outward (t_lo32 / t_hi32).  A ray whose coefficients are not finite
-// or too large tests every box as hit (A = 0, B = -1e30 / +1e30 per axis:
-// the interval becomes [tmin, tmax]): slower, exact.
+// side, up for the far side), so every computed near distance is <= the
+// exact one and every far distance >= it; max/min/med3 and the final compare
+// are exact, so a box the exact interval meets is never rejected.  tmin /
+// tmax enter rounded outward (t_lo32 / t_hi32).  A ray whose coefficients are
+// not finite or too large tests every box as hit (A = 0, B = -1e30 / +1e30
+// per axis: the interval becomes [tmin, tmax]): slower, exact.
 // Node words (bvh.cpp): w[k] = lo_k | hi_k << 16 for axes k = 0..2, w[3] the
 // child code.  Per ray and axis the near bound is lo when the direction is
 // positive, else hi; a per-ray byte selector `s` picks it, so the near and
 // far grid indices of an axis come out of two v_perm_b32 as the float bits
-// of 2^23 + q (exact), one packed subtract of 2^23, and one packed fma gives
-// (t_near, t_far) with no per-box min/max.
+// of 2^23 + q (exact), and one packed fma (with the 2^23 folded into B,
+// below) gives (t_near, t_far) with no per-box min/max.
 typedef float f2 __attribute__((ext_vector_type(2)));
 struct RayQ {
   float ax, ay, az;  // A per axis
@@ -227,18 +223,27 @@ struct RayQ {
   uint32_t sx, sy, sz;  // v_perm selector of the near half (the far half: s ^ 0x0202)
 };
 constexpr uint32_t kSelLo = 0x070c0100u, kSelHi = 0x070c0302u;  // bytes {q, q, 0x00, 0x4B}
+// The kernel evaluates t = fma(Q, A, B') with Q = 2^23 + q (the float whose
+// bits v_perm_b32 builds, no subtraction) and B' = B - 2^23 A, so that
+// Q A + B' = q A + B.  Error against the exact t: |Q (fl(A) - A)| <= |A|
+// (Q < 2^24), fl(B') - B' <= 2^-24 (|B| + 2^23 |A|), and the fma's one
+// rounding 2^-24 |t| <= 2^-24 (65537 |A| + |B|): in all < 1.51 |A| +
+// 2^-23 |B|.  The bound e = 2 |A| + 2^-22 (65536 |A| + |B|) covers it (|A| is
+// one grid step of t: the test widens boxes by about two steps, 2 / 65000 of
+// the scene extent), and is folded outward into B' as before.
 __device__ __forceinline__ void ray_q_axis(double q0, double qd, double o, double id, float& a, f2& b, uint32_t& sel,
                                            bool& ok) {
   const double ik = fmin(fmax(id, -1e30), 1e30);
   const double A = qd * ik, B = (q0 - o) * ik;
-  const double e = (65536.0 * fabs(A) + fabs(B)) * 0x1p-22;
+  const double e = 2.0 * fabs(A) + (65536.0 * fabs(A) + fabs(B)) * 0x1p-22;
+  const double Bp = B - 8388608.0 * A;
   // the near side is pushed down, the far side up
-  const double bn = B - e, bf = B + e;
+  const double bn = Bp - e, bf = Bp + e;
   a = (float)A;
   b = f2{(float)bn, (float)bf};
   sel = ik > 0 ? kSelLo : kSelHi;  // t = q A + B grows with q when A > 0: near = lo
-  ok = ok && __builtin_isfinite(A) && __builtin_isfinite(bn) && __builtin_isfinite(bf) && fabs(bn) < 1e30 &&
-       fabs(bf) < 1e30 && fabs(A) < 1e30;
+  ok = ok && __builtin_isfinite(A) && __builtin_isfinite(bn) && __builtin_isfinite(bf) && fabs(bn) < 1e37 &&
+       fabs(bf) < 1e37 && fabs(A) < 1e30;
 }
 __device__ __forceinline__ RayQ ray_q(const WfParams& p, d3 o, d3 id) {
   RayQ r;
@@ -252,11 +257,10 @@ __device__ __forceinline__ RayQ ray_q(const WfParams& p, d3 o, d3 id) {
   }
   return r;
 }
-// (near, far) grid indices of one axis word as exact floats
+// (near, far) of one axis word as Q = 2^23 + q, exact floats
 __device__ __forceinline__ f2 q_near_far(uint32_t w, uint32_t sel) {
-  const f2 bits = f2{__builtin_bit_cast(float, __builtin_amdgcn_perm(0x4B000000u, w, sel)),
-                     __builtin_bit_cast(float, __builtin_amdgcn_perm(0x4B000000u, w, sel ^ 0x0202u))};
-  return bits - f2{8388608.f, 8388608.f};
+  return f2{__builtin_bit_cast(float, __builtin_amdgcn_perm(0x4B000000u, w, sel)),
+            __builtin_bit_cast(float, __builtin_amdgcn_perm(0x4B000000u, w, sel ^ 0x0202u))};
 }
 __device__ __forceinline__ bool box_q(const uint4 n, const RayQ& r, float tmin, float tmax, float& tn) {
   const f2 tx = __builtin_elementwise_fma(q_near_far(n.x, r.sx), f2{r.ax, r.ax}, r.bx);
