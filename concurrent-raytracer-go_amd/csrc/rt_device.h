@@ -140,14 +140,35 @@ __device__ __forceinline__ uint64_t state_at3(uint64_t x, const uint64_t* jump, 
 }
 
 // RandomVec3InUnitSphere, vector.go:132-139.
+// RandomVec3InUnitSphere (internal/math/vector.go:132-139) from three raw
+// draws: p = 2 RandomFloat() - 1 per axis, accepted when LengthSquared() < 1.
+// The point is exact in binary64 (u = x 2^-32 has 32 significant bits, so
+// 2u - 1 does not round); only the binary64 sum of squares rounds.
+__device__ __forceinline__ d3 unit_ball_point(uint32_t ux, uint32_t uy, uint32_t uz) {
+  return mk(rt_bits_to_unit(ux) * 2 - 1, rt_bits_to_unit(uy) * 2 - 1, rt_bits_to_unit(uz) * 2 - 1);
+}
+// The acceptance decision, screened in binary32: each coordinate is within
+// 2^-22 of the exact 2u - 1 (the draw rounded to 24 bits, one fma rounding),
+// so the float sum of squares is within 2^-19 of the exact one and the
+// binary64 sum within 2^-50.  Below 1 - 2^-16 the binary64 test accepts,
+// above 1 + 2^-16 it rejects; in between (a shell holding ~4e-5 of the
+// tries) the reference's binary64 arithmetic decides.  Same answer, a
+// fraction of the binary64 operations.
+__device__ __forceinline__ bool unit_ball_accept(uint32_t ux, uint32_t uy, uint32_t uz) {
+  const float fx = __builtin_fmaf((float)ux, 0x1p-31f, -1.f), fy = __builtin_fmaf((float)uy, 0x1p-31f, -1.f),
+              fz = __builtin_fmaf((float)uz, 0x1p-31f, -1.f);
+  const float l = __builtin_fmaf(fz, fz, __builtin_fmaf(fy, fy, fx * fx));
+  if (l < 1.f - 0x1p-16f) return true;
+  if (l > 1.f + 0x1p-16f) return false;
+  return len2(unit_ball_point(ux, uy, uz)) < 1;
+}
+
 template <bool kCount>
 __device__ __forceinline__ d3 rand_in_unit_sphere(rt_rng& r, Counters& c) {
   for (;;) {
-    double x = draw<kCount>(r, c);
-    double y = draw<kCount>(r, c);
-    double z = draw<kCount>(r, c);
-    d3 p = mk(x * 2 - 1, y * 2 - 1, z * 2 - 1);
-    if (len2(p) < 1) return p;
+    const uint32_t ux = rt_rng_next(&r), uy = rt_rng_next(&r), uz = rt_rng_next(&r);
+    cnt<kCount>(c, C_RNG, 3);
+    if (unit_ball_accept(ux, uy, uz)) return unit_ball_point(ux, uy, uz);
   }
 }
 

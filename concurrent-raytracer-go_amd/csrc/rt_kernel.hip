@@ -258,11 +258,10 @@ __device__ __forceinline__ int soft_seq(const Geo& p, bool masks, bool trace, d3
                                         Cand cm, rt_rng& rng, int* stack, Counters& c) {
   int need = 16, unocc = 0;
   while (need > 0) {
-    const double x = draw<kCount>(rng, c);
-    const double y = draw<kCount>(rng, c);
-    const double z = draw<kCount>(rng, c);
-    const d3 pt = mk(x * 2 - 1, y * 2 - 1, z * 2 - 1);
-    if (len2(pt) < 1) {
+    const uint32_t ux = rt_rng_next(&rng), uy = rt_rng_next(&rng), uz = rt_rng_next(&rng);
+    cnt<kCount>(c, C_RNG, 3);
+    if (unit_ball_accept(ux, uy, uz)) {
+      const d3 pt = unit_ball_point(ux, uy, uz);
       --need;
       cnt<kCount>(c, C_SHADOW);
       bool occ = false;
@@ -298,10 +297,8 @@ RT_COOP_FN CoopOut soft_coop(const Geo p, bool masks, bool trace, d3 P, d3 ldir,
   while (need > 0) {
     const uint64_t x0 = state_at3(x, jump, lane), x1 = x0 * RT_PCG_MULT + RT_PCG_INC,
                    x2 = x1 * RT_PCG_MULT + RT_PCG_INC;
-    const double dx = rt_bits_to_unit(rt_pcg_out(x0)), dy = rt_bits_to_unit(rt_pcg_out(x1)),
-                 dz = rt_bits_to_unit(rt_pcg_out(x2));
-    const d3 pt = mk(dx * 2 - 1, dy * 2 - 1, dz * 2 - 1);
-    const bool acc = len2(pt) < 1;
+    const uint32_t o0 = rt_pcg_out(x0), o1 = rt_pcg_out(x1), o2 = rt_pcg_out(x2);
+    const bool acc = unit_ball_accept(o0, o1, o2);
     const unsigned long long am = __ballot(acc);
     const int rank = __popcll(am & below);
     const bool chosen = acc && rank < need;
@@ -310,7 +307,9 @@ RT_COOP_FN CoopOut soft_coop(const Geo p, bool masks, bool trace, d3 P, d3 ldir,
     // tries consumed: up to and including the last chosen one
     const int used = nch == need ? 64 - __clzll(chm) : 64;
     bool occ = false;
-    if (chosen && trace) occ = shadow_blocked<kCount>(p, masks, P, normalize(ldir + muls(pt, 0.1)), ldist, cm, stack, c);
+    if (chosen && trace)
+      occ = shadow_blocked<kCount>(p, masks, P, normalize(ldir + muls(unit_ball_point(o0, o1, o2), 0.1)), ldist, cm,
+                                   stack, c);
     unocc += nch - __popcll(__ballot(chosen && occ));
     need -= nch;
     tries += used;
@@ -349,8 +348,7 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
       uy = rt_rng_next(&rng);
       uz = rt_rng_next(&rng);
       cnt<kCount>(c, C_RNG, 3);
-      const d3 pt = mk(rt_bits_to_unit(ux) * 2 - 1, rt_bits_to_unit(uy) * 2 - 1, rt_bits_to_unit(uz) * 2 - 1);
-      if (len2(pt) < 1) {
+      if (unit_ball_accept(ux, uy, uz)) {
         --need;
         cnt<kCount>(c, C_SHADOW);
         if (trace) acc = true;  // only rays that can be blocked are queued

@@ -630,17 +630,18 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
   if (own) {
     uint4* sq = reinterpret_cast<uint4*>(p.softq) + (size_t)shard * p.soft_cap + q;
     rt_rng rng{p.cur.rng[slot]};
+    int k = 0;  // entries written (an index, not a bumped pointer: hipcc of ROCm 7.2
+                // lost the pointer increment of points accepted on the rare
+                // binary64 branch of unit_ball_accept)
     for (uint32_t m = own; m; m &= m - 1) {
       const uint32_t key = (uint32_t)(slot * p.nl) + (uint32_t)__builtin_ctz(m);
       cnt<kCount>(c, C_SHADOW, 16);
-      for (int k = 0; k < 16;) {
+      for (const int end = k + 16; k < end;) {
         const uint32_t ux = rt_rng_next(&rng), uy = rt_rng_next(&rng), uz = rt_rng_next(&rng);
         cnt<kCount>(c, C_RNG, 3);
-        const d3 pt = mk(rt_bits_to_unit(ux) * 2 - 1, rt_bits_to_unit(uy) * 2 - 1, rt_bits_to_unit(uz) * 2 - 1);
-        if (len2(pt) < 1) {
-          *sq++ = make_uint4(key, ux, uy, uz);
-          ++k;
-        }
+        const bool acc = unit_ball_accept(ux, uy, uz);
+        if (acc) sq[k] = make_uint4(key, ux, uy, uz);
+        k += acc ? 1 : 0;
       }
     }
     p.cur.rng[slot] = rng.x;

@@ -118,3 +118,17 @@ def test_c4_full_frame_wavefront_equals_megakernel_and_two_ranks(monkeypatch):
     img_lin, img_rgba = _unpack(w, h, 2, parts)
     assert img_lin.cpu().numpy().tobytes() == a.tobytes()
     assert img_rgba.cpu().numpy().tobytes() == wf_rgba.cpu().numpy().tobytes()
+
+
+def test_wavefront_is_deterministic():
+    """Two renders of a 10k-sphere frame through the wavefront path are
+    byte-identical (paths are re-packed by atomics every bounce, so a race or
+    a lost queue entry shows up as run-to-run noise; a miscompiled pointer
+    increment in wf_softgen once did, rt_wavefront.hip)."""
+    scene = _spheres10k()
+    st = make_settings(rtgo, {"samples": 32}, seed=3)
+    w, h = 960, 540
+    a = _render(scene, w, h, st)
+    b = _render(scene, w, h, st)
+    assert a[0].cpu().numpy().tobytes() == b[0].cpu().numpy().tobytes()
+    assert a[1].cpu().numpy().tobytes() == b[1].cpu().numpy().tobytes()
