@@ -386,7 +386,7 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
           inv_a = approx_rcp(av);
           closest = __builtin_inf();
           best_obj = -1;
-          const d3 id = inv_dir(d);
+          const d3 id = inv_dir_fast(d);
           cnt<kCount>(c, C_BOX);
           if (box_hit(p.g.bvh[0], o, id, tmin, closest)) {
             r32 = ray_q(p, o, id);
@@ -556,7 +556,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
         }
         av = len2(d);
         inv_a = approx_rcp(av);
-        const d3 id = inv_dir(d);
+        const d3 id = inv_dir_fast(d);
         cnt<kCount>(c, C_BOX);
         if (box_hit(p.g.bvh[0], o, id, tmin, tmax)) {
           r32 = ray_q(p, o, id);
