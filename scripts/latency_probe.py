@@ -84,9 +84,12 @@ if os.environ.get("PROBE_SECTIONS"):  # with an RT_WG_TIMING build (RTGO_LIB): s
         ctx.close()
     sys.exit(0)
 
-for name, sc, soft in [("2 lights, soft", scene(), 1), ("2 lights, hard only", scene(), 0),
-                       ("1 light, soft", scene(lights=1), 1), ("shell only, 2 lights, soft", scene(False), 1),
-                       ("no lights", scene(lights=0), 1)]:
+CASES = [("2 lights, soft", scene(), 1), ("2 lights, hard only", scene(), 0),
+         ("1 light, soft", scene(lights=1), 1), ("shell only, 2 lights, soft", scene(False), 1),
+         ("no lights", scene(lights=0), 1)]
+if os.environ.get("PROBE_QUICK"):  # the first and the last case only
+    CASES = [CASES[0], CASES[-1]]
+for name, sc, soft in CASES:
     t1, t26, t51 = time_depth(sc, 1, soft), time_depth(sc, 26, soft), time_depth(sc, 51, soft)
     print(f"W={W} {name:28s} depth1 {t1:7.1f} us  depth51 {t51:7.1f} us  per bounce {(t51 - t1) / 50:6.2f} us"
           f"  (26: {(t26 - t1) / 25:6.2f})", flush=True)
