@@ -3,23 +3,29 @@
 // One launch renders every 32x32 tile (createRenderTasks,
 // internal/renderer/renderer.go:398-436) that this rank owns.  Design
 // (DESIGN.md §4):
-//   persistent waves take work BLOCKS (P pixels of a tile x all their spp
-//     samples) from an atomic queue, in the host's cost-sorted tile order;
-//   a wave alternates FILL (lanes without a path generate camera samples of
-//     the current block and run the primary closest-hit; misses end at once)
-//     and SHADE (every lane holding a path advances it one bounce of
-//     traceRay, renderer.go:165-227, unrolled), so the expensive shading
-//     runs with dense waves even when almost every camera ray misses;
+//   the host cuts this rank's tiles into work BLOCKS (pixels of one tile x
+//     a range of their samples, schedule.cpp), sized and ordered heaviest
+//     first from a one-sample pilot render; one one-wave workgroup renders
+//     one block;
+//   a block runs in three phases (render_kernel below): every camera sample
+//     of the block's live pixels gets its closest hit (misses end at once);
+//     the hit samples form a list that the wave drains through a ring of LDS
+//     radiance slots, a lane without a path taking the next entry, so
+//     traceRay (renderer.go:165-227, unrolled) runs on dense waves even when
+//     almost every camera ray misses; finished entries are summed per pixel
+//     in sample order (tracePixel, renderer.go:150-163), divided by spp,
+//     tone-mapped (toneMap, renderer.go:348-367) and written once (float3
+//     linear radiance + RGBA8);
 //   per bounce and light, the 16 jittered shadow rays (calculateSmartShadow,
-//     renderer.go:299-331) are produced in a wave-converged section: when
-//     only a few lanes of the wave need them, all 64 lanes evaluate one
-//     owner's rejection tries in parallel (PCG jump-ahead, include/rt_rng.h)
-//     and trace the accepted rays in parallel -- same draws, same rays, same
-//     result as the sequential loop;
-//   every sample's radiance lands in its own scratch slot; a finished block
-//     sums each pixel's samples in sample order (tracePixel,
-//     renderer.go:150-163), divides by spp, tone-maps (toneMap,
-//     renderer.go:348-367) and writes float3 linear radiance + RGBA8 once.
+//     renderer.go:299-331) are produced in a wave-converged section: rays of
+//     many owner lanes go through an LDS queue and are traced on full waves
+//     (soft_queue); when only a few lanes need them, all 64 lanes evaluate
+//     one owner's rejection tries in parallel (PCG jump-ahead,
+//     include/rt_rng.h, soft_coop) -- same draws, same rays, same result as
+//     the sequential loop; when few lanes still run paths, the idle lanes
+//     split the closest-hit and cone scans of the others (wide mode).
+// Large sphere scenes (a BVH) take the wavefront path instead
+// (rt_wavefront.hip) unless RTGO_MEGAKERNEL is set.
 // Small linear-scan scenes are staged into LDS by every workgroup; large
 // sphere scenes use a BVH (bvh.cpp) with per-lane LDS stacks.  Primitives
 // that provably cannot be hit (tile frustum / shadow cone tests with wide
