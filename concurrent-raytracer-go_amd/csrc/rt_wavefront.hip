@@ -309,6 +309,22 @@ __device__ __forceinline__ void descend(glb_node* __restrict__ qb, lds_node* __r
   }
 }
 
+// The spheres of a leaf: the loads of the first kLeafBatch are issued
+// together, before any test, so a leaf costs one memory round trip instead of
+// one per sphere (the tests stop early in occlusion, which kept the compiler
+// from hoisting the loads).  Indices past the leaf reload its last sphere.
+#ifndef RT_LEAF_BATCH
+#define RT_LEAF_BATCH 4
+#endif
+constexpr int kLeafBatch = RT_LEAF_BATCH;
+__device__ __forceinline__ void load_leaf(const DSphere* __restrict__ sp, int first, int count, DSphere* out) {
+#pragma unroll
+  for (int k = 0; k < kLeafBatch; ++k) out[k] = sp[first + min(k, count - 1)];
+}
+__device__ __forceinline__ const DSphere& leaf_sphere(const DSphere* sp, const DSphere* ls, int first, int i) {
+  return i - first < kLeafBatch ? ls[i - first] : sp[i];
+}
+
 // Dynamic job distribution of the persistent traversal kernels.  The dense
 // job space [0, n) is cut into kWfShards ranges, each with a head counter
 // (heads[32 s], reset by wf_book); a wave takes chunks of kChunk jobs from
@@ -411,9 +427,11 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
       descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, t_hi32(closest), cur, sp, stack, c);
       if (cur != -1) {  // a leaf: the exact Sphere.Hit tests, in hittable order
         const int first = cur >> 3, count = cur & 7;
+        DSphere ls[kLeafBatch];
+        load_leaf(p.g.spheres, first, count, ls);
         for (int i = first; i < first + count; ++i) {
           cnt<kCount>(c, C_SPH);
-          const DSphere& S = p.g.spheres[i];
+          const DSphere& S = leaf_sphere(p.g.spheres, ls, first, i);
           double num;
           if (sphere_query(S, o, d, av, inv_a, tmin, closest, num)) {
             const double t = num / av;
@@ -577,10 +595,12 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
       bool blocked = false;
       if (cur != -1) {
         const int first = cur >> 3, count = cur & 7;
+        DSphere ls[kLeafBatch];
+        load_leaf(p.g.spheres, first, count, ls);
         for (int i = first; i < first + count && !blocked; ++i) {
           cnt<kCount>(c, C_SPH);
           double num;
-          blocked = sphere_query(p.g.spheres[i], o, d, av, inv_a, tmin, tmax, num) != 0;
+          blocked = sphere_query(leaf_sphere(p.g.spheres, ls, first, i), o, d, av, inv_a, tmin, tmax, num) != 0;
         }
         cur = sp == 0 ? -1 : stack[--sp * 64];
       }
