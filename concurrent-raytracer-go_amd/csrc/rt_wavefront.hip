@@ -279,20 +279,24 @@ __device__ __forceinline__ bool box_q(const uint4 n, const RayQ& r, float tmin, 
 // Node pairs below `nlds` come from the LDS copy `lt` (stage_tree), the rest
 // from global memory.
 // kFull: the whole tree is staged (no global-memory branch).
+template <bool kFull>
+__device__ __forceinline__ void load_pair(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds, int first,
+                                          uint4& L, uint4& R) {
+  if (kFull || first < nlds) {  // nlds is odd or the whole tree: a staged pair is whole
+    L = as_uint4(lt[first]);
+    R = as_uint4(lt[first + 1]);
+  } else {
+    L = as_uint4(qb[first]);
+    R = as_uint4(qb[first + 1]);
+  }
+}
 template <bool kCount, bool kFull>
 __device__ __forceinline__ void descend(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
                                         const RayQ& r, float tminf, float tmaxf, int& cur, int& sp, int* stack,
                                         Counters& c) {
   while ((cur & 7) == 0) {
-    const int first = cur >> 3;
     uint4 L, R;
-    if (kFull || first < nlds) {  // nlds is odd or the whole tree: a staged pair is whole
-      L = as_uint4(lt[first]);
-      R = as_uint4(lt[first + 1]);
-    } else {
-      L = as_uint4(qb[first]);
-      R = as_uint4(qb[first + 1]);
-    }
+    load_pair<kFull>(qb, lt, nlds, cur >> 3, L, R);
     cnt<kCount>(c, C_BOX, 2);
     float tl, tr;
     const bool hl = box_q(L, r, tminf, tmaxf, tl), hr = box_q(R, r, tminf, tmaxf, tr);
