@@ -70,7 +70,7 @@ PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)  # 100 frames: 40 ms; fewer steps weigh the un-overlapped first start and last tail (20: -6 %)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "sphere_reflections_light_facing.json"))
     ap.add_argument("--as-committed", default=os.path.join(ROOT, "scenes", "sphere_reflections_light.json"))
