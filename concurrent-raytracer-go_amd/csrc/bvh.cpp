@@ -73,10 +73,10 @@ constexpr int kDefaultLeaf = 4;   // spheres per leaf at most (C4: 872 ms at 2, 
 
 }  // namespace
 
-void build_sphere_bvh(FlatScene* fs) {
-  int kBins = kDefaultBins, kLeafMax = kDefaultLeaf;  // experiments: RTGO_BVH_BINS, RTGO_BVH_LEAF (<= 7: 3-bit count)
-  if (const char* e = getenv("RTGO_BVH_BINS")) kBins = std::max(2, std::min(kMaxBins, atoi(e)));
-  if (const char* e = getenv("RTGO_BVH_LEAF")) kLeafMax = std::max(1, std::min(7, atoi(e)));
+void build_sphere_bvh(FlatScene* fs, int bins, int leaf) {
+  // rt_tuning: bins, leaf (<= 7: a 3-bit count); 0 = the defaults
+  const int kBins = bins > 0 ? std::max(2, std::min(kMaxBins, bins)) : kDefaultBins;
+  const int kLeafMax = leaf > 0 ? std::min(7, leaf) : kDefaultLeaf;
   fs->bvh.clear();
   fs->qbvh.clear();
   const int n = (int)fs->spheres.size();

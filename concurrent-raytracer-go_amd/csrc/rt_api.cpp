@@ -246,9 +246,9 @@ void flatten_scene(const rt_scene& s, FlatScene* fs) {
 // Pixels per work block.  Tiles without geometry: up to
 // kMaxBlockSamples sample ids (the block's hit list lives in LDS), at most
 // 64 pixels; tiles with work get smaller blocks (prepare_schedule).
-static int big_block_pixels(int spp) {
+static int big_block_pixels(int spp, const rt_tuning& tn) {
   int cap = kMaxBlockSamples;
-  if (const char* e = getenv("RTGO_BLOCK_SAMPLES")) cap = std::max(1, std::min(cap, atoi(e)));  // experiments only
+  if (tn.block_samples > 0) cap = std::min(cap, tn.block_samples);
   if (spp <= 0) return 64;
   return std::max(1, std::min(64, cap / spp));
 }
@@ -301,6 +301,7 @@ using namespace rtgo;
 // ======================================================================== ABI
 struct rt_context {
   int device = 0;
+  rt_tuning tun;  // work partition (rt_context_set_tuning); never changes the image
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool have_scene = false;
@@ -347,6 +348,35 @@ struct rt_context {
 
 extern "C" {
 
+void rt_tuning_default(rt_tuning* t) {
+  if (!t) return;
+  memset(t, 0, sizeof *t);
+  t->path = RT_PATH_AUTO;
+  t->pilot = 1;
+  t->frustum = 1;
+  t->stage = 1;
+  t->wf_lds_nodes = -1;
+}
+
+int rt_context_set_tuning(rt_context* c, const rt_tuning* t) {
+  if (!c || !t) {
+    set_error("context or tuning is NULL");
+    return RT_E_INVALID;
+  }
+  if (t->path != RT_PATH_AUTO && t->path != RT_PATH_MEGAKERNEL) {
+    set_error("tuning.path must be RT_PATH_AUTO or RT_PATH_MEGAKERNEL");
+    return RT_E_INVALID;
+  }
+  if (t->bvh_leaf < 0 || t->bvh_leaf > 7 || t->bvh_bins < 0 || t->block_work < 0 || t->block_samples < 0 ||
+      t->wf_paths < 0 || t->wf_chunk < 0 || t->wf_trav_block < 0 || t->wf_trav_block > 1024 || t->wf_trav_wgs < 0) {
+    set_error("tuning value out of range");
+    return RT_E_INVALID;
+  }
+  c->tun = *t;
+  c->order_key[0] = -1;  // rebuild the schedule
+  return RT_OK;
+}
+
 void rt_settings_default(rt_settings* s) {
   if (!s) return;
   memset(s, 0, sizeof *s);
@@ -358,10 +388,17 @@ void rt_settings_default(rt_settings* s) {
   s->soft_shadows = 1;
   s->depth_of_field = 0;
   s->num_workers = 1;
+  s->num_devices = 1;
   s->seed = 1;
 }
 
 int32_t rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_validate(const rt_scene* scene, int32_t w, int32_t h, const rt_settings* st) {
+  int rc = validate_scene(scene);
+  if (rc) return rc;
+  return validate_settings(st, w, h);
+}
 
 const char* rt_last_error(void) { return g_last_error.c_str(); }
 
@@ -391,6 +428,7 @@ int rt_context_create(int32_t device, rt_context** out) {
   HIP_TRY(hipSetDevice(device));
   rt_context* c = new rt_context();
   c->device = device;
+  rt_tuning_default(&c->tun);
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
@@ -428,6 +466,14 @@ void rt_context_destroy(rt_context* c) {
   delete c;
 }
 
+// Wait until the last render enqueued on this context has finished: before
+// the host overwrites buffers it reads (scene, schedule, wavefront state).
+static int quiesce(rt_context* c) {
+  if (c->have_timing) HIP_TRY(hipEventSynchronize(c->ev1));
+  if (c->stream) HIP_TRY(hipStreamSynchronize(c->stream));
+  return RT_OK;
+}
+
 int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   if (!c) {
     set_error("context is NULL");
@@ -444,7 +490,7 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
       return RT_E_INVALID;
     }
   } else if (want_bvh) {
-    build_sphere_bvh(&c->flat);
+    build_sphere_bvh(&c->flat, c->tun.bvh_bins, c->tun.bvh_leaf);
   }
   const FlatScene& f = c->flat;
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -457,7 +503,8 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   size_t off_b = off_j + al(kJump * 2 * sizeof(uint64_t));
   size_t off_q = off_b + al(f.bvh.size() * sizeof(DBVHNode));
   size_t total = off_q + al(f.qbvh.size() * sizeof(DQNode)) + 256;
-  if (c->stream) HIP_TRY(hipStreamSynchronize(c->stream));
+  rc = quiesce(c);  // the last render may still read the scene
+  if (rc) return rc;
   if (c->d_scene && c->d_scene_bytes < total) {
     HIP_TRY(hipFree(c->d_scene));
     c->d_scene = nullptr;
@@ -499,9 +546,8 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   // small linear-scan scenes are staged into LDS by every workgroup
   // (the 1 KB PCG jump table stays in global memory, L1-cached: only the
   // cooperative soft-shadow form reads it, and scenes near the LDS limit of 12
-  // workgroups per CU ran faster without it; RTGO_STAGE_JUMP: experiments only)
-  const size_t stage_end = getenv("RTGO_STAGE_JUMP") ? off_b : off_j;
-  c->stage_bytes = (f.bvh.empty() && stage_end <= 48 * 1024) ? (int32_t)stage_end : 0;
+  // workgroups per CU ran faster without it)
+  c->stage_bytes = (f.bvh.empty() && off_j <= 48 * 1024) ? (int32_t)off_j : 0;
   c->have_scene = true;
   c->scene_gen += 1;
   return RT_OK;
@@ -525,18 +571,21 @@ static size_t split_flags_bytes(int nsplit, int spp) {
 static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st) {
   const FlatScene& f = c->flat;
   const int w = p->W, h = p->H, rank = p->rank, world = p->world;
-  int bigP = big_block_pixels(st->samples);
+  const rt_tuning& tn = c->tun;
+  int bigP = big_block_pixels(st->samples, tn);
   // path bounces per block: 8 full-wave bounce steps; 16x that with a BVH,
   // whose bounces are long divergent traversals that need full waves more
   // than short blocks (C4: 2.10 s at 512, 1.77 s at 8192)
   double block_work = f.bvh.empty() ? 512.0 : 8192.0;
-  if (const char* e = getenv("RTGO_BLOCK_WORK")) block_work = std::max(1.0, atof(e));  // experiments only
-  const bool pilot = !getenv("RTGO_NO_PILOT");
-  const bool frustum = !getenv("RTGO_NO_FRUSTUM");
+  if (tn.block_work > 0) block_work = std::max(1.0, tn.block_work);
+  const bool pilot = tn.pilot != 0;
+  const bool frustum = tn.frustum != 0;
   const int64_t key[13] = {(int64_t)c->scene_gen, w, h, rank, world, st->samples, st->max_depth,
                            st->recursive_reflections, st->soft_shadows, bigP, (int64_t)(block_work * 16), pilot,
                            frustum};
   if (memcmp(key, c->order_key, sizeof key) != 0) {
+    int rc0 = quiesce(c);  // the last render may still read the blocks, masks and split rows
+    if (rc0) return rc0;
     // primary-ray candidate masks per local tile
     if (f.bvh.empty() && f.spheres.size() <= 64 && f.tris.size() <= 64) {
       tile_primary_masks(f, w, h, rank, world, &c->masks_host);
@@ -658,7 +707,7 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st) {
   p->split_hits = c->nsplit ? (uint32_t*)((char*)c->d_split + (size_t)c->nsplit * st->samples * 3 * sizeof(double))
                             : nullptr;
   p->split_cnt = c->nsplit ? (int32_t*)(p->split_hits + (size_t)c->nsplit * ((st->samples + 31) / 32)) : nullptr;
-  p->tile_masks = (c->masks_host.empty() || getenv("RTGO_NO_FRUSTUM")) ? nullptr : c->d_masks;
+  p->tile_masks = (c->masks_host.empty() || !frustum) ? nullptr : c->d_masks;
   return RT_OK;
 }
 
@@ -670,14 +719,13 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st) {
 constexpr int kWfRing = 4;
 constexpr uint64_t kWfMaxChunkSamples = 1ull << 28;  // 6 GB of radiance (HBM: 288 GB)
 
-static bool use_wavefront(const FlatScene& f) { return !f.bvh.empty() && !getenv("RTGO_MEGAKERNEL"); }
+static bool use_wavefront(const rt_context* c) { return !c->flat.bvh.empty() && c->tun.path != RT_PATH_MEGAKERNEL; }
 
 // path slots per shard (a multiple of kWfBlockSlots: every shard receives the
-// survivors of the workgroups b % kWfShards == shard, at most shard_cap);
-// RTGO_WF_PATHS: tests and experiments only
-static int wf_shard_cap(int nl) {
+// survivors of the workgroups b % kWfShards == shard, at most shard_cap)
+static int wf_shard_cap(int nl, const rt_tuning& tn) {
   long long cap = 1 << 21;
-  if (const char* e = getenv("RTGO_WF_PATHS")) cap = std::max(1ll, std::min(1ll << 24, atoll(e)));
+  if (tn.wf_paths > 0) cap = std::min(1ll << 24, (long long)tn.wf_paths);
   // soft queues: cap * nl * 16 entries of 16 B, at most 2 GB; keys slot * nl + light fit 32 bits
   cap = std::min<long long>(cap, (1ll << 27) / (16ll * std::max(nl, 1)));
   const long long per = kWfShards * kWfBlockSlots;
@@ -687,7 +735,7 @@ static int wf_shard_cap(int nl) {
 static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings* st, hipStream_t s, bool count) {
   const FlatScene& f = c->flat;
   const int nl = (int)f.lights.size();
-  const int shard_cap = wf_shard_cap(nl);
+  const int shard_cap = wf_shard_cap(nl, c->tun);
   const size_t cap = (size_t)shard_cap * kWfShards;
   const size_t nlk = (size_t)std::max(nl, 1);
   const size_t qcap = cap * nlk;  // hard rays per shard: at most every light of every path of its workgroups
@@ -699,6 +747,8 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
                       + (size_t)kWfShards * qcap * 16 * 16  // soft queues
                       + 64 * 256;                       // alignment
   if (need > c->wf_mem_bytes) {
+    int rq = quiesce(c);
+    if (rq) return rq;
     if (c->wf_mem) HIP_TRY(hipFree(c->wf_mem));
     c->wf_mem = nullptr;
     c->wf_mem_bytes = 0;
@@ -714,10 +764,12 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   const uint64_t local_px = (uint64_t)local * 1024;
   const uint64_t spp = (uint64_t)std::max(st->samples, 1);
   uint64_t max_chunk = kWfMaxChunkSamples;
-  if (const char* e = getenv("RTGO_WF_CHUNK")) max_chunk = std::max(1ll, std::min(atoll(e), (long long)max_chunk));  // tests
+  if (c->tun.wf_chunk > 0) max_chunk = std::min<uint64_t>((uint64_t)c->tun.wf_chunk, max_chunk);
   const uint64_t chunk_px = std::max<uint64_t>(1, std::min<uint64_t>(local_px, max_chunk / spp));
   const size_t rad_need = (size_t)(chunk_px * spp * 3 * sizeof(double));
   if (rad_need > c->wf_rad_bytes) {
+    int rq = quiesce(c);
+    if (rq) return rq;
     if (c->wf_rad) HIP_TRY(hipFree(c->wf_rad));
     c->wf_rad = nullptr;
     c->wf_rad_bytes = 0;
@@ -747,16 +799,17 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   // a lane holds at most one pending child per internal node above its leaf:
   // depth - 1 entries (leaves at level bvh_depth, the root at level 1)
   p.stack_depth = std::max(1, f.bvh_depth - 1);
-  // traversal workgroups: RTGO_WF_TRAV_BLOCK threads (64..1024), LDS shared by
-  // RTGO_WF_TRAV_WGS of them per CU (experiments; default one of 1024)
+  // traversal workgroups: trav_block threads (64..1024), LDS shared by
+  // trav_wgs of them per CU (tuning; default one of 1024)
+  const rt_tuning& tn = c->tun;
   p.trav_block = kWfTravBlock;
   int trav_wgs = 1;
-  if (const char* e = getenv("RTGO_WF_TRAV_BLOCK")) p.trav_block = std::max(1, std::min(16, atoi(e) / 64)) * 64;
-  if (const char* e = getenv("RTGO_WF_TRAV_WGS")) trav_wgs = std::max(1, std::min(32, atoi(e)));
+  if (tn.wf_trav_block > 0) p.trav_block = std::max(1, std::min(16, tn.wf_trav_block / 64)) * 64;
+  if (tn.wf_trav_wgs > 0) trav_wgs = std::min(32, tn.wf_trav_wgs);
   p.bvh_nodes = (int)f.qbvh.size();
   p.lds_nodes = wf_lds_nodes(p.stack_depth, (int)f.qbvh.size(), p.trav_block, trav_wgs);
-  if (const char* e = getenv("RTGO_WF_LDS_NODES"))  // tests / experiments: stage fewer nodes
-    p.lds_nodes = std::min(p.lds_nodes, std::max(0, atoi(e)) | 1);
+  if (tn.wf_lds_nodes >= 0)  // stage fewer nodes (an odd count: child pairs never split)
+    p.lds_nodes = std::min(p.lds_nodes, tn.wf_lds_nodes | 1);
   p.shard_cap = shard_cap;
   p.hard_cap = (int64_t)qcap;
   p.soft_cap = (int64_t)qcap * 16;
@@ -894,21 +947,21 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   p.layout = layout;
   {  // LDS staging of the scene prefix + BVH stack placement
     p.stage_src = c->d_scene;
-    p.stage_bytes = getenv("RTGO_NO_STAGE") ? 0 : c->stage_bytes;
+    p.stage_bytes = c->tun.stage ? c->stage_bytes : 0;
     p.stack_off = (p.stage_bytes + 15) & ~15;
     p.stack_depth = std::max(1, f.bvh_depth);
   }
-  const bool wf = use_wavefront(f);
+  const bool wf = use_wavefront(c);
   if (!wf) {
     rc = prepare_schedule(c, &p, st);
     if (rc) return rc;
   }
   p.num_wgs = p.num_blocks;
-  if (const char* e = getenv("RTGO_PRIO")) p.prio_blocks = atoi(e);  // experiments only
-  if (const char* e = getenv("RTGO_MAX_BLOCKS"))  // experiments only: the first N blocks (partial image)
-    p.num_wgs = p.num_blocks = std::min(p.num_blocks, std::max(0, atoi(e)));
-  // the caller's stream, as given (NULL = the legacy default stream)
+  // the caller's stream, as given (NULL = the legacy default stream); a
+  // render enqueued on another stream than this context's last one waits for
+  // that one first (they share the split rows and the wavefront state)
   hipStream_t s = (hipStream_t)stream;
+  if (c->have_timing && s != c->last_stream) HIP_TRY(hipStreamWaitEvent(s, c->ev1, 0));
   if (counts) HIP_TRY(hipMemsetAsync(c->d_counts, 0, 16 * sizeof(unsigned long long), s));
   if (!wf && c->nsplit)  // split pixels: hit bits and sub-block counters start at zero
     HIP_TRY(hipMemsetAsync(p.split_hits, 0, split_flags_bytes(c->nsplit, st->samples), s));
@@ -962,66 +1015,6 @@ int rt_context_last_kernel_seconds(rt_context* c, double* seconds) {
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   *seconds = ms * 1e-3;
-  return RT_OK;
-}
-
-int rt_unpack_tiles_async(int32_t w, int32_t h, int32_t world, int32_t max_local, const float* pl,
-                          const uint8_t* pr, float* ol, uint8_t* orgba, void* stream) {
-  if (w <= 0 || h <= 0 || world < 1 || max_local < 0) {
-    set_error("invalid unpack arguments");
-    return RT_E_INVALID;
-  }
-  int e = launch_unpack(w, h, world, max_local, pl, pr, ol, orgba, stream);
-  if (e != hipSuccess) {
-    set_error(std::string("unpack launch failed: ") + hipGetErrorString((hipError_t)e));
-    return RT_E_DEVICE;
-  }
-  return RT_OK;
-}
-
-int rt_render(const rt_scene* scene, int32_t w, int32_t h, const rt_settings* st, float* out_linear,
-              uint8_t* out_rgba, rt_stats* stats) {
-  int rc = validate_scene(scene);
-  if (rc) return rc;
-  rc = validate_settings(st, w, h);
-  if (rc) return rc;
-  auto t0 = std::chrono::steady_clock::now();
-  rt_context* c = nullptr;
-  rc = rt_context_create(0, &c);
-  if (rc) return rc;
-  struct Guard {
-    rt_context* c;
-    float* dl = nullptr;
-    uint8_t* dr = nullptr;
-    ~Guard() {
-      if (dl) (void)hipFree(dl);
-      if (dr) (void)hipFree(dr);
-      rt_context_destroy(c);
-    }
-  } g{c};
-  rc = rt_context_set_scene(c, scene, 0);
-  if (rc) return rc;
-  const size_t npix = (size_t)w * h;
-  HIP_TRY(hipMalloc((void**)&g.dl, npix * 3 * sizeof(float)));
-  HIP_TRY(hipMalloc((void**)&g.dr, npix * 4));
-  rc = rt_context_render_async(c, w, h, st, 0, 1, RT_LAYOUT_IMAGE, g.dl, g.dr, c->stream, nullptr);
-  if (rc) return rc;
-  if (out_linear)
-    HIP_TRY(hipMemcpyAsync(out_linear, g.dl, npix * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
-  if (out_rgba) HIP_TRY(hipMemcpyAsync(out_rgba, g.dr, npix * 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  double ks = 0;
-  rc = rt_context_last_kernel_seconds(c, &ks);
-  if (rc) return rc;
-  double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  if (stats) {
-    stats->render_seconds = secs;
-    stats->kernel_seconds = ks;
-    stats->rays_per_second = (double)npix * st->samples / secs;
-    stats->pixels_per_second = (double)npix / secs;
-    stats->objects = c->flat.objects;
-    stats->lights = (int32_t)c->flat.lights.size();
-  }
   return RT_OK;
 }
 

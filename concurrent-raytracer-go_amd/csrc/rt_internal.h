@@ -33,7 +33,8 @@ struct FlatScene {
 // GetHittables + createCube + material constructors (scene.go:59-190).
 void flatten_scene(const rt_scene& s, FlatScene* out);
 // Binned-SAH BVH over out->spheres (reorders spheres). Requires no triangles.
-void build_sphere_bvh(FlatScene* fs);
+// bins / leaf: SAH bins per axis and spheres per leaf at most (0: defaults).
+void build_sphere_bvh(FlatScene* fs, int bins, int leaf);
 // Dispatch order of the local tiles of (rank, world): descending estimated
 // cost (primitives whose projected bounds overlap the tile), ties by index.
 void tile_dispatch_order(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
@@ -112,13 +113,12 @@ struct KParams {
   int32_t num_blocks;        // this rank's blocks (one workgroup each)
   int32_t layout;     // RT_LAYOUT_*
   int32_t num_wgs;         // = num_blocks
-  int32_t prio_blocks;     // blocks [0, prio_blocks) of the dispatch order raise their wave priority
 };
 
 // Enqueue the render kernel; returns hipError_t as int.
 int launch_render(const KParams& p, bool count, void* stream);
 size_t render_shmem(const KParams& p);
-int launch_unpack(int32_t W, int32_t H, int32_t world, int32_t max_local, const float* pl, const uint8_t* pr,
+int launch_unpack(int32_t W, int32_t H, int32_t world, const void* gathered, size_t share_bytes, size_t rgba_off,
                   float* ol, uint8_t* orgba, void* stream);
 
 // The geometry an occlusion / closest-hit query needs (device pointers).

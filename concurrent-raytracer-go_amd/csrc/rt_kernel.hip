@@ -25,7 +25,7 @@
 //     the sequential loop; when few lanes still run paths, the idle lanes
 //     split the closest-hit and cone scans of the others (wide mode).
 // Large sphere scenes (a BVH) take the wavefront path instead
-// (rt_wavefront.hip) unless RTGO_MEGAKERNEL is set.
+// (rt_wavefront.hip) unless rt_tuning.path asks for the megakernel.
 // Small linear-scan scenes are staged into LDS by every workgroup; large
 // sphere scenes use a BVH (bvh.cpp) with per-lane LDS stacks.  Primitives
 // that provably cannot be hit (tile frustum / shadow cone tests with wide
@@ -42,12 +42,10 @@
 #include "rt_device.h"
 #include "rt_internal.h"
 
-#ifndef RT_WAVES_PER_SIMD
-#define RT_WAVES_PER_SIMD 3  // measured best of 2/3/4 (4 spills the FP64 path state)
-#endif
-#ifndef RT_COOP_MAX
-#define RT_COOP_MAX 8  // cooperative soft shadows when at most this many lanes need them
-#endif
+// waves per SIMD of render_kernel: measured best of 2/3/4 (4 spills the FP64 path state)
+#define RT_WAVES_PER_SIMD 3
+// cooperative soft shadows when at most this many lanes need them (best of 0/2/4/8)
+#define RT_COOP_MAX 8
 
 namespace rtgo {
 
@@ -254,30 +252,6 @@ __device__ __forceinline__ unsigned long long cone_wide(const Geo& g, bool need,
 }
 
 // ------------------------------------------------------------ soft shadows
-// Sequential form (every lane its own): ONE loop over rejection tries (3
-// draws each — the same draws, in the same order, as 16 calls of
-// RandomVec3InUnitSphere); the ray of an accepted point is traced at once.
-// A wave runs ~max over lanes of the total tries (~43) instead of 16 x the
-// max tries per point (~7).  Returns the number of unoccluded rays.
-template <bool kCount>
-__device__ __forceinline__ int soft_seq(const Geo& p, bool masks, bool trace, d3 P, d3 ldir, double ldist,
-                                        Cand cm, rt_rng& rng, int* stack, Counters& c) {
-  int need = 16, unocc = 0;
-  while (need > 0) {
-    const uint32_t ux = rt_rng_next(&rng), uy = rt_rng_next(&rng), uz = rt_rng_next(&rng);
-    cnt<kCount>(c, C_RNG, 3);
-    if (unit_ball_accept(ux, uy, uz)) {
-      const d3 pt = unit_ball_point(ux, uy, uz);
-      --need;
-      cnt<kCount>(c, C_SHADOW);
-      bool occ = false;
-      if (trace) occ = shadow_blocked<kCount>(p, masks, P, normalize(ldir + muls(pt, 0.1)), ldist, cm, stack, c);
-      unocc += occ ? 0 : 1;
-    }
-  }
-  return unocc;
-}
-
 // Cooperative form for ONE owner lane, executed by the whole (converged)
 // wave: lane h evaluates rejection try h of the owner's stream (draws
 // 3h..3h+2 via the PCG jump table), a ballot picks the first `need`
@@ -289,13 +263,8 @@ struct CoopOut {
   int unocc;   // unoccluded rays
   int tries;   // rejection tries consumed
 };
-#ifdef RT_COOP_NOINLINE
-#define RT_COOP_FN __device__ __noinline__
-#else
-#define RT_COOP_FN __device__ __forceinline__
-#endif
 template <bool kCount>
-RT_COOP_FN CoopOut soft_coop(const Geo p, bool masks, bool trace, d3 P, d3 ldir, double ldist, Cand cm, uint64_t x,
+__device__ __forceinline__ CoopOut soft_coop(const Geo p, bool masks, bool trace, d3 P, d3 ldir, double ldist, Cand cm, uint64_t x,
                              const uint64_t* jump, int* stack, Counters& c) {
   const int lane = (int)(threadIdx.x & 63);
   int need = 16, unocc = 0, tries = 0;
@@ -517,18 +486,12 @@ __device__ __forceinline__ void camera_ray(KArg k, int x, int y, int s, rt_rng& 
 //       renderer.go:150-163, bit for bit); at the end the sum is divided by
 //       spp, tone-mapped (renderer.go:348-367) and written once (float3
 //       linear + RGBA8).
-#ifndef RT_ROUND
-#define RT_ROUND 128
-#endif
-constexpr int kRound = RT_ROUND;  // list entries shaded per round (LDS radiance slots)
+constexpr int kRound = 128;  // list entries shaded per round (LDS radiance slots)
 
 template <bool kCount, bool kStage, bool kPilot>
 __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KParams pk) {
   __shared__ uint32_t hbits[kMaxBlockSamples / 32];  // hit samples of the block
   __shared__ int hoff[kMaxBlockSamples / 32 + 1];    // list offset of each bit word; [words] = #hits
-#ifdef RT_HLIST
-  __shared__ uint16_t hlist[kMaxBlockSamples];       // hit sample ids, ascending
-#endif
   __shared__ double slot[kRound][3];                 // radiance of the round's entries
   __shared__ double psum[64][3];                     // per pixel: running sum over samples
   __shared__ uint8_t lpix[64];                       // phase 1: the block's live pixels
@@ -538,7 +501,6 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   const unsigned long long below = (1ull << lane) - 1ull;
   int* stack = reinterpret_cast<int*>(dyn_lds + pk.stack_off) + lane;
   const BlockLoc blk = block_loc(fresh(), blockIdx.x);
-  if ((int)blockIdx.x < fresh()->prio_blocks) __builtin_amdgcn_s_setprio(3);
   // a black block (up to 64 pixels x spp samples) sets no hit bits
   const int nwords = blk.black ? 0 : (blk.np * blk.ns + 31) >> 5;
   if (lane < nwords) hbits[lane] = 0;
@@ -610,9 +572,6 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     // counting variant still walks its samples for the path counts (its
     // queries have no candidates: no hit bit is ever set).
     const int NL = kCount ? NB : (loc.black ? 0 : nlive * ns);
-#ifdef RT_VIS_UNROLL
-#pragma unroll RT_VIS_UNROLL
-#endif
     for (int j = lane; j < NL; j += 64) {
       // j -> (pixel, sample): every sample of the block (kCount) or of its
       // live pixels, in order
@@ -647,22 +606,12 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     if (lane == 63) hoff[nwords] = incl;
   }
   __syncthreads();
-#ifdef RT_HLIST
-  for (int id = lane; id < nwords * 32; id += 64) {
-    const uint32_t word = hbits[id >> 5];
-    if ((word >> (id & 31)) & 1u) hlist[hoff[id >> 5] + __popc(word & ((1u << (id & 31)) - 1u))] = (uint16_t)id;
-  }
-  __syncthreads();
-#endif
   const int nh = hoff[nwords];
   // sample id (pixel * ns + sample - s0) of hit-list entry e < nh: the bit
   // word holding it (the last word whose list offset is <= e, by binary
   // search over hoff), then the (e - offset)-th set bit of that word.  No
   // materialized list: its 2 KB of LDS cost occupancy.
   auto entry_id = [&](int e) -> int {
-#ifdef RT_HLIST
-    return hlist[e];
-#else
     int w = 0;
     for (int step = 16; step; step >>= 1)
       if (w + step < nwords && hoff[w + step] <= e) w += step;
@@ -677,7 +626,6 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       }
     }
     return w * 32 + pos;
-#endif
   };
 #ifdef RT_WG_TIMING
   dbg_vis = __builtin_amdgcn_s_memtime() - tv0;
@@ -797,7 +745,6 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       int mi = 0, self = -1;
       HitSel hs;
       bool wide_q = false, wide_found = false, wide_fb = false;
-#ifndef RT_NO_WIDE
       if constexpr (kStage) {  // wave-uniform: few paths left -> helpers
         const Hot h = hot<kStage>();
         const bool need = alive && depth < h.max_depth;
@@ -811,7 +758,6 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
           wide_q = true;
         }
       }
-#endif
       if (alive) {
         const Hot h = hot<kStage>();
         const Geo& gg = h.g;
@@ -887,7 +833,6 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
             }
           }
           bool wide_c = false;
-#ifndef RT_NO_WIDE
           if constexpr (kStage) {  // few lit hit points: the cone tests with helpers
             if (masks && gg.nt == 0) {
               const unsigned long long cq = __ballot(shade && lit);
@@ -899,7 +844,6 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
               }
             }
           }
-#endif
           if (shade && lit) {
             if (masks && !wide_c) cm = cone_candidates(gg, P, N, front, self, ldir, ldist);
             occl = shadow_blocked<kCount>(gg, masks, P, ldir, ldist, cm, stack, c);  // hard shadow ray
@@ -944,16 +888,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
                 }
               }
             } else {
-#if defined(RT_SOFT_SEQ)
-              if (need_soft) unocc = soft_seq<kCount>(gg, masks, trace, P, ldir, ldist, cm, rng, stack, c);
-#elif defined(RT_QUEUE_MIN)
-              if (__popcll(owners) > RT_QUEUE_MIN)
-                unocc = soft_queue<kCount>(gg, masks, need_soft, trace, P, ldir, ldist, cm, rng, stack, c);
-              else if (need_soft)
-                unocc = soft_seq<kCount>(gg, masks, trace, P, ldir, ldist, cm, rng, stack, c);
-#else
               unocc = soft_queue<kCount>(gg, masks, need_soft, trace, P, ldir, ldist, cm, rng, stack, c);
-#endif
             }
           }
 #ifdef RT_WG_TIMING
@@ -1108,28 +1043,29 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
 #endif
 }
 
-// Gathered [world][max_local][1024] packed tiles -> W*H image.
-__global__ __launch_bounds__(256) void unpack_kernel(int W, int H, int world, int max_local, int tiles_x,
-                                                     int ntiles, const float* __restrict__ pl,
-                                                     const uint8_t* __restrict__ pr, float* __restrict__ ol,
+// Gathered shares [world][share_bytes] (each: [max_local][1024] float3, then
+// [max_local][1024] RGBA8 at rgba_off) -> W*H images.  One thread per image
+// pixel, so the image writes are coalesced; a tile row's 32 pixels read 384
+// contiguous bytes of its share.
+__global__ __launch_bounds__(256) void unpack_kernel(int W, int H, int world, int tiles_x,
+                                                     const uint8_t* __restrict__ g, size_t share_bytes,
+                                                     size_t rgba_off, float* __restrict__ ol,
                                                      uint8_t* __restrict__ orgba) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // over world*max_local*1024
-  const long long total = (long long)world * max_local * 1024;
-  if (i >= total) return;
-  const int r = (int)(i / ((long long)max_local * 1024));
-  const int rem = (int)(i - (long long)r * max_local * 1024);
-  const int lt = rem / 1024, pi = rem % 1024;
-  const int t = r + lt * world;
-  if (t >= ntiles) return;
-  const int x = (t % tiles_x) * 32 + pi % 32, y = (t / tiles_x) * 32 + pi / 32;
-  if (x >= W || y >= H) return;
-  const size_t o = (size_t)y * W + x;
-  if (ol && pl) {
-    ol[o * 3 + 0] = pl[i * 3 + 0];
-    ol[o * 3 + 1] = pl[i * 3 + 1];
-    ol[o * 3 + 2] = pl[i * 3 + 2];
+  const long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= (long long)W * H) return;
+  const int y = (int)(o / W), x = (int)(o - (long long)y * W);
+  const int t = (y >> 5) * tiles_x + (x >> 5);
+  const int r = t % world, lt = t / world;
+  const size_t pi = (size_t)lt * 1024 + (size_t)((y & 31) * 32 + (x & 31));
+  const uint8_t* share = g + (size_t)r * share_bytes;
+  if (ol) {
+    const float* pl = reinterpret_cast<const float*>(share) + pi * 3;
+    ol[o * 3 + 0] = pl[0];
+    ol[o * 3 + 1] = pl[1];
+    ol[o * 3 + 2] = pl[2];
   }
-  if (orgba && pr) *reinterpret_cast<uint32_t*>(orgba + o * 4) = *reinterpret_cast<const uint32_t*>(pr + i * 4);
+  if (orgba)
+    *reinterpret_cast<uint32_t*>(orgba + o * 4) = *reinterpret_cast<const uint32_t*>(share + rgba_off + pi * 4);
 }
 
 size_t render_shmem(const KParams& p) {
@@ -1159,14 +1095,13 @@ int launch_render(const KParams& p, bool count, void* stream) {
   return (int)hipGetLastError();
 }
 
-int launch_unpack(int32_t W, int32_t H, int32_t world, int32_t max_local, const float* pl, const uint8_t* pr,
+int launch_unpack(int32_t W, int32_t H, int32_t world, const void* gathered, size_t share_bytes, size_t rgba_off,
                   float* ol, uint8_t* orgba, void* stream) {
-  const long long total = (long long)world * max_local * 1024;
+  const long long total = (long long)W * H;
   if (total <= 0) return hipSuccess;
-  const int tiles_x = (W + 31) / 32, ntiles = tiles_x * ((H + 31) / 32);
   const unsigned blocks = (unsigned)((total + 255) / 256);
-  hipLaunchKernelGGL(unpack_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, W, H, world, max_local,
-                     tiles_x, ntiles, pl, pr, ol, orgba);
+  hipLaunchKernelGGL(unpack_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, W, H, world, (W + 31) / 32,
+                     (const uint8_t*)gathered, share_bytes, rgba_off, ol, orgba);
   return (int)hipGetLastError();
 }
 

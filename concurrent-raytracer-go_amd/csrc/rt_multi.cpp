@@ -1,0 +1,442 @@
+// rt_multi.cpp — the multi-GPU side of the C ABI (include/rt_api.h):
+// the persistent renderer (rt_renderer_*, one process driving N devices),
+// the one-shot rt_render on top of it, and the RCCL tile gather for
+// one-process-per-GPU runs (rt_comm_*).
+//
+// Reference: (*ParallelRenderer).Render fans 32x32 tiles out to goroutines
+// and collects their pixels on the main goroutine (renderer.go:67-126,
+// createRenderTasks :398-436).  Here tiles t are dealt to ranks t % N (one
+// rank per GPU), every rank renders its share into a packed buffer (float3
+// + RGBA8, 16 B per pixel, rt_packed_bytes), and the shares meet on the
+// first device in ONE RCCL send/recv group over xGMI, where one kernel
+// scatters them into the image.  The random stream is keyed
+// by global pixel and sample, so the image is the same for every N.
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "rt_internal.h"
+
+using namespace rtgo;
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      set_error(std::string(#expr) + " failed: " + hipGetErrorString(e_));             \
+      return RT_E_DEVICE;                                                               \
+    }                                                                                   \
+  } while (0)
+
+#define NCCL_TRY(expr)                                                                  \
+  do {                                                                                  \
+    ncclResult_t e_ = (expr);                                                           \
+    if (e_ != ncclSuccess) {                                                            \
+      set_error(std::string(#expr) + " failed: " + ncclGetErrorString(e_));            \
+      return RT_E_DEVICE;                                                               \
+    }                                                                                   \
+  } while (0)
+
+namespace {
+
+struct Rank {
+  int device = 0;
+  int comm_idx = 0;             // index of its device in the distinct-device list (0: the root device)
+  rt_context* ctx = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;    // its share is rendered
+  void* share = nullptr;        // its own share buffer (devices other than the root's)
+  size_t share_cap = 0;
+};
+
+// Device buffer that grows on demand.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int grow(int device, size_t bytes) {
+    if (bytes <= cap) return RT_OK;
+    HIP_TRY(hipSetDevice(device));
+    if (p) HIP_TRY(hipFree(p));
+    p = nullptr;
+    cap = 0;
+    HIP_TRY(hipMalloc(&p, bytes));
+    cap = bytes;
+    return RT_OK;
+  }
+  void release(int device) {
+    if (p) {
+      (void)hipSetDevice(device);
+      (void)hipFree(p);
+    }
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// The scene's content as bytes: two calls with equal bytes render the same
+// image, so the second one re-uploads nothing.
+void scene_bytes(const rt_scene& s, std::vector<uint8_t>* out) {
+  out->clear();
+  auto put = [&](const void* p, size_t n) {
+    const uint8_t* b = (const uint8_t*)p;
+    out->insert(out->end(), b, b + n);
+  };
+  put(&s.camera, sizeof s.camera);
+  put(&s.num_objects, sizeof s.num_objects);
+  put(&s.num_lights, sizeof s.num_lights);
+  if (s.num_objects > 0) put(s.objects, sizeof(rt_object) * (size_t)s.num_objects);
+  if (s.num_lights > 0) put(s.lights, sizeof(rt_light) * (size_t)s.num_lights);
+}
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+struct rt_renderer {
+  std::vector<Rank> ranks;
+  std::vector<int> devices;        // distinct devices, the root's first
+  std::vector<ncclComm_t> comms;   // one per distinct device (empty when there is one)
+  std::vector<hipStream_t> comm_streams;  // per distinct device: the stream of its first rank
+  DevBuf gathered;                 // root: [world][share bytes]
+  DevBuf img_lin, img_rgba;        // root: the W*H image
+  std::vector<uint8_t> scene_key;  // content of the scene the contexts hold
+  bool have_scene = false;
+  rt_tuning tun;
+};
+
+struct rt_comm {
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1, device = 0;
+};
+
+namespace {
+
+int renderer_fail_cleanup(rt_renderer* r, int rc) {
+  rt_renderer_destroy(r);
+  return rc;
+}
+
+// Ranks on devices other than the root's send their shares; the root receives
+// each into its slot of the gather buffer (one group, in rank order, so the
+// sends and receives of one device pair match in order).
+int group_gather(rt_renderer* r, size_t share_bytes) {
+  const int n = (int)r->ranks.size();
+  hipStream_t root_s = r->ranks[0].stream;
+  for (int k = 1; k < n; ++k) {
+    Rank& q = r->ranks[k];
+    if (q.comm_idx == 0) continue;
+    HIP_TRY(hipSetDevice(q.device));
+    HIP_TRY(hipEventRecord(q.done, q.stream));
+    HIP_TRY(hipStreamWaitEvent(r->comm_streams[q.comm_idx], q.done, 0));
+  }
+  NCCL_TRY(ncclGroupStart());
+  for (int k = 1; k < n; ++k) {
+    Rank& q = r->ranks[k];
+    if (q.comm_idx == 0) continue;
+    NCCL_TRY(ncclSend(q.share, share_bytes, ncclUint8, 0, r->comms[q.comm_idx], r->comm_streams[q.comm_idx]));
+    NCCL_TRY(ncclRecv((uint8_t*)r->gathered.p + (size_t)k * share_bytes, share_bytes, ncclUint8, q.comm_idx,
+                      r->comms[0], root_s));
+  }
+  NCCL_TRY(ncclGroupEnd());
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t rt_max_local_tiles(int32_t w, int32_t h, int32_t world) { return rt_tiles_for_rank(w, h, 0, world); }
+
+size_t rt_packed_bytes(int32_t w, int32_t h, int32_t world) {
+  return (size_t)std::max(rt_max_local_tiles(w, h, world), 0) * 1024 * 16;
+}
+
+size_t rt_packed_rgba_offset(int32_t w, int32_t h, int32_t world) {
+  return (size_t)std::max(rt_max_local_tiles(w, h, world), 0) * 1024 * 12;
+}
+
+int rt_unpack_tiles_async(int32_t w, int32_t h, int32_t world, const void* d_gathered, float* d_linear,
+                          uint8_t* d_rgba, void* stream) {
+  if (w <= 0 || h <= 0 || world < 1 || !d_gathered) {
+    set_error("invalid unpack arguments");
+    return RT_E_INVALID;
+  }
+  int e = launch_unpack(w, h, world, d_gathered, rt_packed_bytes(w, h, world), rt_packed_rgba_offset(w, h, world),
+                        d_linear, d_rgba, stream);
+  if (e != hipSuccess) {
+    set_error(std::string("unpack launch failed: ") + hipGetErrorString((hipError_t)e));
+    return RT_E_DEVICE;
+  }
+  return RT_OK;
+}
+
+int rt_renderer_create(const int32_t* devices, int32_t n, rt_renderer** out) {
+  if (!out || n < 1 || n > 1024) {
+    set_error("rt_renderer_create: out is NULL or num_devices not in [1, 1024]");
+    return RT_E_INVALID;
+  }
+  *out = nullptr;
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  rt_renderer* r = new rt_renderer();
+  rt_tuning_default(&r->tun);
+  r->ranks.resize(n);
+  for (int k = 0; k < n; ++k) {
+    const int d = devices ? devices[k] : k;
+    if (d < 0 || d >= ndev) {
+      set_error("device " + std::to_string(d) + " out of range (" + std::to_string(ndev) + " devices)");
+      return renderer_fail_cleanup(r, RT_E_DEVICE);
+    }
+    Rank& q = r->ranks[k];
+    q.device = d;
+    auto it = std::find(r->devices.begin(), r->devices.end(), d);
+    q.comm_idx = (int)(it - r->devices.begin());
+    if (it == r->devices.end()) r->devices.push_back(d);
+    int rc = rt_context_create(d, &q.ctx);
+    if (rc) return renderer_fail_cleanup(r, rc);
+    if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&q.done, hipEventDisableTiming) != hipSuccess) {
+      set_error("rt_renderer_create: stream / event creation failed");
+      return renderer_fail_cleanup(r, RT_E_DEVICE);
+    }
+  }
+  for (int k = 0; k < n; ++k) {
+    Rank& q = r->ranks[k];
+    if ((int)r->comm_streams.size() <= q.comm_idx) r->comm_streams.push_back(q.stream);
+  }
+  if (r->devices.size() > 1) {
+    r->comms.resize(r->devices.size());
+    ncclResult_t e = ncclCommInitAll(r->comms.data(), (int)r->devices.size(), r->devices.data());
+    if (e != ncclSuccess) {
+      r->comms.clear();
+      set_error(std::string("ncclCommInitAll failed: ") + ncclGetErrorString(e));
+      return renderer_fail_cleanup(r, RT_E_DEVICE);
+    }
+  }
+  *out = r;
+  return RT_OK;
+}
+
+void rt_renderer_destroy(rt_renderer* r) {
+  if (!r) return;
+  for (Rank& q : r->ranks) {
+    if (q.stream) {
+      (void)hipSetDevice(q.device);
+      (void)hipStreamSynchronize(q.stream);
+    }
+  }
+  for (ncclComm_t c : r->comms) (void)ncclCommDestroy(c);
+  const int root = r->ranks.empty() ? 0 : r->ranks[0].device;
+  r->gathered.release(root);
+  r->img_lin.release(root);
+  r->img_rgba.release(root);
+  for (Rank& q : r->ranks) {
+    (void)hipSetDevice(q.device);
+    if (q.share) (void)hipFree(q.share);
+    if (q.done) (void)hipEventDestroy(q.done);
+    if (q.stream) (void)hipStreamDestroy(q.stream);
+    rt_context_destroy(q.ctx);
+  }
+  delete r;
+}
+
+int rt_renderer_set_tuning(rt_renderer* r, const rt_tuning* t) {
+  if (!r || !t) {
+    set_error("renderer or tuning is NULL");
+    return RT_E_INVALID;
+  }
+  for (Rank& q : r->ranks) {
+    int rc = rt_context_set_tuning(q.ctx, t);
+    if (rc) return rc;
+  }
+  r->tun = *t;
+  r->have_scene = false;  // the BVH shape may change
+  return RT_OK;
+}
+
+int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t h, const rt_settings* st,
+                       float* out_linear, uint8_t* out_rgba, rt_stats* stats) {
+  if (!r) {
+    set_error("renderer is NULL");
+    return RT_E_INVALID;
+  }
+  int rc = rt_validate(scene, w, h, st);
+  if (rc) return rc;
+  const double t0 = now_s();
+  const int n = (int)r->ranks.size();
+  const int root = r->ranks[0].device;
+  // scene upload (flatten + BVH) only when its content changed
+  std::vector<uint8_t> key;
+  scene_bytes(*scene, &key);
+  if (!r->have_scene || key != r->scene_key) {
+    r->have_scene = false;
+    for (Rank& q : r->ranks) {
+      int rc = rt_context_set_scene(q.ctx, scene, 0);
+      if (rc) return rc;
+    }
+    r->scene_key.swap(key);
+    r->have_scene = true;
+  }
+  const size_t npix = (size_t)w * h;
+  rc = r->img_lin.grow(root, npix * 3 * sizeof(float));
+  if (!rc) rc = r->img_rgba.grow(root, npix * 4);
+  if (rc) return rc;
+  hipStream_t root_s = r->ranks[0].stream;
+  if (n == 1) {
+    rc = rt_context_render_async(r->ranks[0].ctx, w, h, st, 0, 1, RT_LAYOUT_IMAGE, (float*)r->img_lin.p,
+                                 (uint8_t*)r->img_rgba.p, root_s, nullptr);
+    if (rc) return rc;
+  } else {
+    const size_t share = rt_packed_bytes(w, h, n), rgba_off = rt_packed_rgba_offset(w, h, n);
+    rc = r->gathered.grow(root, share * (size_t)n);
+    if (rc) return rc;
+    for (int k = 0; k < n; ++k) {
+      Rank& q = r->ranks[k];
+      uint8_t* buf;
+      if (q.comm_idx == 0) {  // the root's device: straight into the gather buffer
+        buf = (uint8_t*)r->gathered.p + (size_t)k * share;
+      } else {
+        if (share > q.share_cap) {
+          HIP_TRY(hipSetDevice(q.device));
+          if (q.share) HIP_TRY(hipFree(q.share));
+          q.share = nullptr;
+          q.share_cap = 0;
+          HIP_TRY(hipMalloc(&q.share, share));
+          q.share_cap = share;
+        }
+        buf = (uint8_t*)q.share;
+      }
+      rc = rt_context_render_async(q.ctx, w, h, st, k, n, RT_LAYOUT_PACKED_TILES, (float*)buf, buf + rgba_off,
+                                   q.stream, nullptr);
+      if (rc) return rc;
+    }
+    if (r->devices.size() > 1) {
+      rc = group_gather(r, share);
+      if (rc) return rc;
+    }
+    HIP_TRY(hipSetDevice(root));
+    for (int k = 1; k < n; ++k) {  // the root's other ranks (their own streams)
+      Rank& q = r->ranks[k];
+      if (q.comm_idx != 0) continue;
+      HIP_TRY(hipEventRecord(q.done, q.stream));
+      HIP_TRY(hipStreamWaitEvent(root_s, q.done, 0));
+    }
+    rc = rt_unpack_tiles_async(w, h, n, r->gathered.p, (float*)r->img_lin.p, (uint8_t*)r->img_rgba.p, root_s);
+    if (rc) return rc;
+  }
+  HIP_TRY(hipSetDevice(root));
+  if (out_linear)
+    HIP_TRY(hipMemcpyAsync(out_linear, r->img_lin.p, npix * 3 * sizeof(float), hipMemcpyDeviceToHost, root_s));
+  if (out_rgba) HIP_TRY(hipMemcpyAsync(out_rgba, r->img_rgba.p, npix * 4, hipMemcpyDeviceToHost, root_s));
+  double ks = 0;
+  for (Rank& q : r->ranks) {
+    HIP_TRY(hipSetDevice(q.device));
+    HIP_TRY(hipStreamSynchronize(q.stream));
+    double s = 0;
+    rc = rt_context_last_kernel_seconds(q.ctx, &s);
+    if (rc) return rc;
+    ks = std::max(ks, s);
+  }
+  const double secs = now_s() - t0;
+  if (stats) {
+    memset(stats, 0, sizeof *stats);
+    stats->render_seconds = secs;
+    stats->kernel_seconds = ks;
+    stats->rays_per_second = (double)npix * st->samples / secs;
+    stats->pixels_per_second = (double)npix / secs;
+    stats->objects = scene->num_objects;  // len(hittables): a cube counts once (renderer.go:109)
+    stats->lights = scene->num_lights;
+  }
+  return RT_OK;
+}
+
+int rt_render(const rt_scene* scene, int32_t w, int32_t h, const rt_settings* st, float* out_linear,
+              uint8_t* out_rgba, rt_stats* stats) {
+  int rc = rt_validate(scene, w, h, st);  // before touching a device
+  if (rc) return rc;
+  const double t0 = now_s();
+  rt_renderer* r = nullptr;
+  rc = rt_renderer_create(nullptr, std::max(1, st->num_devices), &r);
+  if (rc) return rc;
+  rc = rt_renderer_render(r, scene, w, h, st, out_linear, out_rgba, stats);
+  rt_renderer_destroy(r);
+  if (!rc && stats) {  // Go's Render time covers everything (renderer.go:68,101)
+    stats->render_seconds = now_s() - t0;
+    stats->rays_per_second = (double)w * h * st->samples / stats->render_seconds;
+    stats->pixels_per_second = (double)w * h / stats->render_seconds;
+  }
+  return rc;
+}
+
+// ------------------------------------------------------------ multi-process
+
+int rt_comm_unique_id(uint8_t* id) {
+  if (!id) {
+    set_error("id is NULL");
+    return RT_E_INVALID;
+  }
+  static_assert(sizeof(ncclUniqueId) == RT_COMM_ID_BYTES, "RT_COMM_ID_BYTES != NCCL_UNIQUE_ID_BYTES");
+  ncclUniqueId u;
+  NCCL_TRY(ncclGetUniqueId(&u));
+  memcpy(id, &u, sizeof u);
+  return RT_OK;
+}
+
+int rt_comm_create(const uint8_t* id, int32_t world, int32_t rank, int32_t device, rt_comm** out) {
+  if (!id || !out || world < 1 || rank < 0 || rank >= world) {
+    set_error("rt_comm_create: invalid arguments");
+    return RT_E_INVALID;
+  }
+  *out = nullptr;
+  HIP_TRY(hipSetDevice(device));
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  rt_comm* c = new rt_comm();
+  c->rank = rank;
+  c->world = world;
+  c->device = device;
+  ncclResult_t e = ncclCommInitRank(&c->comm, world, u, rank);
+  if (e != ncclSuccess) {
+    delete c;
+    set_error(std::string("ncclCommInitRank failed: ") + ncclGetErrorString(e));
+    return RT_E_DEVICE;
+  }
+  *out = c;
+  return RT_OK;
+}
+
+void rt_comm_destroy(rt_comm* c) {
+  if (!c) return;
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  delete c;
+}
+
+int rt_comm_gather_tiles_async(rt_comm* c, int32_t w, int32_t h, const void* d_share, void* d_gathered,
+                               void* stream) {
+  if (!c || w <= 0 || h <= 0 || !d_share || (c->rank == 0 && !d_gathered)) {
+    set_error("rt_comm_gather_tiles_async: invalid arguments");
+    return RT_E_INVALID;
+  }
+  if (c->world == 1) return RT_OK;
+  const size_t share = rt_packed_bytes(w, h, c->world);
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipSetDevice(c->device));
+  NCCL_TRY(ncclGroupStart());
+  if (c->rank == 0) {
+    for (int k = 1; k < c->world; ++k)
+      NCCL_TRY(ncclRecv((uint8_t*)d_gathered + (size_t)k * share, share, ncclUint8, k, c->comm, s));
+  } else {
+    NCCL_TRY(ncclSend(d_share, share, ncclUint8, 0, c->comm, s));
+  }
+  NCCL_TRY(ncclGroupEnd());
+  return RT_OK;
+}
+
+}  // extern "C"

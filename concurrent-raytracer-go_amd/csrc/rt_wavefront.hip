@@ -54,9 +54,7 @@ constexpr int kWfBlock = kWfBlockSlots;  // threads per workgroup of the dense k
 // fits behind them (10k spheres: all 6,623 nodes, 104 KB).  The launch size
 // (p.trav_block <= kTravBlock) and workgroups per CU are host choices.
 constexpr int kTravBlock = kWfTravBlock;
-#ifndef RT_WF_TRAV_WAVES
 #define RT_WF_TRAV_WAVES 4  // waves per SIMD the traversal kernels are compiled for
-#endif
 #define RT_TRAV_ATTR __launch_bounds__(kTravBlock) __attribute__((amdgpu_waves_per_eu(RT_WF_TRAV_WAVES)))
 constexpr int kLdsBytes = 160 * 1024;    // LDS per CU (MI355X), all of it available to one workgroup
 constexpr int kRefill = 16;              // persistent traversal: refill once this many lanes are idle
@@ -317,10 +315,7 @@ __device__ __forceinline__ void descend(glb_node* __restrict__ qb, lds_node* __r
 // together, before any test, so a leaf costs one memory round trip instead of
 // one per sphere (the tests stop early in occlusion, which kept the compiler
 // from hoisting the loads).  Indices past the leaf reload its last sphere.
-#ifndef RT_LEAF_BATCH
-#define RT_LEAF_BATCH 4
-#endif
-constexpr int kLeafBatch = RT_LEAF_BATCH;
+constexpr int kLeafBatch = 4;  // = the BVH's largest leaf (bvh.cpp)
 __device__ __forceinline__ void load_leaf(const DSphere* __restrict__ sp, int first, int count, DSphere* out) {
 #pragma unroll
   for (int k = 0; k < kLeafBatch; ++k) out[k] = sp[first + min(k, count - 1)];
@@ -479,7 +474,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade1(const WfParams p) {
   const int j = blockIdx.x * kWfBlock + threadIdx.x;
   size_t slot = 0;
   bool hit = false;
-  uint32_t lit = 0;
+  d3 P = mk(0, 0, 0);
   if (j < n) {
     slot = dense_at(dn, j, p.shard_cap);
     const int hi = p.hidx[slot];
@@ -490,7 +485,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade1(const WfParams p) {
       const d3 o = ld_o(a, slot), d = ld_d(a, slot);
       const DSphere& S0 = p.g.spheres[hi];
       const double t = p.hnum[slot] / len2(d);
-      const d3 P = o + muls(d, t);
+      P = o + muls(d, t);
       const d3 outward = divs(P - ld3(S0.c), S0.r);
       const bool front = dot(d, outward) < 0;
       const d3 N = front ? outward : neg(outward);
@@ -501,7 +496,16 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade1(const WfParams p) {
       p.ny[slot] = N.y;
       p.nz[slot] = N.z;
       p.hinfo[slot] = (S0.mat << 1) | (front ? 1 : 0);
-      for (int li = 0; li < p.nl; ++li) {
+    }
+  }
+  const int shard = blockIdx.x % kWfShards;
+  uint32_t* hq = p.hardq + (size_t)shard * p.hard_cap;
+  // lights in chunks of 32 (one bit each; any number of lights)
+  for (int base = 0; base < p.nl; base += 32) {
+    uint32_t lit = 0;
+    if (hit) {
+      const int end = min(p.nl, base + 32);
+      for (int li = base; li < end; ++li) {
         d3 ldir;
         double ldist;
         light_vec(p.lights[li], P, ldir, ldist);
@@ -509,15 +513,13 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade1(const WfParams p) {
         if (!(ldist < 0.001)) {
           cnt<kCount>(c, C_LIGHT);
           cnt<kCount>(c, C_SHADOW);
-          lit |= 1u << li;
+          lit |= 1u << (li - base);
         }
       }
     }
+    int q = block_append(__popc(lit), &p.ctl->hard_cnt[shard * 32], s_wave, &s_base);
+    for (uint32_t m = lit; m; m &= m - 1) hq[q++] = (uint32_t)(slot * p.nl) + (uint32_t)(base + __builtin_ctz(m));
   }
-  const int shard = blockIdx.x % kWfShards;
-  int q = block_append(__popc(lit), &p.ctl->hard_cnt[shard * 32], s_wave, &s_base);
-  uint32_t* hq = p.hardq + (size_t)shard * p.hard_cap;
-  for (uint32_t m = lit; m; m &= m - 1) hq[q++] = (uint32_t)(slot * p.nl) + (uint32_t)__builtin_ctz(m);
   flush_counts<kCount>(p, c);
 }
 
@@ -636,40 +638,45 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
     for (int k = 0; k < 9; ++k) c.v[k] = 0;
   const int j = blockIdx.x * kWfBlock + threadIdx.x;
   size_t slot = 0;
-  uint32_t own = 0;
+  bool hit = false;
+  d3 P = mk(0, 0, 0);
   if (j < n) {
     slot = dense_at(dn, j, p.shard_cap);
-    if (p.hidx[slot] >= 0) {
-      const d3 P = mk(p.px[slot], p.py[slot], p.pz[slot]);
-      for (int li = 0; li < p.nl; ++li) {
+    hit = p.hidx[slot] >= 0;
+    if (hit) P = mk(p.px[slot], p.py[slot], p.pz[slot]);
+  }
+  const int shard = blockIdx.x % kWfShards;
+  rt_rng rng{hit ? p.cur.rng[slot] : 0ull};
+  // lights in chunks of 32 (one bit each; any number of lights), in light order
+  for (int base = 0; base < p.nl; base += 32) {
+    uint32_t own = 0;
+    if (hit) {
+      const int end = min(p.nl, base + 32);
+      for (int li = base; li < end; ++li) {
         d3 ldir;
         double ldist;
         light_vec(p.lights[li], P, ldir, ldist);
-        if (!(ldist < 0.001) && !(p.lstate[slot * p.nl + li] & kHardBit)) own |= 1u << li;
+        if (!(ldist < 0.001) && !(p.lstate[slot * p.nl + li] & kHardBit)) own |= 1u << (li - base);
+      }
+    }
+    const int q = block_append(16 * __popc(own), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
+    if (own) {
+      uint4* sq = reinterpret_cast<uint4*>(p.softq) + (size_t)shard * p.soft_cap + q;
+      int k = 0;  // entries written (an index, not a bumped pointer)
+      for (uint32_t m = own; m; m &= m - 1) {
+        const uint32_t key = (uint32_t)(slot * p.nl) + (uint32_t)(base + __builtin_ctz(m));
+        cnt<kCount>(c, C_SHADOW, 16);
+        for (const int end = k + 16; k < end;) {
+          const uint32_t ux = rt_rng_next(&rng), uy = rt_rng_next(&rng), uz = rt_rng_next(&rng);
+          cnt<kCount>(c, C_RNG, 3);
+          const bool acc = unit_ball_accept(ux, uy, uz);
+          if (acc) sq[k] = make_uint4(key, ux, uy, uz);
+          k += acc ? 1 : 0;
+        }
       }
     }
   }
-  const int shard = blockIdx.x % kWfShards;
-  const int q = block_append(16 * __popc(own), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
-  if (own) {
-    uint4* sq = reinterpret_cast<uint4*>(p.softq) + (size_t)shard * p.soft_cap + q;
-    rt_rng rng{p.cur.rng[slot]};
-    int k = 0;  // entries written (an index, not a bumped pointer: hipcc of ROCm 7.2
-                // lost the pointer increment of points accepted on the rare
-                // binary64 branch of unit_ball_accept)
-    for (uint32_t m = own; m; m &= m - 1) {
-      const uint32_t key = (uint32_t)(slot * p.nl) + (uint32_t)__builtin_ctz(m);
-      cnt<kCount>(c, C_SHADOW, 16);
-      for (const int end = k + 16; k < end;) {
-        const uint32_t ux = rt_rng_next(&rng), uy = rt_rng_next(&rng), uz = rt_rng_next(&rng);
-        cnt<kCount>(c, C_RNG, 3);
-        const bool acc = unit_ball_accept(ux, uy, uz);
-        if (acc) sq[k] = make_uint4(key, ux, uy, uz);
-        k += acc ? 1 : 0;
-      }
-    }
-    p.cur.rng[slot] = rng.x;
-  }
+  if (hit) p.cur.rng[slot] = rng.x;
   flush_counts<kCount>(p, c);
 }
 

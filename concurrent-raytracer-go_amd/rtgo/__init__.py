@@ -22,7 +22,9 @@ from datetime import datetime, timezone
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# RTGO_LIB selects an alternative build of the same library (A/B variants)
+# RTGO_LIB selects an alternative build of the same library (the RT_WG_TIMING
+# instrumented build of scripts/wg_timing.py); the library itself reads no
+# environment variable
 LIB_PATH = os.environ.get("RTGO_LIB") or os.path.join(os.path.dirname(_HERE), "build", "librtgo.so")
 
 RT_OK = 0
@@ -37,6 +39,8 @@ MATERIAL_KINDS = {
     "diffuselight": 6,
 }
 RT_LAYOUT_IMAGE, RT_LAYOUT_PACKED_TILES = 0, 1
+RT_PATH_AUTO, RT_PATH_MEGAKERNEL = 0, 1
+RT_COMM_ID_BYTES = 128
 
 
 class RenderError(RuntimeError):
@@ -106,8 +110,29 @@ class Settings(ctypes.Structure):
         ("soft_shadows", ctypes.c_int32),
         ("depth_of_field", ctypes.c_int32),
         ("num_workers", ctypes.c_int32),
-        ("_pad", ctypes.c_int32),
+        ("num_devices", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
+    ]
+
+
+class Tuning(ctypes.Structure):
+    """rt_tuning: how the same work is cut and ordered (never the image)."""
+
+    _fields_ = [
+        ("path", ctypes.c_int32),
+        ("pilot", ctypes.c_int32),
+        ("frustum", ctypes.c_int32),
+        ("stage", ctypes.c_int32),
+        ("block_work", ctypes.c_double),
+        ("block_samples", ctypes.c_int32),
+        ("bvh_bins", ctypes.c_int32),
+        ("bvh_leaf", ctypes.c_int32),
+        ("wf_paths", ctypes.c_int32),
+        ("wf_chunk", ctypes.c_int64),
+        ("wf_lds_nodes", ctypes.c_int32),
+        ("wf_trav_block", ctypes.c_int32),
+        ("wf_trav_wgs", ctypes.c_int32),
+        ("_pad", ctypes.c_int32),
     ]
 
 
@@ -154,13 +179,27 @@ EXPORTED_SYMBOLS = [
     "rt_scene_free",
     "rt_scene_print_hittables",
     "rt_render",
+    "rt_validate",
+    "rt_renderer_create",
+    "rt_renderer_render",
+    "rt_renderer_destroy",
+    "rt_renderer_set_tuning",
+    "rt_tuning_default",
+    "rt_context_set_tuning",
     "rt_context_create",
     "rt_context_destroy",
     "rt_context_set_scene",
     "rt_num_tiles",
     "rt_tiles_for_rank",
+    "rt_max_local_tiles",
+    "rt_packed_bytes",
+    "rt_packed_rgba_offset",
     "rt_context_render_async",
     "rt_unpack_tiles_async",
+    "rt_comm_unique_id",
+    "rt_comm_create",
+    "rt_comm_destroy",
+    "rt_comm_gather_tiles_async",
     "rt_context_last_kernel_seconds",
     "rt_context_set_debug_buffer",
     "rt_tonemap_rgba",
@@ -206,6 +245,23 @@ def lib():
             ctypes.c_int,
             [ctypes.POINTER(SceneView), i32, i32, ctypes.POINTER(Settings), vp, vp, ctypes.POINTER(Stats)],
         ),
+        "rt_validate": (ctypes.c_int, [ctypes.POINTER(SceneView), i32, i32, ctypes.POINTER(Settings)]),
+        "rt_renderer_create": (ctypes.c_int, [ctypes.POINTER(i32), i32, ctypes.POINTER(vp)]),
+        "rt_renderer_render": (
+            ctypes.c_int,
+            [vp, ctypes.POINTER(SceneView), i32, i32, ctypes.POINTER(Settings), vp, vp, ctypes.POINTER(Stats)],
+        ),
+        "rt_renderer_destroy": (None, [vp]),
+        "rt_renderer_set_tuning": (ctypes.c_int, [vp, ctypes.POINTER(Tuning)]),
+        "rt_tuning_default": (None, [ctypes.POINTER(Tuning)]),
+        "rt_context_set_tuning": (ctypes.c_int, [vp, ctypes.POINTER(Tuning)]),
+        "rt_max_local_tiles": (i32, [i32, i32, i32]),
+        "rt_packed_bytes": (sz, [i32, i32, i32]),
+        "rt_packed_rgba_offset": (sz, [i32, i32, i32]),
+        "rt_comm_unique_id": (ctypes.c_int, [vp]),
+        "rt_comm_create": (ctypes.c_int, [vp, i32, i32, i32, ctypes.POINTER(vp)]),
+        "rt_comm_destroy": (None, [vp]),
+        "rt_comm_gather_tiles_async": (ctypes.c_int, [vp, i32, i32, vp, vp, vp]),
         "rt_context_create": (ctypes.c_int, [i32, ctypes.POINTER(vp)]),
         "rt_context_destroy": (None, [vp]),
         "rt_context_set_scene": (ctypes.c_int, [vp, ctypes.POINTER(SceneView), i32]),
@@ -215,7 +271,7 @@ def lib():
             ctypes.c_int,
             [vp, i32, i32, ctypes.POINTER(Settings), i32, i32, i32, vp, vp, vp, ctypes.POINTER(Counts)],
         ),
-        "rt_unpack_tiles_async": (ctypes.c_int, [i32, i32, i32, i32, vp, vp, vp, vp, vp]),
+        "rt_unpack_tiles_async": (ctypes.c_int, [i32, i32, i32, vp, vp, vp, vp]),
         "rt_context_last_kernel_seconds": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
         "rt_context_set_debug_buffer": (ctypes.c_int, [vp, vp]),
         "rt_tonemap_rgba": (None, [vp, i32, vp]),
@@ -240,6 +296,14 @@ def default_settings() -> Settings:
     s = Settings()
     lib().rt_settings_default(ctypes.byref(s))
     return s
+
+
+def default_tuning(**over) -> Tuning:
+    t = Tuning()
+    lib().rt_tuning_default(ctypes.byref(t))
+    for k, v in over.items():
+        setattr(t, k, v)
+    return t
 
 
 # --------------------------------------------------------------- scene
@@ -348,12 +412,47 @@ class ParallelRenderer:
         "Better specular highlights for metallic surfaces",
     ]
 
-    def __init__(self, num_workers: int = 1):
+    def __init__(self, num_workers: int = 1, num_devices: int = 1, devices=None):
+        """devices: the device of each rank (default 0..num_devices-1; a
+        device may repeat: its ranks share it)."""
         self.settings = default_settings()  # NewParallelRenderer defaults, renderer.go:54-65
         self.settings.num_workers = num_workers
+        self.settings.num_devices = len(devices) if devices else num_devices
+        self.devices = list(devices) if devices else None
         self.benchmark_data: dict = {}
         self.last_linear = None
         self.last_stats = None
+        self._r = None  # the rt_renderer (made by the first render, kept like the Go object)
+        self._tuning = None
+
+    def set_tuning(self, tuning: Tuning):
+        self._tuning = tuning
+        if self._r is not None:
+            _check(lib().rt_renderer_set_tuning(self._r, ctypes.byref(tuning)))
+
+    def _renderer(self):
+        if self._r is None:
+            h = ctypes.c_void_p()
+            if self.devices:
+                devs = (ctypes.c_int32 * len(self.devices))(*self.devices)
+                _check(lib().rt_renderer_create(devs, len(self.devices), ctypes.byref(h)))
+            else:
+                _check(lib().rt_renderer_create(None, max(1, self.settings.num_devices), ctypes.byref(h)))
+            self._r = h
+            if self._tuning is not None:
+                _check(lib().rt_renderer_set_tuning(self._r, ctypes.byref(self._tuning)))
+        return self._r
+
+    def close(self):
+        if self._r is not None and _lib is not None:
+            _lib.rt_renderer_destroy(self._r)
+        self._r = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     # settings.go:3-25
     def set_samples(self, samples: int):
@@ -395,11 +494,13 @@ class ParallelRenderer:
         The mean linear radiance (before tone mapping) is kept in
         ``self.last_linear`` as an (H, W, 3) float32 array.
         """
+        _check(lib().rt_validate(ctypes.byref(scene.view), width, height, ctypes.byref(self.settings)))
         lin = np.zeros((height, width, 3), np.float32)
         rgba = np.zeros((height, width, 4), np.uint8)
         st = Stats()
         _check(
-            lib().rt_render(
+            lib().rt_renderer_render(
+                self._renderer(),
                 ctypes.byref(scene.view),
                 width,
                 height,
@@ -456,6 +557,9 @@ class Context:
         self._scene = scene  # keep alive
         _check(lib().rt_context_set_scene(self._h, ctypes.byref(scene.view), force_bvh))
 
+    def set_tuning(self, tuning: Tuning):
+        _check(lib().rt_context_set_tuning(self._h, ctypes.byref(tuning)))
+
     def render_async(self, width, height, settings: Settings, d_linear: int, d_rgba: int, stream: int = 0,
                      rank: int = 0, world: int = 1, layout: int = RT_LAYOUT_IMAGE):
         _check(
@@ -504,10 +608,65 @@ def tiles_for_rank(width: int, height: int, rank: int, world: int) -> int:
     return lib().rt_tiles_for_rank(width, height, rank, world)
 
 
-def unpack_tiles_async(width, height, world, max_local, d_pl, d_pr, d_ol, d_or, stream=0):
+def render(scene: Scene, width: int, height: int, settings: Settings):
+    """One-shot rt_render: (rgba (H,W,4) u8, linear (H,W,3) f32, Stats)."""
+    lin = np.zeros((height, width, 3), np.float32)
+    rgba = np.zeros((height, width, 4), np.uint8)
+    st = Stats()
+    _check(lib().rt_render(ctypes.byref(scene.view), width, height, ctypes.byref(settings), lin.ctypes.data,
+                           rgba.ctypes.data, ctypes.byref(st)))
+    return rgba, lin, st
+
+
+def max_local_tiles(width: int, height: int, world: int) -> int:
+    return lib().rt_max_local_tiles(width, height, world)
+
+
+def packed_bytes(width: int, height: int, world: int) -> int:
+    """Bytes of one rank's packed share: float3 + RGBA8 per pixel of rank 0's tiles."""
+    return lib().rt_packed_bytes(width, height, world)
+
+
+def packed_rgba_offset(width: int, height: int, world: int) -> int:
+    return lib().rt_packed_rgba_offset(width, height, world)
+
+
+def unpack_tiles_async(width, height, world, d_gathered, d_linear, d_rgba, stream=0):
+    """Scatter gathered shares [world][packed_bytes] into W*H images."""
     _check(
         lib().rt_unpack_tiles_async(
-            width, height, world, max_local, ctypes.c_void_p(d_pl), ctypes.c_void_p(d_pr),
-            ctypes.c_void_p(d_ol), ctypes.c_void_p(d_or), ctypes.c_void_p(stream),
+            width, height, world, ctypes.c_void_p(d_gathered), ctypes.c_void_p(d_linear), ctypes.c_void_p(d_rgba),
+            ctypes.c_void_p(stream),
         )
     )
+
+
+class Comm:
+    """rt_comm: the RCCL communicator of one process per GPU (rank 0 makes
+    the id with ``unique_id()``; the caller broadcasts it)."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * RT_COMM_ID_BYTES)()
+        _check(lib().rt_comm_unique_id(buf))
+        return bytes(buf)
+
+    def __init__(self, uid: bytes, world: int, rank: int, device: int):
+        buf = (ctypes.c_uint8 * RT_COMM_ID_BYTES)(*uid)
+        self._h = ctypes.c_void_p()
+        _check(lib().rt_comm_create(buf, world, rank, device, ctypes.byref(self._h)))
+
+    def gather_tiles_async(self, width, height, d_share, d_gathered, stream=0):
+        _check(lib().rt_comm_gather_tiles_async(self._h, width, height, ctypes.c_void_p(d_share),
+                                                ctypes.c_void_p(d_gathered), ctypes.c_void_p(stream)))
+
+    def close(self):
+        if self._h:
+            lib().rt_comm_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

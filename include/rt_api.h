@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* status codes */
 #define RT_OK 0
@@ -119,8 +119,9 @@ typedef struct {
   int32_t recursive_reflections; /* SetRecursiveReflections; default 1 */
   int32_t soft_shadows;          /* SetSoftShadows; default 1 */
   int32_t depth_of_field;        /* SetDepthOfField; inert (advanced.go unused) */
-  int32_t num_workers;           /* NewParallelRenderer(n); recorded in benchmark data only */
-  int32_t _pad;
+  int32_t num_workers;           /* NewParallelRenderer(n) (the Go CLI passes runtime.NumCPU(),
+                                    cmd/raytracer/main.go:46); recorded in benchmark data only */
+  int32_t num_devices;           /* rt_render: GPUs 0..n-1 render tiles t % n (0 or 1: device 0 only) */
   uint64_t seed;                 /* counter-based RNG seed (include/rt_rng.h); default 1 */
 } rt_settings;
 
@@ -183,6 +184,31 @@ int rt_scene_print_hittables(const rt_scene_buf* buf);
  * message) when no device is present — there is no CPU fallback. */
 int rt_render(const rt_scene* scene, int32_t width, int32_t height, const rt_settings* settings,
               float* out_linear_rgb, uint8_t* out_rgba, rt_stats* stats);
+/* The argument checks rt_render makes before it touches a device (scene
+ * arrays and kinds; 1 <= W, H <= 65536; samples range): RT_OK or RT_E_INVALID. */
+int rt_validate(const rt_scene* scene, int32_t width, int32_t height, const rt_settings* settings);
+
+/* ------------------------------------------ persistent multi-GPU renderer */
+
+/* The ParallelRenderer object itself (NewParallelRenderer, renderer.go:54-65,
+ * then Render per frame, renderer.go:67-126), on GPUs instead of goroutines.
+ * One process drives `num_devices` ranks; rank r renders the 32x32 tiles
+ * t with t % num_devices == r on devices[r] (devices NULL: 0..n-1).  Ranks
+ * whose device is devices[0] render straight into the gather buffer there;
+ * the others send their packed tiles (float3 + RGBA8, 16 B per pixel) to
+ * devices[0] in ONE RCCL group over xGMI (ncclCommInitAll over the distinct
+ * devices), where one kernel scatters them into the image.  Output is
+ * bit-identical for every device count (the random stream is keyed by
+ * global pixel and sample).  The renderer keeps each device's scene, work
+ * schedule and buffers between calls: a call with the same scene content,
+ * size and settings (any seed) re-uploads nothing.  Not thread-safe (nor is
+ * the Go renderer: renderer.go:103-112). */
+typedef struct rt_renderer rt_renderer;
+int rt_renderer_create(const int32_t* devices, int32_t num_devices, rt_renderer** out);
+/* Render with the renderer's devices (settings->num_devices is ignored). */
+int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t width, int32_t height,
+                       const rt_settings* settings, float* out_linear_rgb, uint8_t* out_rgba, rt_stats* stats);
+void rt_renderer_destroy(rt_renderer* r);
 
 /* ------------------------------------------- resident context (bench/MGPU) */
 
@@ -195,6 +221,34 @@ void rt_context_destroy(rt_context* ctx);
  * upload the scene to device memory.  Builds the BVH when the scene is
  * large (or when force_bvh > 0; force_bvh < 0 forbids it). */
 int rt_context_set_scene(rt_context* ctx, const rt_scene* scene, int32_t force_bvh);
+
+/* Work-partition tuning.  No setting changes a single output bit (the GPU
+ * parity tests render with each and compare against the oracle): they only
+ * choose how the same work is cut into blocks and ordered, and exist for the
+ * tests that force every kind of work block and for experiments.  The
+ * library never reads the environment. */
+#define RT_PATH_AUTO 0        /* wavefront kernels for BVH scenes, else the megakernel */
+#define RT_PATH_MEGAKERNEL 1  /* the megakernel also for BVH scenes */
+typedef struct {
+  int32_t path;           /* RT_PATH_* */
+  int32_t pilot;          /* 1: block sizes from a one-sample pilot render; 0: geometric estimate */
+  int32_t frustum;        /* 1: primary-ray candidate masks (cull, black tiles) */
+  int32_t stage;          /* 1: small scenes staged into LDS */
+  double block_work;      /* path bounces x samples per block; 0: default (512; 8192 with a BVH) */
+  int32_t block_samples;  /* pixels x samples of a large block at most; 0: 1024 */
+  int32_t bvh_bins;       /* SAH bins per axis; 0: 32 */
+  int32_t bvh_leaf;       /* spheres per BVH leaf at most (1..7); 0: 4 */
+  int32_t wf_paths;       /* wavefront path slots; 0: 2^21 */
+  int64_t wf_chunk;       /* wavefront samples per chunk; 0: 2^28 */
+  int32_t wf_lds_nodes;   /* BVH nodes staged into LDS; -1: as many as fit */
+  int32_t wf_trav_block;  /* threads per traversal workgroup (64..1024); 0: 1024 */
+  int32_t wf_trav_wgs;    /* traversal workgroups sharing a CU's LDS; 0: 1 */
+  int32_t _pad;
+} rt_tuning;
+void rt_tuning_default(rt_tuning* t);
+/* Applies to later rt_context_set_scene (BVH shape) and render calls. */
+int rt_context_set_tuning(rt_context* ctx, const rt_tuning* t);
+int rt_renderer_set_tuning(rt_renderer* r, const rt_tuning* t);
 
 #define RT_LAYOUT_IMAGE 0        /* write pixels of this rank's tiles into a W*H image */
 #define RT_LAYOUT_PACKED_TILES 1 /* write this rank's tiles packed: [local_tile][32*32] */
@@ -214,11 +268,37 @@ int rt_context_render_async(rt_context* ctx, int32_t width, int32_t height, cons
                             int32_t rank, int32_t world, int32_t layout, float* d_linear, uint8_t* d_rgba,
                             void* hip_stream, rt_counts* counts);
 
-/* Scatter packed tiles gathered from all ranks, laid out
- * [world][max_local_tiles][1024] (float3 and rgba), into W*H images. */
-int rt_unpack_tiles_async(int32_t width, int32_t height, int32_t world, int32_t max_local_tiles,
-                          const float* d_packed_linear, const uint8_t* d_packed_rgba, float* d_linear,
+/* Packed share of one rank, as rt_comm_gather_tiles_async moves it:
+ * [max_local_tiles * 1024 float3][max_local_tiles * 1024 RGBA8] = 16 B per
+ * pixel of the largest share (rank 0's).  Render a share with layout
+ * RT_LAYOUT_PACKED_TILES, d_linear = share, d_rgba = share + rt_packed_rgba_offset(). */
+int32_t rt_max_local_tiles(int32_t width, int32_t height, int32_t world);
+size_t rt_packed_bytes(int32_t width, int32_t height, int32_t world);
+size_t rt_packed_rgba_offset(int32_t width, int32_t height, int32_t world);
+
+/* Scatter the gathered shares [world][rt_packed_bytes] into W*H images
+ * (d_linear float3 and/or d_rgba; either may be NULL). */
+int rt_unpack_tiles_async(int32_t width, int32_t height, int32_t world, const void* d_gathered, float* d_linear,
                           uint8_t* d_rgba, void* hip_stream);
+
+/* ---------------------------------------------- RCCL tile gather (xGMI) */
+
+/* One communicator per process for multi-process runs (one process per GPU,
+ * e.g. torch.distributed.run): rank 0 makes the id (ncclGetUniqueId), the
+ * caller broadcasts its RT_COMM_ID_BYTES bytes, every rank calls
+ * rt_comm_create (ncclCommInitRank) on its device. */
+#define RT_COMM_ID_BYTES 128
+typedef struct rt_comm rt_comm;
+int rt_comm_unique_id(uint8_t* id);
+int rt_comm_create(const uint8_t* id, int32_t world, int32_t rank, int32_t device, rt_comm** out);
+void rt_comm_destroy(rt_comm* comm);
+/* The frame's one collective: rank r > 0 sends its packed share
+ * (rt_packed_bytes, device pointer d_share) to rank 0, which receives it
+ * into d_gathered + r * rt_packed_bytes (one ncclSend/ncclRecv group on
+ * `hip_stream`).  Rank 0 renders its own share into d_gathered directly
+ * (d_share == d_gathered: nothing to copy). */
+int rt_comm_gather_tiles_async(rt_comm* comm, int32_t width, int32_t height, const void* d_share, void* d_gathered,
+                               void* hip_stream);
 
 /* Debug hook: a device buffer of 32 u64 per workgroup (8 per wave) that
  * RT_WG_TIMING builds of the kernel fill: s_memrealtime at start / loop end

@@ -21,10 +21,8 @@ SPP = int(sys.argv[3]) if len(sys.argv) > 3 else 64
 
 
 def render(mega):
-    os.environ.pop("RTGO_MEGAKERNEL", None)
-    if mega:
-        os.environ["RTGO_MEGAKERNEL"] = "1"
     ctx = rtgo.Context(0)
+    ctx.set_tuning(rtgo.default_tuning(path=rtgo.RT_PATH_MEGAKERNEL if mega else rtgo.RT_PATH_AUTO))
     ctx.set_scene(scene)
     st = rtgo.default_settings()
     st.samples, st.seed = SPP, 1

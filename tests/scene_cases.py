@@ -86,3 +86,13 @@ GOLDEN_CASES = [
     ("all_materials", ("json", None), 48, 32, {"samples": 4}, 7),
     ("all_materials_hard_depth4", ("json", None), 40, 24, {"samples": 2, "soft_shadows": 0, "max_depth": 4}, 2),
 ]
+
+
+def spheres10k_scene(rtgo, n=10000):
+    """The procedural C4/C5 scene (scenes/gen_spheres.py, SHA-256 pinned)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("gen_spheres", scene_path("gen_spheres.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    return rtgo.Scene.from_json_text(g.dumps(g.generate(n)))

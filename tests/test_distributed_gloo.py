@@ -2,7 +2,8 @@
 
 Each rank renders only its tiles (t % world == rank) with the
 oracle, packs them in the packed-tile layout, and the ranks run the same
-single gather bench.py uses on RCCL (rtgo.shard.gather_packed).  Rank 0
+single equal-size gather of packed shares that bench.py runs on RCCL
+(rt_comm_gather_tiles_async; here rtgo.shard.gather_packed over gloo).  Rank 0
 unpacks and must obtain exactly the 1-rank image: the stream is keyed by
 global pixel and sample, never by rank or tile."""
 import os
@@ -42,21 +43,16 @@ def _worker(rank, world, port, outdir):
         scene = load_case(rtgo, ("json", None))
         st = make_settings(rtgo, {"samples": SPP}, seed=5)
         lin, rgba, counts = oracle.render(scene, W, H, st, rank=rank, world=world, nthreads=2, counts=True)
-        lin32 = lin.astype(np.float32)
-        p_lin = torch.from_numpy(np.ascontiguousarray(shard.pack_host(np.nan_to_num(lin32, nan=0.0), rank,
-                                                                      world)).ravel())
-        p_rgba = torch.from_numpy(np.ascontiguousarray(shard.pack_host(rgba, rank, world)).ravel())
-        n = shard.max_local_tiles(W, H, world) * 1024
-        g_lin = torch.empty(world * n * 3, dtype=torch.float32) if rank == 0 else None
-        g_rgba = torch.empty(world * n * 4, dtype=torch.uint8) if rank == 0 else None
-        g_lin = shard.gather_packed(dist, p_lin, world, rank, g_lin)
-        g_rgba = shard.gather_packed(dist, p_rgba, world, rank, g_rgba)
+        lin32 = np.nan_to_num(lin.astype(np.float32), nan=0.0)
+        share = torch.from_numpy(shard.pack_share_host(lin32, rgba, rank, world))
+        nb = rtgo.packed_bytes(W, H, world)
+        g = torch.empty(world * nb, dtype=torch.uint8) if rank == 0 else None
+        g = shard.gather_packed(dist, share, world, rank, g)
         # per-rank work sums to the whole frame (weak-scaling accounting in bench.py)
         cam = torch.tensor([counts["camera_rays"]], dtype=torch.int64)
         dist.all_reduce(cam)
         if rank == 0:
-            img = shard.unpack_host(g_lin.numpy().reshape(-1, 3), W, H, world)
-            img_rgba = shard.unpack_host(g_rgba.numpy().reshape(-1, 4), W, H, world)
+            img, img_rgba = shard.unpack_shares_host(g.numpy(), W, H, world)
             np.savez(os.path.join(outdir, "r0.npz"), lin=img, rgba=img_rgba, cam=cam.numpy())
     finally:
         dist.destroy_process_group()
@@ -91,7 +87,10 @@ def test_packed_index_covers_every_pixel_once():
 def test_pack_unpack_roundtrip():
     from rtgo import shard
 
-    img = np.random.default_rng(0).random((41, 75, 3)).astype(np.float32)
+    rng = np.random.default_rng(0)
+    img = rng.random((41, 75, 3)).astype(np.float32)
+    rgba = rng.integers(0, 256, (41, 75, 4), dtype=np.uint8)
     for world in (1, 2, 5):
-        g = np.concatenate([shard.pack_host(img, r, world) for r in range(world)])
-        assert np.array_equal(shard.unpack_host(g, 75, 41, world), img)
+        g = np.concatenate([shard.pack_share_host(img, rgba, r, world) for r in range(world)])
+        lin2, rgba2 = shard.unpack_shares_host(g, 75, 41, world)
+        assert np.array_equal(lin2, img) and np.array_equal(rgba2, rgba)

@@ -1,0 +1,90 @@
+"""GPU: configs C4 and C5 (10k procedural spheres, the BVH + wavefront path)
+at their FULL size, against the linear-scan oracle on a sample of tiles.
+
+The oracle cannot render a whole 10k-sphere frame (~10^13 sphere tests), but
+it renders single 32x32 tiles at full spp and depth 50, and the random
+stream is keyed by global (pixel, sample), so its tile is the tile of the
+full frame.  tests/golden/make_bvh_tiles.py chose the tiles with the most
+bounces in a 1-spp oracle survey (tests/golden/survey_c4.json, survey_c5.json)
+and rendered them: tests/golden/oracle_c4_tiles.npz, oracle_c5_tiles.npz.
+
+- C4 (BASELINE configs[3], 1920x1080x64): the whole frame in one launch
+  sequence; the 4 heaviest surveyed tiles equal the oracle's bit for bit,
+  and each tile's path counts equal the oracle's.
+- C5 (configs[4], 3840x2160x256 over 8 GPUs): the packed shares of ranks 0
+  and 7 of 8 (exactly what those GPUs render); their 2 heaviest surveyed
+  tiles each equal the oracle's bit for bit.
+Tolerance (north star): per-channel RMSE < 1e-4; asserted: max |diff| == 0.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import rtgo
+from conftest import GOLDEN
+from gpu_util import render_dev
+from scene_cases import make_settings, spheres10k_scene
+
+pytestmark = pytest.mark.gpu
+
+PATH_KEYS = ("camera_rays", "bounce_rays", "shadow_rays", "shade_events", "light_evals", "rng_draws")
+
+
+def _fixture(name):
+    g = np.load(os.path.join(GOLDEN, f"oracle_{name}_tiles.npz"))
+    w, h, spp, depth, seed = (int(v) for v in g["config"])
+    return g, w, h, make_settings(rtgo, {"samples": spp, "max_depth": depth}, seed=seed)
+
+
+def _tile_of_image(img, w, t):
+    tx_n = (w + 31) // 32
+    x0, y0 = (t % tx_n) * 32, (t // tx_n) * 32
+    return img[y0:y0 + 32, x0:x0 + 32]
+
+
+def test_c4_full_frame_tiles_match_oracle():
+    g, w, h, st = _fixture("c4")
+    scene = spheres10k_scene(rtgo)
+    lin, rgba, _, _ = render_dev(scene, w, h, st)
+    lin, rgba = lin.reshape(h, w, 3), rgba.reshape(h, w, 4)
+    assert not np.isnan(lin).any()
+    for i, t in enumerate(g["tiles"]):
+        a = _tile_of_image(lin, w, int(t))
+        ref = g["linear"][i]
+        rmse = np.sqrt(np.mean((a.astype(np.float64) - ref) ** 2, axis=(0, 1)))
+        print(f"C4 tile {t}: rmse {rmse}, max |d| {np.abs(a - ref).max():.3e}")
+        assert a.tobytes() == ref.tobytes(), f"tile {t}"
+        assert _tile_of_image(rgba, w, int(t)).tobytes() == g["rgba"][i].tobytes(), f"tile {t}"
+
+
+def test_c4_tile_path_counts_match_oracle():
+    """Each fixture tile alone (rank t of world = #tiles): the wavefront
+    path's path counts equal the oracle's (camera, bounce and shadow rays,
+    shading events, light evaluations, RNG draws)."""
+    g, w, h, st = _fixture("c4")
+    scene = spheres10k_scene(rtgo)
+    n = rtgo.num_tiles(w, h)
+    for i, t in enumerate(g["tiles"]):
+        _, _, _, c = render_dev(scene, w, h, st, rank=int(t), world=n, count=True)
+        want = dict(zip(rtgo.COUNT_FIELDS, (int(v) for v in g["counts"][i])))
+        assert {k: c[k] for k in PATH_KEYS} == {k: want[k] for k in PATH_KEYS}, f"tile {t}"
+
+
+@pytest.mark.parametrize("rank", [0, 7])
+def test_c5_rank_shares_match_oracle(rank):
+    g, w, h, st = _fixture("c5")
+    world = 8
+    scene = spheres10k_scene(rtgo)
+    lin, rgba, _, _ = render_dev(scene, w, h, st, rank=rank, world=world)
+    local = rtgo.tiles_for_rank(w, h, rank, world)
+    assert not np.isnan(lin[:local * 1024]).any()
+    mine = [(i, int(t)) for i, t in enumerate(g["tiles"]) if int(t) % world == rank]
+    assert len(mine) == 2
+    for i, t in mine:
+        lt = t // world
+        a = lin[lt * 1024:(lt + 1) * 1024].reshape(32, 32, 3)
+        ref = g["linear"][i]
+        print(f"C5 rank {rank} tile {t}: max |d| {np.abs(a - ref).max():.3e}")
+        assert a.tobytes() == ref.tobytes(), f"tile {t}"
+        assert rgba[lt * 1024:(lt + 1) * 1024].reshape(32, 32, 4).tobytes() == g["rgba"][i].tobytes()

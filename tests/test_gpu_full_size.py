@@ -12,56 +12,22 @@
   smaller frames), bit for bit, plus a 2-rank sharding of the same frame.
 Tolerance (north star): per-channel RMSE < 1e-4; asserted: max |diff| == 0.
 """
-import importlib.util
-import os
-
 import numpy as np
 import pytest
 
 import oracle
 import rtgo
-from rtgo import shard
-from scene_cases import make_settings, scene_path
+from gpu_util import render_dev, unpack_dev
+from scene_cases import make_settings, scene_path, spheres10k_scene
 
 pytestmark = pytest.mark.gpu
 
 RMSE_TOL = 1e-4
 
 
-def _render(scene, w, h, st, rank=0, world=1, env=None, monkeypatch=None):
-    import torch
-
-    if env:
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-    ctx = rtgo.Context(0)
-    ctx.set_scene(scene)
-    packed = world > 1
-    n = shard.max_local_tiles(w, h, world) * 1024 if packed else w * h
-    lin = torch.full((n * 3,), float("nan"), dtype=torch.float32, device="cuda")
-    rgba = torch.zeros(n * 4, dtype=torch.uint8, device="cuda")
-    layout = rtgo.RT_LAYOUT_PACKED_TILES if packed else rtgo.RT_LAYOUT_IMAGE
-    ctx.render_async(w, h, st, lin.data_ptr(), rgba.data_ptr(), 0, rank, world, layout)
-    torch.cuda.synchronize()
-    ctx.close()
-    if env:
-        for k in env:
-            monkeypatch.delenv(k)
-    return lin, rgba
-
-
-def _unpack(w, h, world, parts):
-    import torch
-
-    ml = shard.max_local_tiles(w, h, world)
-    g_lin = torch.cat([p[0] for p in parts])
-    g_rgba = torch.cat([p[1] for p in parts])
-    img_lin = torch.full((h * w * 3,), float("nan"), dtype=torch.float32, device="cuda")
-    img_rgba = torch.zeros(h * w * 4, dtype=torch.uint8, device="cuda")
-    rtgo.unpack_tiles_async(w, h, world, ml, g_lin.data_ptr(), g_rgba.data_ptr(), img_lin.data_ptr(),
-                            img_rgba.data_ptr(), 0)
-    torch.cuda.synchronize()
-    return img_lin, img_rgba
+def _render(scene, w, h, st, rank=0, world=1, tuning=None):
+    lin, rgba, share, _ = render_dev(scene, w, h, st, rank=rank, world=world, tuning=tuning)
+    return share if world > 1 else (lin, rgba)
 
 
 @pytest.mark.parametrize("name,w,h", [("sphere_reflections_light_facing.json", 800, 600),
@@ -73,13 +39,13 @@ def test_full_frame_matches_oracle(name, w, h):
     st = make_settings(rtgo, {"samples": 100}, seed=1)
     lin, rgba = _render(scene, w, h, st)
     ref, ref_rgba, _ = oracle.render(scene, w, h, st)
-    g = lin.cpu().numpy().reshape(h, w, 3).astype(np.float64)
+    g = lin.reshape(h, w, 3).astype(np.float64)
     r32 = ref.astype(np.float32).astype(np.float64)
     rmse = np.sqrt(np.mean((g - r32) ** 2, axis=(0, 1)))
     print(f"{name} {w}x{h}x100: rmse {rmse}, max |d| {np.abs(g - r32).max():.3e}")
     assert np.all(rmse < RMSE_TOL)
     assert g.tobytes() == r32.tobytes()
-    assert rgba.cpu().numpy().reshape(h, w, 4).tobytes() == ref_rgba.tobytes()
+    assert rgba.reshape(h, w, 4).tobytes() == ref_rgba.tobytes()
 
 
 def test_weak_scaling_frame_of_eight_ranks_equals_one():
@@ -90,45 +56,36 @@ def test_weak_scaling_frame_of_eight_ranks_equals_one():
     st = make_settings(rtgo, {"samples": 100}, seed=1)
     w, h, world = 800, 600 * 8, 8
     one_lin, one_rgba = _render(scene, w, h, st)
-    parts = [_render(scene, w, h, st, rank=r, world=world) for r in range(world)]
-    img_lin, img_rgba = _unpack(w, h, world, parts)
-    assert img_lin.cpu().numpy().tobytes() == one_lin.cpu().numpy().tobytes()
-    assert img_rgba.cpu().numpy().tobytes() == one_rgba.cpu().numpy().tobytes()
+    shares = [_render(scene, w, h, st, rank=r, world=world) for r in range(world)]
+    img_lin, img_rgba = unpack_dev(w, h, world, shares)
+    assert img_lin.tobytes() == one_lin.tobytes()
+    assert img_rgba.tobytes() == one_rgba.tobytes()
 
 
-def _spheres10k():
-    spec = importlib.util.spec_from_file_location(
-        "gen_spheres", os.path.join(os.path.dirname(scene_path("x")), "gen_spheres.py"))
-    g = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(g)
-    return rtgo.Scene.from_json_text(g.dumps(g.generate(10000)))
-
-
-def test_c4_full_frame_wavefront_equals_megakernel_and_two_ranks(monkeypatch):
-    scene = _spheres10k()
+def test_c4_full_frame_wavefront_equals_megakernel_and_two_ranks():
+    scene = spheres10k_scene(rtgo)
     st = make_settings(rtgo, {"samples": 64}, seed=1)
     w, h = 1920, 1080
     wf_lin, wf_rgba = _render(scene, w, h, st)
-    mk_lin, mk_rgba = _render(scene, w, h, st, env={"RTGO_MEGAKERNEL": "1"}, monkeypatch=monkeypatch)
-    a = wf_lin.cpu().numpy()
-    assert not np.isnan(a).any()
-    assert a.tobytes() == mk_lin.cpu().numpy().tobytes()
-    assert wf_rgba.cpu().numpy().tobytes() == mk_rgba.cpu().numpy().tobytes()
-    parts = [_render(scene, w, h, st, rank=r, world=2) for r in range(2)]
-    img_lin, img_rgba = _unpack(w, h, 2, parts)
-    assert img_lin.cpu().numpy().tobytes() == a.tobytes()
-    assert img_rgba.cpu().numpy().tobytes() == wf_rgba.cpu().numpy().tobytes()
+    mk_lin, mk_rgba = _render(scene, w, h, st, tuning=rtgo.default_tuning(path=rtgo.RT_PATH_MEGAKERNEL))
+    assert not np.isnan(wf_lin).any()
+    assert wf_lin.tobytes() == mk_lin.tobytes()
+    assert wf_rgba.tobytes() == mk_rgba.tobytes()
+    shares = [_render(scene, w, h, st, rank=r, world=2) for r in range(2)]
+    img_lin, img_rgba = unpack_dev(w, h, 2, shares)
+    assert img_lin.tobytes() == wf_lin.tobytes()
+    assert img_rgba.tobytes() == wf_rgba.tobytes()
 
 
-def test_wavefront_is_deterministic():
+@pytest.mark.parametrize("w,h,spp,seed", [(960, 540, 32, 3), (1920, 1080, 64, 11)], ids=["960x540x32_s3", "C4_s11"])
+def test_wavefront_is_deterministic(w, h, spp, seed):
     """Two renders of a 10k-sphere frame through the wavefront path are
     byte-identical (paths are re-packed by atomics every bounce, so a race or
     a lost queue entry shows up as run-to-run noise; a miscompiled pointer
     increment in wf_softgen once did, rt_wavefront.hip)."""
-    scene = _spheres10k()
-    st = make_settings(rtgo, {"samples": 32}, seed=3)
-    w, h = 960, 540
+    scene = spheres10k_scene(rtgo)
+    st = make_settings(rtgo, {"samples": spp}, seed=seed)
     a = _render(scene, w, h, st)
     b = _render(scene, w, h, st)
-    assert a[0].cpu().numpy().tobytes() == b[0].cpu().numpy().tobytes()
-    assert a[1].cpu().numpy().tobytes() == b[1].cpu().numpy().tobytes()
+    assert a[0].tobytes() == b[0].tobytes()
+    assert a[1].tobytes() == b[1].tobytes()

@@ -18,8 +18,9 @@ import pytest
 import oracle
 import rtgo
 from conftest import GOLDEN, ROOT
+from gpu_util import render_dev, unpack_dev
 from rtgo import shard
-from scene_cases import GOLDEN_CASES, load_case, make_settings
+from scene_cases import GOLDEN_CASES, load_case, make_settings, spheres10k_scene
 
 pytestmark = pytest.mark.gpu
 
@@ -44,33 +45,70 @@ def test_kernel_reproduces_committed_fixture(case):
 
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_packed_tiles_and_unpack_reassemble_the_image(world):
-    import torch
-
     scene = load_case(rtgo, ("json", None))
     st = make_settings(rtgo, {"samples": 3})
     w, h = 75, 50
     ref_lin, ref_rgba = _gpu(scene, w, h, st)
-    ctx = rtgo.Context(0)
-    ctx.set_scene(scene)
-    ml = shard.max_local_tiles(w, h, world)
-    g_lin = torch.zeros(world * ml * 1024 * 3, dtype=torch.float32, device="cuda")
-    g_rgba = torch.zeros(world * ml * 1024 * 4, dtype=torch.uint8, device="cuda")
+    shares = [render_dev(scene, w, h, st, rank=r, world=world)[2] for r in range(world)]
+    img_lin, img_rgba = unpack_dev(w, h, world, shares)
+    assert img_lin.tobytes() == ref_lin.tobytes()
+    assert img_rgba.tobytes() == ref_rgba.tobytes()
+    # the packed layout is exactly rtgo.shard's (the gloo CPU test relies on it):
+    # compare the RGBA8 half and the non-padding float3 slots
     for r in range(world):
-        pl = g_lin[r * ml * 1024 * 3:(r + 1) * ml * 1024 * 3]
-        pr = g_rgba[r * ml * 1024 * 4:(r + 1) * ml * 1024 * 4]
-        ctx.render_async(w, h, st, pl.data_ptr(), pr.data_ptr(), 0, r, world, rtgo.RT_LAYOUT_PACKED_TILES)
-    img_lin = torch.full((h * w * 3,), float("nan"), dtype=torch.float32, device="cuda")
-    img_rgba = torch.zeros(h * w * 4, dtype=torch.uint8, device="cuda")
-    rtgo.unpack_tiles_async(w, h, world, ml, g_lin.data_ptr(), g_rgba.data_ptr(), img_lin.data_ptr(),
-                            img_rgba.data_ptr(), 0)
+        want = shard.pack_share_host(ref_lin, ref_rgba, r, world)
+        off = rtgo.packed_rgba_offset(w, h, world)
+        assert np.array_equal(shares[r][off:], want[off:])
+        ok = shard.packed_index(w, h, r, world) >= 0
+        assert shares[r][:off].view(np.float32).reshape(-1, 3)[ok].tobytes() == \
+            want[:off].view(np.float32).reshape(-1, 3)[ok].tobytes()
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]], ids=["1_device", "3_ranks_on_device_0"])
+def test_renderer_multi_rank_equals_one_rank(devices):
+    """rt_renderer_render (the persistent renderer of the C ABI) with several
+    ranks on device 0: every rank renders its share straight into the gather
+    buffer, one kernel unpacks; the image equals the 1-rank image, and a
+    second call (same scene, new seed) equals a fresh renderer's."""
+    scene = load_case(rtgo, ("json", None))
+    st = make_settings(rtgo, {"samples": 3}, seed=9)
+    w, h = 75, 50
+    ref_lin, ref_rgba = _gpu(scene, w, h, st)
+    r = rtgo.ParallelRenderer(devices=devices)
+    st.num_devices = len(devices)
+    r.settings = st
+    rgba = r.render(scene, w, h)
+    assert r.last_linear.tobytes() == ref_lin.tobytes()
+    assert rgba.tobytes() == ref_rgba.tobytes()
+    st2 = make_settings(rtgo, {"samples": 3}, seed=10)
+    r.settings.seed = 10
+    rgba2 = r.render(scene, w, h)
+    lin2 = r.last_linear.copy()
+    ref2_lin, ref2_rgba = _gpu(scene, w, h, st2)
+    assert lin2.tobytes() == ref2_lin.tobytes()
+    assert rgba2.tobytes() == ref2_rgba.tobytes()
+    r.close()
+
+
+def test_comm_of_one_rank_and_one_shot_render():
+    """rt_comm over one rank (ncclCommInitRank, world 1: the gather moves
+    nothing) and the one-shot rt_render with num_devices = 1."""
+    import torch
+
+    uid = rtgo.Comm.unique_id()
+    assert len(uid) == rtgo.RT_COMM_ID_BYTES
+    c = rtgo.Comm(uid, 1, 0, 0)
+    buf = torch.zeros(rtgo.packed_bytes(64, 64, 1), dtype=torch.uint8, device="cuda")
+    c.gather_tiles_async(64, 64, buf.data_ptr(), buf.data_ptr(), 0)
     torch.cuda.synchronize()
-    assert img_lin.cpu().numpy().reshape(h, w, 3).tobytes() == ref_lin.tobytes()
-    assert img_rgba.cpu().numpy().reshape(h, w, 4).tobytes() == ref_rgba.tobytes()
-    # the packed layout is exactly rtgo.shard's (the gloo CPU test relies on it)
-    packed = g_rgba.cpu().numpy().reshape(world * ml * 1024, 4)
-    want = np.concatenate([shard.pack_host(ref_rgba, r, world) for r in range(world)])
-    assert np.array_equal(packed, want)
-    ctx.close()
+    c.close()
+    scene = load_case(rtgo, ("json", None))
+    st = make_settings(rtgo, {"samples": 2}, seed=3)
+    rgba, lin, stats = rtgo.render(scene, 40, 30, st)
+    ref, ref_rgba, _ = oracle.render(scene, 40, 30, st)
+    assert lin.tobytes() == ref.astype(np.float32).tobytes()
+    assert rgba.tobytes() == ref_rgba.tobytes()
+    assert stats.render_seconds >= stats.kernel_seconds > 0
 
 
 def _sphere_field(n, seed=42):
@@ -101,20 +139,9 @@ def test_bvh_matches_linear_oracle():
 
 
 def test_forced_bvh_equals_linear_scan_on_gpu():
-    import torch
-
     scene = rtgo.Scene.from_json_text(json.dumps(_sphere_field(40, seed=3)))
     st = make_settings(rtgo, {"samples": 2})
-    outs = []
-    for force in (-1, 1):  # -1: never BVH, 1: always
-        ctx = rtgo.Context(0)
-        ctx.set_scene(scene, force_bvh=force)
-        lin = torch.zeros(48 * 32 * 3, dtype=torch.float32, device="cuda")
-        rgba = torch.zeros(48 * 32 * 4, dtype=torch.uint8, device="cuda")
-        ctx.render_async(48, 32, st, lin.data_ptr(), rgba.data_ptr())
-        torch.cuda.synchronize()
-        outs.append(lin.cpu().numpy())
-        ctx.close()
+    outs = [render_dev(scene, 48, 32, st, force_bvh=force)[0] for force in (-1, 1)]  # -1: never BVH, 1: always
     assert outs[0].tobytes() == outs[1].tobytes()
 
 
@@ -155,12 +182,7 @@ def test_cli_writes_png_and_benchmark_data(tmp_path):
 def test_ten_thousand_sphere_field_matches_oracle():
     """Config C4's scene (scenes/gen_spheres.py, 10k spheres: the BVH path)
     at a size the linear-scan oracle finishes in seconds."""
-    import importlib.util
-
-    spec = importlib.util.spec_from_file_location("gen_spheres", os.path.join(ROOT, "scenes", "gen_spheres.py"))
-    g = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(g)
-    scene = rtgo.Scene.from_json_text(g.dumps(g.generate(10000)))
+    scene = spheres10k_scene(rtgo)
     st = make_settings(rtgo, {"samples": 2, "max_depth": 4})
     lin, rgba = _gpu(scene, 32, 18, st)
     ref, ref_rgba, _ = oracle.render(scene, 32, 18, st)

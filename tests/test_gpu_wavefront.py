@@ -16,6 +16,7 @@ import pytest
 import oracle
 import rtgo
 from scene_cases import ALL_MATERIALS, make_settings
+from gpu_util import render_dev
 from test_gpu_paths import _sphere_field
 
 pytestmark = pytest.mark.gpu
@@ -31,33 +32,12 @@ def _spheres_only_all_materials():
     return s
 
 
-def _render(scene, w, h, st, monkeypatch, mega, force_bvh=0, rank=0, world=1, env=None, count=False):
-    import torch
-
-    monkeypatch.delenv("RTGO_MEGAKERNEL", raising=False)
-    if mega:
-        monkeypatch.setenv("RTGO_MEGAKERNEL", "1")
-    for k, v in (env or {}).items():
-        monkeypatch.setenv(k, v)
-    ctx = rtgo.Context(0)
-    ctx.set_scene(scene, force_bvh=force_bvh)
-    packed = world > 1
-    n = rtgo.tiles_for_rank(w, h, rank, world) * 1024 if packed else w * h
-    lin = torch.full((n * 3,), float("nan"), dtype=torch.float32, device="cuda")
-    rgba = torch.zeros(n * 4, dtype=torch.uint8, device="cuda")
-    layout = rtgo.RT_LAYOUT_PACKED_TILES if packed else rtgo.RT_LAYOUT_IMAGE
-    counts = None
-    if count:
-        counts = ctx.count(w, h, st, lin.data_ptr(), rgba.data_ptr(), 0, rank, world, layout)
-    else:
-        ctx.render_async(w, h, st, lin.data_ptr(), rgba.data_ptr(), 0, rank, world, layout)
-    torch.cuda.synchronize()
-    out = lin.cpu().numpy(), rgba.cpu().numpy(), counts
-    ctx.close()
-    for k in (env or {}):
-        monkeypatch.delenv(k)
-    monkeypatch.delenv("RTGO_MEGAKERNEL", raising=False)
-    return out
+def _render(scene, w, h, st, mega, force_bvh=0, rank=0, world=1, tuning=None, count=False):
+    t = tuning or rtgo.default_tuning()
+    t.path = rtgo.RT_PATH_MEGAKERNEL if mega else rtgo.RT_PATH_AUTO
+    lin, rgba, _, counts = render_dev(scene, w, h, st, rank=rank, world=world, tuning=t, force_bvh=force_bvh,
+                                      count=count)
+    return lin, rgba, counts
 
 
 SETTINGS = [
@@ -71,12 +51,12 @@ SETTINGS = [
 
 
 @pytest.mark.parametrize("name,over", SETTINGS, ids=[s[0] for s in SETTINGS])
-def test_wavefront_equals_megakernel(name, over, monkeypatch):
+def test_wavefront_equals_megakernel(name, over):
     scene = rtgo.Scene.from_json_text(json.dumps(_sphere_field(300, seed=5)))
     st = make_settings(rtgo, over)
     w, h = 72, 40
-    lw, rw, cw = _render(scene, w, h, st, monkeypatch, mega=False, count=True)
-    lm, rm, cm = _render(scene, w, h, st, monkeypatch, mega=True, count=True)
+    lw, rw, cw = _render(scene, w, h, st, mega=False, count=True)
+    lm, rm, cm = _render(scene, w, h, st, mega=True, count=True)
     assert lw.tobytes() == lm.tobytes()
     assert rw.tobytes() == rm.tobytes()
     assert {k: cw[k] for k in PATH_KEYS} == {k: cm[k] for k in PATH_KEYS}
@@ -84,37 +64,56 @@ def test_wavefront_equals_megakernel(name, over, monkeypatch):
         assert cw["shade_events"] > 0
 
 
-def test_wavefront_all_sphere_materials_matches_oracle(monkeypatch):
+def test_wavefront_all_sphere_materials_matches_oracle():
     """Every sphere material (incl. dielectric, shiny, mirror, light) through
     the forced BVH + wavefront path, against the oracle's linear scan."""
     scene = rtgo.Scene.from_json_text(json.dumps(_spheres_only_all_materials()))
     st = make_settings(rtgo, {"samples": 6})
-    lin, rgba, _ = _render(scene, 60, 40, st, monkeypatch, mega=False, force_bvh=1)
+    lin, rgba, _ = _render(scene, 60, 40, st, mega=False, force_bvh=1)
     ref, ref_rgba, _ = oracle.render(scene, 60, 40, st)
     assert lin.reshape(40, 60, 3).tobytes() == ref.astype(np.float32).tobytes()
     assert rgba.reshape(40, 60, 4).tobytes() == ref_rgba.tobytes()
 
 
-@pytest.mark.parametrize("env", [{"RTGO_WF_PATHS": "64"}, {"RTGO_WF_PATHS": "4096"},
-                                 {"RTGO_WF_CHUNK": "700"}, {"RTGO_WF_PATHS": "128", "RTGO_WF_CHUNK": "3000"},
-                                 {"RTGO_WF_LDS_NODES": "0"}, {"RTGO_WF_LDS_NODES": "31"}],
-                         ids=["64_paths", "4096_paths", "chunks", "both", "bvh_all_global", "bvh_top_in_lds"])
-def test_capacity_and_chunks_do_not_change_the_image(env, monkeypatch):
+@pytest.mark.parametrize("tun", [{"wf_paths": 64}, {"wf_paths": 4096}, {"wf_chunk": 700},
+                                 {"wf_paths": 128, "wf_chunk": 3000}, {"wf_lds_nodes": 0}, {"wf_lds_nodes": 31},
+                                 {"wf_trav_block": 256, "wf_trav_wgs": 4}, {"bvh_leaf": 1}, {"bvh_leaf": 7, "bvh_bins": 4}],
+                         ids=["64_paths", "4096_paths", "chunks", "both", "bvh_all_global", "bvh_top_in_lds",
+                              "small_traversal_groups", "leaf1", "leaf7_bins4"])
+def test_capacity_and_chunks_do_not_change_the_image(tun):
     """... nor how much of the BVH the traversal kernels stage in LDS (by
     default all of it; here none, or only the top 31 nodes)."""
     scene = rtgo.Scene.from_json_text(json.dumps(_sphere_field(200, seed=9)))
     st = make_settings(rtgo, {"samples": 7})
-    base = _render(scene, 50, 37, st, monkeypatch, mega=False)
-    other = _render(scene, 50, 37, st, monkeypatch, mega=False, env=env)
+    base = _render(scene, 50, 37, st, mega=False)
+    other = _render(scene, 50, 37, st, mega=False, tuning=rtgo.default_tuning(**tun))
     assert base[0].tobytes() == other[0].tobytes()
     assert base[1].tobytes() == other[1].tobytes()
 
 
 @pytest.mark.parametrize("rank,world", [(0, 3), (2, 3)])
-def test_wavefront_packed_tiles_equal_megakernel(rank, world, monkeypatch):
+def test_wavefront_packed_tiles_equal_megakernel(rank, world):
     scene = rtgo.Scene.from_json_text(json.dumps(_sphere_field(150, seed=2)))
     st = make_settings(rtgo, {"samples": 3})
-    a = _render(scene, 100, 70, st, monkeypatch, mega=False, rank=rank, world=world)
-    b = _render(scene, 100, 70, st, monkeypatch, mega=True, rank=rank, world=world)
+    a = _render(scene, 100, 70, st, mega=False, rank=rank, world=world)
+    b = _render(scene, 100, 70, st, mega=True, rank=rank, world=world)
     assert a[0].tobytes() == b[0].tobytes()
     assert a[1].tobytes() == b[1].tobytes()
+
+
+def test_more_than_32_lights_match_the_oracle():
+    """The wavefront kernels keep per-light state in 32-light chunks: a
+    BVH scene (> 64 spheres) with 40 lights equals the oracle's linear scan,
+    which loops over the lights with no limit (renderer.go:248-294)."""
+    field = _sphere_field(80, seed=13)
+    rng = np.random.default_rng(4)
+    field["lights"] = [{"position": [float(v) for v in rng.uniform(-15, 15, 3)], "color": [1, 1, 1],
+                        "intensity": float(rng.uniform(20, 200))} for _ in range(40)]
+    scene = rtgo.Scene.from_json_text(json.dumps(field))
+    st = make_settings(rtgo, {"samples": 2, "max_depth": 5})
+    lin, rgba, _ = _render(scene, 40, 24, st, mega=False)
+    ref, ref_rgba, _ = oracle.render(scene, 40, 24, st)
+    assert lin.reshape(24, 40, 3).tobytes() == ref.astype(np.float32).tobytes()
+    assert rgba.reshape(24, 40, 4).tobytes() == ref_rgba.tobytes()
+    mk = _render(scene, 40, 24, st, mega=True)
+    assert mk[0].tobytes() == lin.tobytes()
