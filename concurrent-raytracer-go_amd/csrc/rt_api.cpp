@@ -320,21 +320,22 @@ struct rt_context {
   hipStream_t last_stream = nullptr;
   bool have_timing = false;
   unsigned long long* dbg = nullptr;
-  // tile dispatch order (schedule.cpp), cached per (scene, W, H, rank, world)
+  // the work schedule (rt_schedule.hip), cached per (scene, W, H, rank, world, settings)
   uint64_t scene_gen = 0;
   int64_t order_key[13] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
-  std::vector<int32_t> order_host;   // local tiles by projected-primitive count (fallback estimate)
-  std::vector<int32_t> blocks_host;  // work blocks, kBlockInts ints each (schedule.cpp build_blocks)
-  int32_t* d_blocks = nullptr;
-  size_t d_blocks_cap = 0;
+  int32_t* d_blocks = nullptr;  // work blocks, kBlockInts ints each, heaviest first
+  size_t d_blocks_cap = 0;  // bytes
+  int32_t num_blocks = 0;
   int32_t nsplit = 0;       // split pixels of the current schedule
-  void* d_split = nullptr;  // their per-sample radiance rows + sub-block counters
+  char* d_split = nullptr;  // their per-sample radiance rows + sub-block counters
   size_t split_cap = 0;
-  void* d_pilot = nullptr;  // pilot render scratch: packed float3 + rgba + per-tile work
-  size_t pilot_cap = 0;     // pixels
+  char* d_pilot = nullptr;  // pilot render scratch: packed float3 + rgba + path lengths
+  size_t pilot_cap = 0;
+  char* d_sched = nullptr;  // scheduler scratch (sched_layout) + the per-tile inputs
+  size_t sched_cap = 0;
+  int32_t* h_totals = nullptr;  // pinned: block and split counts of the last schedule
   std::vector<unsigned long long> masks_host;  // per local tile primary-ray masks
-  unsigned long long* d_masks = nullptr;
-  size_t d_masks_cap = 0;
+  unsigned long long* d_masks = nullptr;       // (inside d_sched)
   int32_t stage_bytes = 0;  // scene prefix staged into LDS per workgroup (0 = none)
   // wavefront path (BVH scenes): path arrays + queues, per-chunk radiance, loop control
   void* wf_mem = nullptr;
@@ -356,6 +357,11 @@ void rt_tuning_default(rt_tuning* t) {
   t->frustum = 1;
   t->stage = 1;
   t->wf_lds_nodes = -1;
+  // a pilot path is followed for 12 bounces at most: every longer path is
+  // "heavy" alike (split, dispatched first), and the pilot's own tail is one
+  // 12-bounce path instead of a 50-bounce one (C2 first frame 1.39 -> 1.07 ms,
+  // the main launch unchanged; scripts/first_frame_probe.py)
+  t->pilot_depth = 12;
 }
 
 int rt_context_set_tuning(rt_context* c, const rt_tuning* t) {
@@ -367,7 +373,7 @@ int rt_context_set_tuning(rt_context* c, const rt_tuning* t) {
     set_error("tuning.path must be RT_PATH_AUTO or RT_PATH_MEGAKERNEL");
     return RT_E_INVALID;
   }
-  if (t->bvh_leaf < 0 || t->bvh_leaf > 7 || t->bvh_bins < 0 || t->block_work < 0 || t->block_samples < 0 ||
+  if (t->pilot_depth < 0 || t->bvh_leaf < 0 || t->bvh_leaf > 7 || t->bvh_bins < 0 || t->block_work < 0 || t->block_samples < 0 ||
       t->wf_paths < 0 || t->wf_chunk < 0 || t->wf_trav_block < 0 || t->wf_trav_block > 1024 || t->wf_trav_wgs < 0) {
     set_error("tuning value out of range");
     return RT_E_INVALID;
@@ -433,6 +439,7 @@ int rt_context_create(int32_t device, rt_context** out) {
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_counts, 16 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_totals, 4 * sizeof(int32_t), hipHostMallocDefault);
 
   if (e != hipSuccess) {
     set_error(std::string("context init failed: ") + hipGetErrorString(e));
@@ -453,7 +460,8 @@ void rt_context_destroy(rt_context* c) {
   if (c->d_blocks) (void)hipFree(c->d_blocks);
   if (c->d_pilot) (void)hipFree(c->d_pilot);
   if (c->d_split) (void)hipFree(c->d_split);
-  if (c->d_masks) (void)hipFree(c->d_masks);
+  if (c->d_sched) (void)hipFree(c->d_sched);
+  if (c->h_totals) (void)hipHostFree(c->h_totals);
   if (c->wf_mem) (void)hipFree(c->wf_mem);
   if (c->wf_rad) (void)hipFree(c->wf_rad);
   if (c->wf_ctl) (void)hipFree(c->wf_ctl);
@@ -554,21 +562,34 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
 }
 
 // Per (scene, frame, rank, settings) schedule, cached in the context: the
-// tiles' primary-ray candidate masks and the work blocks.  Block sizes and
-// their dispatch order come from a ONE-SAMPLE PILOT render of this rank's
-// pixels (same kernel, kPilot instantiation, output discarded) that reports
+// tiles' primary-ray candidate masks (host: tiles x primitives) and the work
+// blocks, built on the GPU by rt_schedule.hip from a ONE-SAMPLE PILOT render
+// of this rank's pixels (same kernel, kPilot instantiation) that reports
 // each pixel's path length: pixels whose paths bounce a lot go into small
 // blocks (or are split into sample ranges) dispatched first, empty sky into
 // large blocks.  The pilot traces hard shadows only: the soft rays do not
 // change how long a path is, only what a bounce costs, and tracing them
 // would make the pilot's own tail (one 50-bounce path) several times longer.
+// One 12-byte device->host copy (block and split counts) sizes the launch.
 // This only partitions and orders the work; every block is rendered by the
 // same code, so the image does not depend on it (tests/test_gpu_schedules.py).
 static size_t split_flags_bytes(int nsplit, int spp) {
   return (size_t)nsplit * ((spp + 31) / 32) * sizeof(uint32_t) + (size_t)nsplit * sizeof(int32_t);
 }
 
-static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st) {
+// device buffer *ptr of *cap bytes, grown to at least n bytes
+static int grow(void* ptr, size_t* cap, size_t n) {
+  void** p = (void**)ptr;
+  if (n <= *cap) return RT_OK;
+  if (*p) HIP_TRY(hipFree(*p));
+  *p = nullptr;
+  *cap = 0;
+  HIP_TRY(hipMalloc(p, n));
+  *cap = n;
+  return RT_OK;
+}
+
+static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hipStream_t s) {
   const FlatScene& f = c->flat;
   const int w = p->W, h = p->H, rank = p->rank, world = p->world;
   const rt_tuning& tn = c->tun;
@@ -581,74 +602,66 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st) {
   const bool pilot = tn.pilot != 0;
   const bool frustum = tn.frustum != 0;
   const int64_t key[13] = {(int64_t)c->scene_gen, w, h, rank, world, st->samples, st->max_depth,
-                           st->recursive_reflections, st->soft_shadows, bigP, (int64_t)(block_work * 16), pilot,
-                           frustum};
+                           st->recursive_reflections, st->soft_shadows, bigP, (int64_t)(block_work * 16),
+                           pilot ? 1 + tn.pilot_depth : 0, frustum};
+  const bool masks = f.bvh.empty() && f.spheres.size() <= 64 && f.tris.size() <= 64;
   if (memcmp(key, c->order_key, sizeof key) != 0) {
-    int rc0 = quiesce(c);  // the last render may still read the blocks, masks and split rows
-    if (rc0) return rc0;
-    // primary-ray candidate masks per local tile
-    if (f.bvh.empty() && f.spheres.size() <= 64 && f.tris.size() <= 64) {
-      tile_primary_masks(f, w, h, rank, world, &c->masks_host);
-      if (c->masks_host.size() > c->d_masks_cap) {
-        if (c->d_masks) HIP_TRY(hipFree(c->d_masks));
-        c->d_masks = nullptr;
-        HIP_TRY(hipMalloc((void**)&c->d_masks, c->masks_host.size() * sizeof(unsigned long long)));
-        c->d_masks_cap = c->masks_host.size();
-      }
-      if (!c->masks_host.empty())
-        HIP_TRY(hipMemcpy(c->d_masks, c->masks_host.data(), c->masks_host.size() * sizeof(unsigned long long),
-                          hipMemcpyHostToDevice));
-    } else {
-      c->masks_host.clear();
-    }
+    int rc = quiesce(c);  // the last render may still read the blocks, masks and split rows
+    if (rc) return rc;
     const int local = rt_tiles_for_rank(w, h, rank, world);
-    // per-pixel primary masks (phase 1 traces only the samples of pixels
-    // whose own masks are not empty, against their block's union)
-    std::vector<unsigned long long> pix;
-    if (!c->masks_host.empty()) pixel_primary_masks(f, w, h, rank, world, c->masks_host, &pix);
-    // fallback estimate: primitives projected onto the tile
-    std::vector<float> tile_cost;
-    tile_dispatch_order(f, w, h, rank, world, &c->order_host, &tile_cost);
-    // without a pilot: every pixel of a tile with geometry weighs half a block
-    // (2-pixel blocks), tiles ordered by their count
-    std::vector<float> work((size_t)local * 1024, 0.0f);
-    for (int lt = 0; lt < local; ++lt)
-      if (tile_cost[lt] > 0)
-        for (int q = 0; q < 1024; ++q)
-          work[(size_t)lt * 1024 + q] = (float)(block_work / (2.0 * std::max(1, st->samples))) *
-                                        (1.0f + 1e-3f * std::min(tile_cost[lt], 100.0f));
-    auto upload_blocks = [&](const std::vector<int32_t>& b) -> int {
-      if (b.size() > c->d_blocks_cap) {
-        if (c->d_blocks) HIP_TRY(hipFree(c->d_blocks));
-        c->d_blocks = nullptr;
-        HIP_TRY(hipMalloc((void**)&c->d_blocks, b.size() * sizeof(int32_t)));
-        c->d_blocks_cap = b.size();
-      }
-      if (!b.empty()) HIP_TRY(hipMemcpy(c->d_blocks, b.data(), b.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-      return RT_OK;
-    };
+    // per-tile inputs (host): primary-ray candidate masks, projected-primitive counts
+    if (masks) tile_primary_masks(f, w, h, rank, world, &c->masks_host);
+    else c->masks_host.clear();
+    std::vector<float> cost;
+    tile_cost(f, w, h, rank, world, &cost);
+    const size_t scratch = sched_scratch_bytes(local);
+    const size_t inputs = c->masks_host.size() * sizeof(unsigned long long) + cost.size() * sizeof(float);
+    rc = grow(&c->d_sched, &c->sched_cap, scratch + inputs + 256);
+    if (rc) return rc;
+    SchedParams sp;
+    memset(&sp, 0, sizeof sp);
+    sched_layout(c->d_sched, local, &sp);
+    char* in = (char*)c->d_sched + ((scratch + 255) & ~size_t(255));
+    c->d_masks = masks ? (unsigned long long*)in : nullptr;
+    float* d_cost = (float*)(in + c->masks_host.size() * sizeof(unsigned long long));
+    if (!c->masks_host.empty())
+      HIP_TRY(hipMemcpyAsync(c->d_masks, c->masks_host.data(), c->masks_host.size() * sizeof(unsigned long long),
+                             hipMemcpyHostToDevice, s));
+    if (!cost.empty()) HIP_TRY(hipMemcpyAsync(d_cost, cost.data(), cost.size() * sizeof(float), hipMemcpyHostToDevice, s));
+    sp.spheres = c->d_spheres;
+    sp.tris = c->d_tris;
+    memcpy(sp.cam, f.cam_pos, sizeof sp.cam);
+    sp.vw = 2.0 * f.aspect;
+    sp.W = w;
+    sp.H = h;
+    sp.rank = rank;
+    sp.world = world;
+    sp.tiles_x = (w + 31) / 32;
+    sp.ntiles = rt_num_tiles(w, h);
+    sp.local = local;
+    sp.spp = st->samples;
+    sp.big_pixels = bigP;
+    sp.frustum = frustum;
+    sp.block_work = block_work;
+    sp.tile_masks = c->d_masks;
+    sp.tile_cost = d_cost;
+    int e = sched_launch_pixels(sp, s);
+    if (e != hipSuccess) {
+      set_error(std::string("schedule launch failed: ") + hipGetErrorString((hipError_t)e));
+      return RT_E_DEVICE;
+    }
     if (pilot && local > 0 && st->samples > 0 && st->max_depth > 0) {
       // one sample per pixel, blocks of 64 pixels, packed output into scratch
-      std::vector<int32_t> pb;
-      for (int lt = 0; lt < local; ++lt)
-        for (int p0 = 0; p0 < 1024; p0 += 64) pb.insert(pb.end(), {lt, p0, 64, 0, 1, -1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0});
-      if (!c->masks_host.empty()) fill_block_masks(pix, &pb);
-      int rc = upload_blocks(pb);
-      if (rc) return rc;
       const size_t npx = (size_t)local * 1024;
-      if (npx > c->pilot_cap) {
-        if (c->d_pilot) HIP_TRY(hipFree(c->d_pilot));
-        c->d_pilot = nullptr;
-        HIP_TRY(hipMalloc(&c->d_pilot, npx * 20 + 256));
-        c->pilot_cap = npx;
-      }
+      rc = grow(&c->d_pilot, &c->pilot_cap, npx * 20 + 256);
+    if (rc) return rc;
       float* plin = (float*)c->d_pilot;
       uint8_t* prgba = (uint8_t*)c->d_pilot + npx * 12;
       unsigned int* plen = (unsigned int*)((uint8_t*)c->d_pilot + npx * 16);
       KParams q = *p;
       q.spp = 1;
-      q.blocks = c->d_blocks;
-      q.num_blocks = (int32_t)(pb.size() / kBlockInts);
+      q.blocks = sp.pilot_blocks;
+      q.num_blocks = local * 16;
       q.num_wgs = q.num_blocks;
       q.layout = RT_LAYOUT_PACKED_TILES;
       q.out_linear = plin;
@@ -657,57 +670,49 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st) {
       q.dbg = nullptr;
       q.tile_work = plen;
       q.soft = 0;  // path lengths only (see above)
-      q.tile_masks = c->masks_host.empty() ? nullptr : c->d_masks;
-      HIP_TRY(hipMemsetAsync(plen, 0, npx * sizeof(unsigned int), c->stream));
-      const int e = launch_render(q, false, c->stream);
+      if (tn.pilot_depth > 0) q.max_depth = std::min(q.max_depth, tn.pilot_depth);
+      q.tile_masks = c->d_masks;
+      q.split_rad = nullptr;
+      q.split_hits = nullptr;
+      q.split_cnt = nullptr;
+      HIP_TRY(hipMemsetAsync(plen, 0, npx * sizeof(unsigned int), s));
+      e = launch_render(q, false, s);
       if (e != hipSuccess) {
         set_error(std::string("pilot launch failed: ") + hipGetErrorString((hipError_t)e));
         return RT_E_DEVICE;
       }
-      std::vector<unsigned int> len(npx);
-      HIP_TRY(hipMemcpyAsync(len.data(), plen, npx * sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
-      // a pixel's estimate: the longest pilot path among it and its 4
-      // neighbours (one sample is a noisy estimate of a pixel's mean), plus
-      // a small constant for the camera ray of every sample
-      for (int lt = 0; lt < local; ++lt) {
-        const unsigned int* L = len.data() + (size_t)lt * 1024;
-        for (int q = 0; q < 1024; ++q) {
-          const int x = q & 31, y = q >> 5;
-          unsigned int m = L[q];
-          if (x > 0) m = std::max(m, L[q - 1]);
-          if (x < 31) m = std::max(m, L[q + 1]);
-          if (y > 0) m = std::max(m, L[q - 32]);
-          if (y < 31) m = std::max(m, L[q + 32]);
-          work[(size_t)lt * 1024 + q] = (float)m + 0.02f;
-        }
-      }
+      sp.plen = plen;
     }
-    // tiles whose camera rays provably miss everything (both primary masks
-    // empty): black without tracing
-    std::vector<uint8_t> black;
-    if (frustum && !c->masks_host.empty())
-      for (int lt = 0; lt < local; ++lt) black.push_back((c->masks_host[2 * lt] | c->masks_host[2 * lt + 1]) == 0);
-    c->nsplit = build_blocks(work, st->samples, bigP, block_work, black, &c->blocks_host);
-    if (!c->masks_host.empty()) fill_block_masks(pix, &c->blocks_host);
-    int rc = upload_blocks(c->blocks_host);
+    e = sched_launch_blocks(sp, false, s);
+    if (e != hipSuccess) {
+      set_error(std::string("schedule launch failed: ") + hipGetErrorString((hipError_t)e));
+      return RT_E_DEVICE;
+    }
+    HIP_TRY(hipMemcpyAsync(c->h_totals, sp.totals, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const int nblocks = c->h_totals[0], nsplit = c->h_totals[1];
+    rc = grow(&c->d_blocks, &c->d_blocks_cap, (size_t)std::max(nblocks, 1) * kBlockInts * sizeof(int32_t));
     if (rc) return rc;
-    const size_t need = (size_t)c->nsplit * st->samples * 3 * sizeof(double) + split_flags_bytes(c->nsplit, st->samples);
-    if (need > c->split_cap) {
-      if (c->d_split) HIP_TRY(hipFree(c->d_split));
-      c->d_split = nullptr;
-      HIP_TRY(hipMalloc(&c->d_split, need + 256));
-      c->split_cap = need;
+    sp.blocks = c->d_blocks;
+    e = sched_launch_blocks(sp, true, s);
+    if (e != hipSuccess) {
+      set_error(std::string("schedule launch failed: ") + hipGetErrorString((hipError_t)e));
+      return RT_E_DEVICE;
     }
+    const size_t need = (size_t)nsplit * st->samples * 3 * sizeof(double) + split_flags_bytes(nsplit, st->samples);
+    rc = grow(&c->d_split, &c->split_cap, need + 256);
+    if (rc) return rc;
+    c->num_blocks = nblocks;
+    c->nsplit = nsplit;
     memcpy(c->order_key, key, sizeof key);
   }
   p->blocks = c->d_blocks;
-  p->num_blocks = (int32_t)(c->blocks_host.size() / kBlockInts);
+  p->num_blocks = c->num_blocks;
   p->split_rad = c->nsplit ? (double*)c->d_split : nullptr;
   p->split_hits = c->nsplit ? (uint32_t*)((char*)c->d_split + (size_t)c->nsplit * st->samples * 3 * sizeof(double))
                             : nullptr;
   p->split_cnt = c->nsplit ? (int32_t*)(p->split_hits + (size_t)c->nsplit * ((st->samples + 31) / 32)) : nullptr;
-  p->tile_masks = (c->masks_host.empty() || !frustum) ? nullptr : c->d_masks;
+  p->tile_masks = (masks && frustum) ? c->d_masks : nullptr;
   return RT_OK;
 }
 
@@ -951,17 +956,17 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
     p.stack_off = (p.stage_bytes + 15) & ~15;
     p.stack_depth = std::max(1, f.bvh_depth);
   }
-  const bool wf = use_wavefront(c);
-  if (!wf) {
-    rc = prepare_schedule(c, &p, st);
-    if (rc) return rc;
-  }
-  p.num_wgs = p.num_blocks;
   // the caller's stream, as given (NULL = the legacy default stream); a
   // render enqueued on another stream than this context's last one waits for
   // that one first (they share the split rows and the wavefront state)
   hipStream_t s = (hipStream_t)stream;
   if (c->have_timing && s != c->last_stream) HIP_TRY(hipStreamWaitEvent(s, c->ev1, 0));
+  const bool wf = use_wavefront(c);
+  if (!wf) {
+    rc = prepare_schedule(c, &p, st, s);
+    if (rc) return rc;
+  }
+  p.num_wgs = p.num_blocks;
   if (counts) HIP_TRY(hipMemsetAsync(c->d_counts, 0, 16 * sizeof(unsigned long long), s));
   if (!wf && c->nsplit)  // split pixels: hit bits and sub-block counters start at zero
     HIP_TRY(hipMemsetAsync(p.split_hits, 0, split_flags_bytes(c->nsplit, st->samples), s));

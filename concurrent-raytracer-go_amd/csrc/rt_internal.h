@@ -35,32 +35,46 @@ void flatten_scene(const rt_scene& s, FlatScene* out);
 // Binned-SAH BVH over out->spheres (reorders spheres). Requires no triangles.
 // bins / leaf: SAH bins per axis and spheres per leaf at most (0: defaults).
 void build_sphere_bvh(FlatScene* fs, int bins, int leaf);
-// Dispatch order of the local tiles of (rank, world): descending estimated
-// cost (primitives whose projected bounds overlap the tile), ties by index.
-void tile_dispatch_order(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
-                         std::vector<int32_t>* order, std::vector<float>* local_cost);
-// Work blocks in dispatch order, 8 ints each (KParams::blocks): sized by
-// estimated work per pixel-sample (pixel_work[lt * 1024 + p]), the heaviest
-// pixels split into sample ranges, most expensive first (schedule.cpp).
-// Returns the number of split pixels.
-// black_tiles[lt] != 0: every camera ray of local tile lt provably misses
-// (empty primary masks); its pixels go to kBlockBlack blocks.
+// Per local tile of (rank, world): primitives whose projected bounds overlap
+// it (the work estimate of a schedule without a pilot render).
+void tile_cost(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
+               std::vector<float>* local_cost);
 constexpr int32_t kBlockBlack = 1;  // block flag (8th int): black tile, nothing to trace
 constexpr int kBlockInts = 16;      // ints per work block record (KParams::blocks)
-int build_blocks(const std::vector<float>& pixel_work, int spp, int big_pixels, double block_work,
-                 const std::vector<uint8_t>& black_tiles, std::vector<int32_t>* blocks);
 // Primary-ray candidate masks per local tile (2 x u64: spheres, triangles;
 // scenes with <= 64 of each): bit i set unless primitive i's bounding sphere
 // provably misses the cone of the tile's camera rays.
 void tile_primary_masks(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
                         std::vector<unsigned long long>* masks);
-// The same per pixel of every local tile (2 x u64 per pixel, lt * 1024 + p;
-// only candidates of the pixel's tile are tested; 0 outside the image).
-void pixel_primary_masks(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
-                         const std::vector<unsigned long long>& tile_masks, std::vector<unsigned long long>* pix);
-// Per block record: the union of its pixels' masks (ints 8..11) and the bits
-// of its pixels whose masks are not empty (ints 12..13).
-void fill_block_masks(const std::vector<unsigned long long>& pix, std::vector<int32_t>* blocks);
+
+// The GPU work scheduler (rt_schedule.hip).
+struct SchedParams {
+  const DSphere* spheres;
+  const DTri* tris;
+  double cam[3];
+  double vw;                   // viewport width 2 * aspect (getRay, renderer.go:377-390)
+  int32_t W, H, rank, world, tiles_x, ntiles, local;
+  int32_t spp, big_pixels, frustum;
+  double block_work;
+  const unsigned long long* tile_masks;  // per local tile (2 u64) or null (no primary culling)
+  const float* tile_cost;      // per local tile: projected primitives (estimate without a pilot)
+  const unsigned int* plen;    // pilot path length per local pixel, or null (no pilot)
+  // scratch (sched_layout)
+  unsigned long long* pixmask; // per local pixel: 2 u64
+  float* est;                  // per local pixel: estimated work of one sample
+  int32_t* pilot_blocks;       // 16 records per local tile: the pilot's 64-pixel blocks
+  int32_t* hist;               // per weight class: blocks (pass 1)
+  int32_t* cursor;             // per weight class: next record (pass 2)
+  int32_t* totals;             // [0] blocks, [1] split pixels, [2] split-slot cursor
+  int32_t* blocks;             // the records, heaviest class first (pass 2)
+};
+size_t sched_scratch_bytes(int local);
+void sched_layout(void* scratch, int local, SchedParams* p);
+// masks + pilot blocks (zeroes the class counters first)
+int sched_launch_pixels(const SchedParams& p, void* stream);
+// write = false: estimates, pass 1 (class counts, split count), scan;
+// write = true: pass 2 (the records)
+int sched_launch_blocks(const SchedParams& p, bool write, void* stream);
 
 // ---------------------------------------------------------------- kernels
 // PCG jump-ahead entries: cooperative soft shadows evaluate up to 64

@@ -1,21 +1,12 @@
-// schedule.cpp — how a rank's 32x32 tiles become work blocks.
+// schedule.cpp — the per-tile inputs of the work schedule, on the host.
 //
-// The reference hands tiles to goroutines in row-major order through a
-// channel (createRenderTasks, internal/renderer/renderer.go:398-436); a
-// goroutine that draws a slow tile just keeps it while the others continue.
-// On the GPU a workgroup is dispatched once and runs to completion, so a
-// slow block dispatched late (long multi-bounce paths between mirrors and
-// inside glass) runs alone at the end of the launch.  The host therefore
-//   - estimates each tile's cost from the primitives projected onto it
-//     (tile_dispatch_order) and each tile's primary-ray candidates
-//     (tile_primary_masks),
-//   - and, from a one-sample pilot render (rt_api.cpp prepare_schedule),
-//     each pixel's path length; build_blocks cuts the pixels into blocks of
-//     about equal work, splits the heaviest pixels into sample ranges, and
-//     orders the blocks most expensive first.
-// This only partitions and orders work: every block is rendered by the same
-// code and every pixel's samples are summed in sample order, so the image
-// does not depend on the schedule.
+// The schedule itself (per-pixel masks, pilot render, blocks, dispatch
+// order) is built on the GPU (rt_schedule.hip).  Its per-TILE inputs are
+// cheap (tiles x primitives) and stay here:
+//   - tile_primary_masks: the primitives whose bounding sphere meets the cone
+//     of a tile's camera rays (the per-pixel masks refine these);
+//   - tile_cost: primitives projected onto each tile, the work estimate of a
+//     schedule built without a pilot render.
 #include <math.h>
 
 #include <algorithm>
@@ -26,8 +17,8 @@
 
 namespace rtgo {
 
-void tile_dispatch_order(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
-                         std::vector<int32_t>* order, std::vector<float>* local_cost) {
+void tile_cost(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
+               std::vector<float>* local_cost) {
   const int tiles_x = (W + 31) / 32, tiles_y = (H + 31) / 32, ntiles = tiles_x * tiles_y;
   std::vector<float> cost(ntiles, 0.0f);
   const double vw = 2.0 * fs.aspect;
@@ -59,72 +50,8 @@ void tile_dispatch_order(const FlatScene& fs, int32_t W, int32_t H, int32_t rank
   for (const DSphere& s : fs.spheres) add_sphere(s.c, s.r);
   for (const DTri& t : fs.tris) add_sphere(t.bc, t.br);
 
-  order->clear();
   local_cost->clear();
-  for (int t = rank, lt = 0; t < ntiles; t += world, ++lt) {
-    order->push_back(lt);
-    local_cost->push_back(cost[t]);
-  }
-  std::stable_sort(order->begin(), order->end(), [&](int32_t a, int32_t b) {
-    return cost[rank + a * world] > cost[rank + b * world];
-  });
-}
-
-int build_blocks(const std::vector<float>& pixel_work, int spp, int big_pixels, double block_work,
-                 const std::vector<uint8_t>& black_tiles, std::vector<int32_t>* blocks) {
-  // pixel_work[lt * 1024 + p]: estimated path work per sample of pixel p
-  // (row-major) of local tile lt.  Pixels are taken in row-major order and
-  // grouped into blocks of consecutive pixels while the block's work
-  // spp * sum(work) stays within block_work (at most big_pixels pixels).  A
-  // pixel whose own work exceeds block_work is split into sample ranges of
-  // at most 64 samples (one path per lane), each its own block; the pixel
-  // is resolved by whichever of its blocks finishes last.  Blocks are
-  // dispatched most expensive first, so the longest paths start at once.
-  // A tile flagged in black_tiles (no camera ray of it can hit anything,
-  // tile_primary_masks) becomes 16 blocks of 64 pixels marked kBlockBlack,
-  // dispatched last: the kernel writes their black pixels without tracing.
-  struct B {
-    double est;
-    int32_t lt, p0, np, s0, ns, slot, nsub, flags;
-  };
-  std::vector<B> v;
-  int nsplit = 0;
-  const double S = std::max(spp, 1);
-  const int local = (int)(pixel_work.size() / 1024);
-  for (int lt = 0; lt < local; ++lt) {
-    if (spp > 0 && lt < (int)black_tiles.size() && black_tiles[lt]) {
-      for (int p0 = 0; p0 < 1024; p0 += 64) v.push_back(B{0.0, lt, p0, 64, 0, spp, -1, 1, kBlockBlack});
-      continue;
-    }
-    const float* w = pixel_work.data() + (size_t)lt * 1024;
-    int p = 0;
-    while (p < 1024) {
-      const double e = S * w[p];
-      if (spp > 1 && e > block_work) {  // split this pixel
-        const int k = (spp + 63) / 64;  // ranges of <= 64 samples: one path per lane
-        const int slot = nsplit++;
-        for (int j = 0; j < k; ++j) {
-          const int s0 = (int)((long long)spp * j / k), s1 = (int)((long long)spp * (j + 1) / k);
-          v.push_back(B{(s1 - s0) * (double)w[p], lt, p, 1, s0, s1 - s0, slot, k, 0});
-        }
-        ++p;
-        continue;
-      }
-      int np = 1;
-      double sum = e;
-      while (p + np < 1024 && np < big_pixels && S * w[p + np] <= block_work && sum + S * w[p + np] <= block_work) {
-        sum += S * w[p + np];
-        ++np;
-      }
-      v.push_back(B{sum, lt, p, np, 0, spp, -1, 1, 0});
-      p += np;
-    }
-  }
-  std::stable_sort(v.begin(), v.end(), [](const B& a, const B& b) { return a.est > b.est; });
-  blocks->clear();
-  for (const B& b : v)
-    blocks->insert(blocks->end(), {b.lt, b.p0, b.np, b.s0, b.ns, b.slot, b.nsub, b.flags, 0, 0, 0, 0, 0, 0, 0, 0});
-  return nsplit;
+  for (int t = rank; t < ntiles; t += world) local_cost->push_back(cost[t]);
 }
 
 // Does the cone (apex, unit axis, cos/sin of its half-angle) meet the sphere
@@ -198,48 +125,6 @@ void tile_primary_masks(const FlatScene& fs, int32_t W, int32_t H, int32_t rank,
     cone_masks(fs, axis, cmin, smax, low_bits(std::min(ns, 64)), low_bits(std::min(nt, 64)), &ms, &mt);
     masks->push_back(ms);
     masks->push_back(mt);
-  }
-}
-
-void pixel_primary_masks(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
-                         const std::vector<unsigned long long>& tile_masks, std::vector<unsigned long long>* pix) {
-  const int tiles_x = (W + 31) / 32, ntiles = tiles_x * ((H + 31) / 32);
-  const double vw = 2.0 * fs.aspect;
-  const int local = (int)(tile_masks.size() / 2);
-  pix->assign((size_t)local * 1024 * 2, 0ull);
-  for (int lt = 0; lt < local; ++lt) {
-    const int t = rank + lt * world;
-    const unsigned long long ts = tile_masks[2 * lt], tt = tile_masks[2 * lt + 1];
-    if (t >= ntiles || (ts | tt) == 0) continue;
-    const int tx = t % tiles_x, ty = t / tiles_x;
-    for (int q = 0; q < 1024; ++q) {
-      const int x = tx * 32 + (q & 31), y = ty * 32 + (q >> 5);
-      if (x >= W || y >= H) continue;
-      double axis[3], cmin, smax;
-      rect_cone(vw, W, H, x, x + 1, y, y + 1, axis, &cmin, &smax);
-      unsigned long long* m = pix->data() + ((size_t)lt * 1024 + q) * 2;
-      cone_masks(fs, axis, cmin, smax, ts, tt, &m[0], &m[1]);
-    }
-  }
-}
-
-void fill_block_masks(const std::vector<unsigned long long>& pix, std::vector<int32_t>* blocks) {
-  for (size_t b = 0; b + kBlockInts <= blocks->size(); b += kBlockInts) {
-    int32_t* r = blocks->data() + b;
-    const int lt = r[0], p0 = r[1], np = std::min(r[2], 64);
-    unsigned long long ms = 0, mt = 0, live = 0;
-    for (int k = 0; k < np && p0 + k < 1024; ++k) {
-      const unsigned long long* m = pix.data() + ((size_t)lt * 1024 + p0 + k) * 2;
-      ms |= m[0];
-      mt |= m[1];
-      if (m[0] | m[1]) live |= 1ull << k;
-    }
-    r[8] = (int32_t)(uint32_t)ms;
-    r[9] = (int32_t)(uint32_t)(ms >> 32);
-    r[10] = (int32_t)(uint32_t)mt;
-    r[11] = (int32_t)(uint32_t)(mt >> 32);
-    r[12] = (int32_t)(uint32_t)live;
-    r[13] = (int32_t)(uint32_t)(live >> 32);
   }
 }
 

@@ -132,7 +132,7 @@ class Tuning(ctypes.Structure):
         ("wf_lds_nodes", ctypes.c_int32),
         ("wf_trav_block", ctypes.c_int32),
         ("wf_trav_wgs", ctypes.c_int32),
-        ("_pad", ctypes.c_int32),
+        ("pilot_depth", ctypes.c_int32),
     ]
 
 

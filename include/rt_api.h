@@ -243,7 +243,7 @@ typedef struct {
   int32_t wf_lds_nodes;   /* BVH nodes staged into LDS; -1: as many as fit */
   int32_t wf_trav_block;  /* threads per traversal workgroup (64..1024); 0: 1024 */
   int32_t wf_trav_wgs;    /* traversal workgroups sharing a CU's LDS; 0: 1 */
-  int32_t _pad;
+  int32_t pilot_depth;    /* bounces the pilot render follows a path at most (default 12); 0: max_depth */
 } rt_tuning;
 void rt_tuning_default(rt_tuning* t);
 /* Applies to later rt_context_set_scene (BVH shape) and render calls. */
