@@ -2,7 +2,7 @@
 //
 //   raytracer <scene_file> <output_file> <width> <height>
 //             [--samples N] [--max-depth N] [--seed N] [--no-soft-shadows]
-//             [--no-recursive]
+//             [--no-recursive] [--devices N] [--sky default|white|sunset|night]
 //
 // Same positional arguments, stdout lines, ".png" default extension
 // (main.go:53-56) and benchmark_data.json next to the output
@@ -11,7 +11,8 @@
 // as P3 PPM (Go writes PNG bytes whatever the extension), benchmark_data.json
 // gains the published rays_per_second / pixels_per_second fields
 // (README.md:60-61), and the optional flags above (the Go CLI never calls
-// the renderer's setters, settings.go:3-25).
+// the renderer's setters, settings.go:3-25; --sky is the opt-in atmosphere,
+// include/rt_api.h RT_SKY_*).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -102,6 +103,20 @@ int main(int argc, char** argv) {
       st.soft_shadows = 0;
     } else if (a == "--no-recursive") {
       st.recursive_reflections = 0;
+    } else if (a == "--devices") {  // GPUs the tiles are sharded over (rt_settings.num_devices)
+      if (!parse_int(need("--devices"), &v) || v < 1) return 2;
+      st.num_devices = (int32_t)v;
+    } else if (a == "--sky") {  // opt-in sky on miss (atmosphere.go presets); default: black
+      const std::string k = need("--sky");
+      if (k == "none") st.sky = RT_SKY_NONE;
+      else if (k == "default") st.sky = RT_SKY_DEFAULT;
+      else if (k == "white") st.sky = RT_SKY_WHITE;
+      else if (k == "sunset") st.sky = RT_SKY_SUNSET;
+      else if (k == "night") st.sky = RT_SKY_NIGHT;
+      else {
+        fprintf(stderr, "unknown --sky %s\n", k.c_str());
+        return 2;
+      }
     } else {
       args.push_back(a);
     }

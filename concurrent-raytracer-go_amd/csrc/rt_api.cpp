@@ -176,6 +176,42 @@ static void push_tri(FlatScene* fs, v3 v0, v3 v1, v3 v2, int mat, int obj) {
   fs->tris.push_back(t);
 }
 
+void sky_presets(DSky out[kSkies]) {
+  memset(out, 0, sizeof(DSky) * kSkies);
+  struct P {
+    double top[3], bottom[3], sun_dir[3], sun_color[3], sun_intensity, sun_size, rayleigh[3], mie[3], depth, fog,
+        fog_color[3], haze, tod;
+  };
+  // NewDefaultAtmosphere, NewWhiteAtmosphere, NewSunsetAtmosphere,
+  // NewNightAtmosphere (atmosphere.go:28-98); HazeIntensity is unused by GetSkyColor
+  static const P presets[kSkies] = {
+      {{0.6, 0.8, 1.0}, {0.9, 0.95, 1.0}, {0.0, 0.8, -0.6}, {1.0, 0.98, 0.95}, 1.2, 0.015, {0.6, 0.8, 1.0},
+       {1.0, 0.98, 0.95}, 0.3, 0.0, {0.9, 0.92, 0.95}, 0.05, 0.6},
+      {{0.98, 0.98, 1.0}, {0.92, 0.92, 0.95}, {0.0, 0.8, -0.6}, {1.0, 0.99, 0.97}, 0.8, 0.012, {0.9, 0.9, 0.95},
+       {0.95, 0.95, 0.98}, 0.2, 0.0, {0.95, 0.95, 0.98}, 0.02, 0.6},
+      {{1.0, 0.4, 0.2}, {1.0, 0.8, 0.6}, {0.0, 0.3, -0.9}, {1.0, 0.6, 0.3}, 1.2, 0.03, {1.0, 0.4, 0.2},
+       {1.0, 0.8, 0.6}, 0.8, 0.1, {1.0, 0.8, 0.6}, 0.3, 0.8},
+      {{0.1, 0.1, 0.3}, {0.2, 0.2, 0.4}, {0.0, -0.7, -0.7}, {0.8, 0.8, 1.0}, 0.3, 0.005, {0.1, 0.1, 0.3},
+       {0.8, 0.8, 1.0}, 0.2, 0.0, {0.1, 0.1, 0.2}, 0.0, 0.0},
+  };
+  for (int i = 0; i < kSkies; ++i) {
+    const P& p = presets[i];
+    DSky& d = out[i];
+    memcpy(d.top, p.top, sizeof d.top);
+    memcpy(d.bottom, p.bottom, sizeof d.bottom);
+    memcpy(d.sun_dir, p.sun_dir, sizeof d.sun_dir);
+    memcpy(d.sun_color, p.sun_color, sizeof d.sun_color);
+    d.sun_intensity = p.sun_intensity;
+    d.sun_size = p.sun_size;
+    memcpy(d.rayleigh, p.rayleigh, sizeof d.rayleigh);
+    memcpy(d.mie, p.mie, sizeof d.mie);
+    d.depth = p.depth;
+    d.fog_density = p.fog;
+    memcpy(d.fog_color, p.fog_color, sizeof d.fog_color);
+    d.time_of_day = p.tod;
+  }
+}
+
 void flatten_scene(const rt_scene& s, FlatScene* fs) {
   *fs = FlatScene();
   for (int i = 0; i < s.num_objects; ++i) {
@@ -291,6 +327,10 @@ static int validate_settings(const rt_settings* st, int32_t w, int32_t h) {
     set_error("samples must be in [0, " + std::to_string(kMaxBlockSamples) + "]");
     return RT_E_INVALID;
   }
+  if (st->sky < RT_SKY_NONE || st->sky > RT_SKY_NIGHT) {
+    set_error("sky must be one of RT_SKY_*");
+    return RT_E_INVALID;
+  }
   return RT_OK;
 }
 
@@ -316,6 +356,7 @@ struct rt_context {
   const DBVHNode* d_bvh = nullptr;
   const DQNode* d_qbvh = nullptr;
   const uint64_t* d_jump = nullptr;
+  const DSky* d_sky = nullptr;  // the kSkies presets
   unsigned long long* d_counts = nullptr;
   hipStream_t last_stream = nullptr;
   bool have_timing = false;
@@ -510,7 +551,8 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   size_t off_j = off_l + al(f.lights.size() * sizeof(DLight));
   size_t off_b = off_j + al(kJump * 2 * sizeof(uint64_t));
   size_t off_q = off_b + al(f.bvh.size() * sizeof(DBVHNode));
-  size_t total = off_q + al(f.qbvh.size() * sizeof(DQNode)) + 256;
+  size_t off_sky = off_q + al(f.qbvh.size() * sizeof(DQNode));
+  size_t total = off_sky + al(kSkies * sizeof(DSky)) + 256;
   rc = quiesce(c);  // the last render may still read the scene
   if (rc) return rc;
   if (c->d_scene && c->d_scene_bytes < total) {
@@ -542,6 +584,7 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   }
   memcpy(host.data() + off_b, f.bvh.data(), f.bvh.size() * sizeof(DBVHNode));
   memcpy(host.data() + off_q, f.qbvh.data(), f.qbvh.size() * sizeof(DQNode));
+  sky_presets(reinterpret_cast<DSky*>(host.data() + off_sky));
   HIP_TRY(hipMemcpy(base, host.data(), total, hipMemcpyHostToDevice));
   c->d_spheres = (const DSphere*)(base + off_s);
   c->d_tris = (const DTri*)(base + off_t);
@@ -551,6 +594,7 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   c->d_bvh = (const DBVHNode*)(base + off_b);
   c->d_qbvh = (const DQNode*)(base + off_q);
   c->d_jump = (const uint64_t*)(base + off_j);
+  c->d_sky = (const DSky*)(base + off_sky);
   // small linear-scan scenes are staged into LDS by every workgroup
   // (the 1 KB PCG jump table stays in global memory, L1-cached: only the
   // cooperative soft-shadow form reads it, and scenes near the LDS limit of 12
@@ -600,10 +644,13 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
   double block_work = f.bvh.empty() ? 512.0 : 8192.0;
   if (tn.block_work > 0) block_work = std::max(1.0, tn.block_work);
   const bool pilot = tn.pilot != 0;
-  const bool frustum = tn.frustum != 0;
+  // a sky makes every camera sample count (a miss returns the sky, not +0):
+  // no primary-ray culling, no black tiles
+  const bool sky = st->sky != RT_SKY_NONE;
+  const bool frustum = tn.frustum != 0 && !sky;
   const int64_t key[13] = {(int64_t)c->scene_gen, w, h, rank, world, st->samples, st->max_depth,
                            st->recursive_reflections, st->soft_shadows, bigP, (int64_t)(block_work * 16),
-                           pilot ? 1 + tn.pilot_depth : 0, frustum};
+                           pilot ? 1 + tn.pilot_depth : 0, (frustum ? 1 : 0) | (sky ? 2 : 0)};
   const bool masks = f.bvh.empty() && f.spheres.size() <= 64 && f.tris.size() <= 64;
   if (memcmp(key, c->order_key, sizeof key) != 0) {
     int rc = quiesce(c);  // the last render may still read the blocks, masks and split rows
@@ -789,6 +836,7 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   memcpy(p.qd, f.qd, sizeof p.qd);
   p.mats = kp.mats;
   p.lights = kp.lights;
+  p.sky = kp.sky;
   p.nl = nl;
   p.max_depth = kp.max_depth;
   p.recursive = kp.recursive;
@@ -927,6 +975,7 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   p.lights = c->d_lights;
   p.bvh = c->d_bvh;
   p.jump = c->d_jump;
+  p.sky = st->sky != RT_SKY_NONE ? c->d_sky + (st->sky - 1) : nullptr;
   p.out_linear = d_linear;
   p.out_rgba = d_rgba;
   p.counts = counts ? c->d_counts : nullptr;

@@ -619,6 +619,51 @@ __device__ __forceinline__ CamK make_cam(uint64_t seed_key, int W, int H, double
 // ------------------------------------------------------------ pixel output
 // toneMap (renderer.go:348-367) then Vec3.ToRGB (vector.go:106-109) of a
 // pixel's mean radiance: opaque RGBA8.
+// Go's math.Max / math.Min (NaN propagates; +0 > -0).
+__device__ __forceinline__ double go_max2(double x, double y) {
+  if (__builtin_isinf(x) && x > 0) return x;
+  if (__builtin_isinf(y) && y > 0) return y;
+  if (__builtin_isnan(x) || __builtin_isnan(y)) return __builtin_nan("");
+  if (x == 0 && x == y) return __builtin_signbit(x) ? y : x;
+  return x > y ? x : y;
+}
+__device__ __forceinline__ double go_min2(double x, double y) {
+  if (__builtin_isinf(x) && x < 0) return x;
+  if (__builtin_isinf(y) && y < 0) return y;
+  if (__builtin_isnan(x) || __builtin_isnan(y)) return __builtin_nan("");
+  if (x == 0 && x == y) return __builtin_signbit(x) ? x : y;
+  return x < y ? x : y;
+}
+
+// AtmosphereConfig.GetSkyColor (internal/atmosphere/atmosphere.go:100-135),
+// binary64 in its order; its undefined FastVec3* helpers are the Vec3
+// methods (vector.go): Normalize (0 for a zero vector), a.Lerp(b, t) =
+// a + (b - a) * t, Dot, MulScalar; Max / Min with Go's NaN rules; Clamp(0.1, 0.98).
+__device__ __forceinline__ d3 sky_lerp(d3 a, d3 b, double t) { return a + muls(b - a, t); }
+__device__ __noinline__ d3 sky_color(const DSky* __restrict__ a, d3 dir) {
+  const d3 u = normalize(dir);
+  const double t = 0.5 * (u.y + 1.0);
+  d3 sky = sky_lerp(ld3(a->bottom), ld3(a->top), t);
+  const double depth = go_max2(0.0, u.y);
+  const double atmospheric = exp(-depth * a->depth);
+  const d3 scattering = sky_lerp(ld3(a->rayleigh), ld3(a->mie), atmospheric);
+  sky = sky_lerp(sky, scattering, 0.25);
+  const double sun_dot = dot(u, ld3(a->sun_dir));
+  if (sun_dot > (1.0 - a->sun_size)) {
+    double si = pow((sun_dot - (1.0 - a->sun_size)) / a->sun_size, 1.5);
+    si = go_min2(si, 1.0);
+    sky = sky_lerp(sky, ld3(a->sun_color), si * a->sun_intensity * 0.9);
+  }
+  double tf = a->time_of_day;
+  if (tf > 0.5) tf = 1.0 - tf;
+  tf *= 2.0;
+  const double darkness = 1.0 - tf * 0.3;
+  sky = muls(sky, darkness);
+  if (a->fog_density > 0.0) sky = sky_lerp(ld3(a->fog_color), sky, exp(-a->fog_density));
+  return mk(go_max2(0.1, go_min2(0.98, sky.x)), go_max2(0.1, go_min2(0.98, sky.y)),
+            go_max2(0.1, go_min2(0.98, sky.z)));
+}
+
 __device__ __forceinline__ uint32_t tonemap_rgba8(double mx, double my, double mz) {
   const double g = 1.0 / 2.2;
   const double tx_ = clamp01(pow_gamma(1.0 - exp(-(mx * 1.0)), g));

@@ -30,6 +30,11 @@ struct FlatScene {
   int32_t objects = 0;        // len(hittables)
 };
 
+// The AtmosphereConfig presets of RT_SKY_DEFAULT .. RT_SKY_NIGHT
+// (internal/atmosphere/atmosphere.go:28-98), index sky - 1.
+constexpr int kSkies = 4;
+void sky_presets(DSky out[kSkies]);
+
 // GetHittables + createCube + material constructors (scene.go:59-190).
 void flatten_scene(const rt_scene& s, FlatScene* out);
 // Binned-SAH BVH over out->spheres (reorders spheres). Requires no triangles.
@@ -111,6 +116,7 @@ struct KParams {
   int32_t* split_cnt;          // split pixels: sub-blocks finished (zeroed per launch)
   unsigned int* tile_work;     // pilot renders (spp 1, 64-pixel blocks): per pixel, its path length (else null)
   const unsigned long long* tile_masks;  // per local tile: primary-ray candidate masks (spheres, tris) or null
+  const DSky* sky;             // miss radiance (rt_settings.sky) or null: black (renderer.go:170-173)
   const void* stage_src;       // start of the scene prefix staged into LDS (spheres..lights)
   int32_t stage_bytes;         // bytes to stage (multiple of 16); 0 = read the scene from global memory
   int32_t stack_off;           // byte offset of the BVH stacks in dynamic LDS
@@ -176,6 +182,7 @@ struct WfParams {
   double q0[3], qd[3];
   const DMat* mats;
   const DLight* lights;
+  const DSky* sky;           // miss radiance or null (black)
   int32_t nl, max_depth, recursive, soft, spp;
   int32_t W, H, rank, world, tiles_x, ntiles, layout;
   int32_t stack_depth;       // BVH stack entries per lane (the tree's depth - 1)

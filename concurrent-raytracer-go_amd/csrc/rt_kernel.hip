@@ -572,6 +572,9 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     // counting variant still walks its samples for the path counts (its
     // queries have no candidates: no hit bit is ever set).
     const int NL = kCount ? NB : (loc.black ? 0 : nlive * ns);
+    // with an opted-in sky a miss returns the sky (not +0): every camera
+    // sample is shaded (no culling applies: the host disables the masks)
+    const bool sky = k->sky != nullptr;
     for (int j = lane; j < NL; j += 64) {
       // j -> (pixel, sample): every sample of the block (kCount) or of its
       // live pixels, in order
@@ -588,8 +591,8 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       cnt<kCount>(c, C_BOUNCE);
       // hit or miss is all this phase needs: an any-hit query over
       // [0.001, +inf) decides exactly what hitWorld's closest hit would
-      const bool hit = h.masks ? any_hit_masked<kCount>(h.g, o, d, __builtin_inf(), prim, c)
-                               : any_hit<kCount>(h.g, o, d, __builtin_inf(), stack, c);
+      const bool hit = sky || (h.masks ? any_hit_masked<kCount>(h.g, o, d, __builtin_inf(), prim, c)
+                                       : any_hit<kCount>(h.g, o, d, __builtin_inf(), stack, c));
       if (hit) atomicOr(&hbits[id >> 5], 1u << (id & 31));
     }
   }
@@ -762,6 +765,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
         const Hot h = hot<kStage>();
         const Geo& gg = h.g;
         bool done = depth >= h.max_depth;  // traceRay depth cut-off: contributes 0
+        bool missed = false;
         if (!done) {
           if (kCount && depth == 0) {  // phase 1 counted the primary query
             Counters nc;
@@ -771,9 +775,14 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
             done = (wide_q && !wide_fb) ? !wide_found
                                         : !closest_hit<kCount>(gg, o, d, hs, stack, all, c);  // miss -> black
           }
+          missed = done;
         }
         if (done) {
           fin = true;
+          if (missed) {  // an opted-in sky instead of black (rt_settings.sky)
+            const DSky* sky = fresh()->sky;
+            if (sky) L = L + mul(T, sky_color(sky, d));
+          }
         } else {
           shade = true;
           cnt<kCount>(c, C_SHADE);

@@ -79,6 +79,20 @@ struct alignas(16) DLight {  // 64 B
   double pad;
 };
 
+// An AtmosphereConfig preset (internal/atmosphere/atmosphere.go:8-98): the
+// radiance of a ray that hits nothing when a sky is opted in (rt_settings.sky).
+struct alignas(16) DSky {  // 240 B
+  double top[3], bottom[3];     // SkyColorTop, SkyColorBottom
+  double sun_dir[3], sun_color[3];
+  double sun_intensity, sun_size;
+  double rayleigh[3], mie[3];   // RayleighScattering, MieScattering
+  double depth;                 // AtmosphericDepth
+  double fog_density;
+  double fog_color[3];
+  double time_of_day;
+  double pad;
+};
+
 // BVH node over spheres (binned SAH, built on host).  Bounds are float,
 // rounded outward so a box never excludes a sphere point; leaves reference
 // [first, first+count) of the BVH-ordered sphere array.

@@ -414,7 +414,12 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
         }
         if (miss) {
           p.hidx[slot] = -1;
-          if (sid != kDeadSid) finish(p, sid, mk(a.lx[slot], a.ly[slot], a.lz[slot]));
+          if (sid != kDeadSid) {
+            d3 L = mk(a.lx[slot], a.ly[slot], a.lz[slot]);
+            if (p.sky && a.depth[slot] < p.max_depth)  // the root box missed: the sky (opt-in)
+              L = L + mul(mk(a.tx[slot], a.ty[slot], a.tz[slot]), sky_color(p.sky, ld_d(a, slot)));
+            finish(p, sid, L);
+          }
         }
       }
     }
@@ -450,7 +455,9 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
           p.hnum[slot] = bnum;
         } else {
           p.hidx[slot] = -1;
-          finish(p, a.sid[slot], mk(a.lx[slot], a.ly[slot], a.lz[slot]));
+          d3 L = mk(a.lx[slot], a.ly[slot], a.lz[slot]);
+          if (p.sky) L = L + mul(mk(a.tx[slot], a.ty[slot], a.tz[slot]), sky_color(p.sky, d));  // opt-in sky
+          finish(p, a.sid[slot], L);
         }
       }
     }

@@ -40,6 +40,7 @@ MATERIAL_KINDS = {
 }
 RT_LAYOUT_IMAGE, RT_LAYOUT_PACKED_TILES = 0, 1
 RT_PATH_AUTO, RT_PATH_MEGAKERNEL = 0, 1
+SKIES = {"none": 0, "default": 1, "white": 2, "sunset": 3, "night": 4}  # RT_SKY_*
 RT_COMM_ID_BYTES = 128
 
 
@@ -112,6 +113,8 @@ class Settings(ctypes.Structure):
         ("num_workers", ctypes.c_int32),
         ("num_devices", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
+        ("sky", ctypes.c_int32),
+        ("_pad2", ctypes.c_int32),
     ]
 
 
@@ -475,6 +478,10 @@ class ParallelRenderer:
 
     def set_seed(self, seed: int):
         self.settings.seed = seed
+
+    def set_sky(self, sky: str):
+        """Opt-in sky on miss (atmosphere.go presets); "none" = black, the reference."""
+        self.settings.sky = SKIES[sky]
 
     def get_stats(self) -> dict:  # settings.go:27-36
         s = self.settings

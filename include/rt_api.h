@@ -123,7 +123,24 @@ typedef struct {
                                     cmd/raytracer/main.go:46); recorded in benchmark data only */
   int32_t num_devices;           /* rt_render: GPUs 0..n-1 render tiles t % n (0 or 1: device 0 only) */
   uint64_t seed;                 /* counter-based RNG seed (include/rt_rng.h); default 1 */
+  int32_t sky;                   /* RT_SKY_*: radiance of a ray that hits nothing; default RT_SKY_NONE */
+  int32_t _pad2;
 } rt_settings;
+
+/* What a ray that hits nothing returns.  The reference's live path returns
+ * black (traceRay, renderer.go:170-173): RT_SKY_NONE, the default and the
+ * parity setting.  The others are OPT-IN and follow the reference's
+ * (unlinked) atmosphere package: AtmosphereConfig.GetSkyColor
+ * (internal/atmosphere/atmosphere.go:100-135) with the presets
+ * NewDefaultAtmosphere / NewWhiteAtmosphere / NewSunsetAtmosphere /
+ * NewNightAtmosphere (atmosphere.go:28-98); its undefined FastVec3* helpers
+ * are taken as the Vec3 methods of the same name (Normalize, a.Lerp(b, t) =
+ * a + (b - a) t, Dot, MulScalar; internal/math/vector.go). */
+#define RT_SKY_NONE 0
+#define RT_SKY_DEFAULT 1
+#define RT_SKY_WHITE 2
+#define RT_SKY_SUNSET 3
+#define RT_SKY_NIGHT 4
 
 typedef struct {
   double render_seconds;    /* wall time of rt_render, upload + kernels + download (Go Render semantics) */

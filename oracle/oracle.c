@@ -233,7 +233,70 @@ typedef struct {
   int max_depth, samples, recursive, soft;
   uint64_t seed_key;
   int W, H;
+  int sky; /* RT_SKY_*: 0 = a miss is black (renderer.go:170-173) */
 } oscene;
+
+/* ------------------------------------------------------------ sky (opt-in)
+ * AtmosphereConfig (internal/atmosphere/atmosphere.go:8-26) and its presets
+ * NewDefaultAtmosphere / NewWhiteAtmosphere / NewSunsetAtmosphere /
+ * NewNightAtmosphere (atmosphere.go:28-98), index RT_SKY_* - 1. */
+typedef struct {
+  vec3 top, bottom, sun_dir, sun_color;
+  double sun_intensity, sun_size;
+  vec3 rayleigh, mie;
+  double depth, fog_density;
+  vec3 fog_color;
+  double haze, time_of_day;
+} osky;
+
+static const osky kSkyPresets[4] = {
+    {{0.6, 0.8, 1.0}, {0.9, 0.95, 1.0}, {0.0, 0.8, -0.6}, {1.0, 0.98, 0.95}, 1.2, 0.015, {0.6, 0.8, 1.0},
+     {1.0, 0.98, 0.95}, 0.3, 0.0, {0.9, 0.92, 0.95}, 0.05, 0.6},
+    {{0.98, 0.98, 1.0}, {0.92, 0.92, 0.95}, {0.0, 0.8, -0.6}, {1.0, 0.99, 0.97}, 0.8, 0.012, {0.9, 0.9, 0.95},
+     {0.95, 0.95, 0.98}, 0.2, 0.0, {0.95, 0.95, 0.98}, 0.02, 0.6},
+    {{1.0, 0.4, 0.2}, {1.0, 0.8, 0.6}, {0.0, 0.3, -0.9}, {1.0, 0.6, 0.3}, 1.2, 0.03, {1.0, 0.4, 0.2},
+     {1.0, 0.8, 0.6}, 0.8, 0.1, {1.0, 0.8, 0.6}, 0.3, 0.8},
+    {{0.1, 0.1, 0.3}, {0.2, 0.2, 0.4}, {0.0, -0.7, -0.7}, {0.8, 0.8, 1.0}, 0.3, 0.005, {0.1, 0.1, 0.3},
+     {0.8, 0.8, 1.0}, 0.2, 0.0, {0.1, 0.1, 0.2}, 0.0, 0.0},
+};
+
+/* FastVec3Lerp(a, b, t): undefined in the reference; taken as a.Lerp(b, t) =
+ * a.Add(b.Sub(a).MulScalar(t)) (vector.go:116-118), like FastLerp
+ * (advanced_math.go:84-86). */
+static vec3 sky_lerp(vec3 a, vec3 b, double t) { return vadd(a, vmuls(vsub(b, a), t)); }
+
+/* GetSkyColor, atmosphere.go:100-135 (FastVec3Normalize/Dot/MulScalar taken
+ * as Normalize, Dot, MulScalar). */
+vec3 oracle_sky_color_v(int sky, vec3 dir) {
+  const osky* a = &kSkyPresets[sky - 1];
+  vec3 u = vnorm(dir);
+  double t = 0.5 * (u.y + 1.0);
+  vec3 c = sky_lerp(a->bottom, a->top, t);
+  double depth = oracle_go_max(0.0, u.y);
+  double atmospheric = exp(-depth * a->depth);
+  vec3 scattering = sky_lerp(a->rayleigh, a->mie, atmospheric);
+  c = sky_lerp(c, scattering, 0.25);
+  double sun_dot = vdot(u, a->sun_dir);
+  if (sun_dot > (1.0 - a->sun_size)) {
+    double si = oracle_go_pow((sun_dot - (1.0 - a->sun_size)) / a->sun_size, 1.5);
+    si = oracle_go_min(si, 1.0);
+    c = sky_lerp(c, a->sun_color, si * a->sun_intensity * 0.9);
+  }
+  double tf = a->time_of_day;
+  if (tf > 0.5) tf = 1.0 - tf;
+  tf *= 2.0;
+  double darkness = 1.0 - tf * 0.3;
+  c = vmuls(c, darkness);
+  if (a->fog_density > 0.0) c = sky_lerp(a->fog_color, c, exp(-a->fog_density));
+  return vclamp(c, 0.1, 0.98);
+}
+
+void oracle_sky_color(int sky, const double dir[3], double out[3]) {
+  vec3 c = oracle_sky_color_v(sky, V(dir[0], dir[1], dir[2]));
+  out[0] = c.x;
+  out[1] = c.y;
+  out[2] = c.z;
+}
 
 typedef struct {
   double t;
@@ -605,7 +668,8 @@ static vec3 trace_ray(const oscene* sc, oray r, int depth, ostream* s) {
   if (depth >= sc->max_depth) return V(0, 0, 0);
   hitrec h;
   s->c->bounce_rays++;
-  if (!hit_world(sc, r, 0.001, INFINITY, &h, s->c)) return V(0.0, 0.0, 0.0);
+  if (!hit_world(sc, r, 0.001, INFINITY, &h, s->c))  /* black, or an opted-in sky (rt_settings.sky) */
+    return sc->sky ? oracle_sky_color_v(sc->sky, r.d) : V(0.0, 0.0, 0.0);
   const omat* m = h.mat;
   s->c->shade_events++;
   vec3 emitted = mat_emitted(m);
@@ -797,6 +861,7 @@ int oracle_render(const rt_scene* scene, int32_t width, int32_t height, const rt
   sc.cam_pos = varr(scene->camera.position);
   sc.aspect = scene->camera.aspect_ratio;
   sc.max_depth = st->max_depth;
+  sc.sky = st->sky;
   sc.samples = st->samples;
   sc.recursive = st->recursive_reflections != 0;
   sc.soft = st->soft_shadows != 0;

@@ -96,3 +96,71 @@ def spheres10k_scene(rtgo, n=10000):
     g = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(g)
     return rtgo.Scene.from_json_text(g.dumps(g.generate(n)))
+
+
+def _edge_scenes():
+    """Scenes at the edges of the kernel's exact culling (rt_kernel.hip
+    in_cone / cone_candidates, rt_schedule.hip pixel cones): their margins
+    are relative (1e-7 .. 1e-5), so these stress huge radii, far
+    coordinates, tiny spheres and a light almost on a surface."""
+    def sph(p, r, m):
+        return {"type": "sphere", "position": list(p), "radius": r, "material": m}
+
+    metal = {"type": "metal", "color": [0.9, 0.8, 0.7], "roughness": 0.1}
+    mirror = {"type": "metal", "color": [0.95, 0.95, 0.95], "roughness": 0.0, "metallic": 1.0}
+    glass = {"type": "glass", "color": [0.95, 0.95, 1.0], "refractionIndex": 1.5}
+    lamb = {"type": "lambertian", "color": [0.6, 0.5, 0.4]}
+    out = {}
+    # a radius-1e6 ground sphere (self-exclusion and cone tests at huge radius)
+    out["huge_ground"] = {
+        "camera": {"position": [0, 0.5, 6], "aspectRatio": 1.5},
+        "objects": [sph((0, -1e6 - 1, 0), 1e6, lamb), sph((-1.5, 0, 0), 1, metal), sph((1.2, -0.2, 0.5), 0.8, glass),
+                    sph((0, 0.4, -2), 1.4, mirror),
+                    {"type": "cube", "position": [2.6, -0.5, 1.0], "size": [1, 1, 1], "material": metal}],
+        "lights": [{"position": [5, 8, 6], "color": [1, 1, 1], "intensity": 80},
+                   {"position": [-4, 2, 3], "color": [1, 0.8, 0.7], "intensity": 30}],
+    }
+    # the same scene around (1e5, 1e5, 1e5): camera, objects and lights
+    off = (1e5, 1e5, 1e5)
+
+    def shift(sc):
+        sc = json.loads(json.dumps(sc))
+        sc["camera"]["position"] = [a + b for a, b in zip(sc["camera"]["position"], off)]
+        for o in sc["objects"]:
+            o["position"] = [a + b for a, b in zip(o["position"], off)]
+        for li in sc["lights"]:
+            li["position"] = [a + b for a, b in zip(li["position"], off)]
+        return sc
+
+    far = shift(out["huge_ground"])
+    far["objects"][0]["radius"] = 1e3  # (a 1e6 ground at 1e5 would swallow the camera)
+    far["objects"][0]["position"][1] = off[1] - 1e3 - 1
+    out["far_coordinates"] = far
+    # radius-1e-3 spheres seen from 2 cm (culling margins of tiny bounding spheres)
+    tiny = []
+    for i in range(40):
+        x = ((i * 37) % 13 - 6) * 2.3e-3
+        y = ((i * 11) % 9 - 4) * 2.1e-3
+        z = -0.02 - (i % 5) * 1.7e-3
+        tiny.append(sph((x, y, z), 1e-3, [metal, glass, lamb, mirror][i % 4]))
+    tiny.append(sph((0, -1e3 - 0.02, 0), 1e3, lamb))
+    out["tiny_spheres"] = {
+        "camera": {"position": [0, 0, 0], "aspectRatio": 1.5},
+        "objects": tiny,
+        "lights": [{"position": [0.01, 0.02, -0.01], "color": [1, 1, 1], "intensity": 0.002},
+                   {"position": [-0.02, 0.01, 0.0], "color": [1, 0.9, 0.8], "intensity": 0.001}],
+    }
+    # lights 2e-3 and 5e-4 (< 0.001: skipped by renderer.go:252-254) above surfaces
+    out["light_on_surface"] = {
+        "camera": {"position": [0, 0.5, 6], "aspectRatio": 1.5},
+        "objects": [sph((0, -1001, 0), 1000, lamb), sph((0, 0, 0), 1, metal), sph((2.2, 0, 0), 0.9, glass),
+                    sph((-2.2, 0, 0), 0.9, lamb)],
+        "lights": [{"position": [0, 1.002, 0], "color": [1, 1, 1], "intensity": 2},
+                   {"position": [2.2, 0.9005, 0], "color": [1, 1, 1], "intensity": 2},
+                   {"position": [-2.2, -0.1, 0.902], "color": [1, 0.7, 0.6], "intensity": 3},
+                   {"position": [0, -0.998, 3], "color": [0.5, 0.5, 1], "intensity": 5}],
+    }
+    return out
+
+
+EDGE_SCENES = _edge_scenes()

@@ -84,3 +84,63 @@ def test_path_counts_match_oracle(case):
     for k in ("camera_rays", "bounce_rays", "shadow_rays", "shade_events", "light_evals", "rng_draws"):
         assert cg[k] == cr[k], (name, k, cg[k], cr[k])
     ctx.close()
+
+
+@pytest.mark.parametrize("name", sorted(__import__("scene_cases").EDGE_SCENES))
+def test_culling_edge_scenes_match_oracle(name):
+    """Huge radii, far coordinates, tiny spheres and lights almost on a
+    surface: the exact-culling margins (relative) must never drop a
+    primitive that can be hit (scene_cases._edge_scenes)."""
+    import json
+
+    from scene_cases import EDGE_SCENES
+
+    scene = rtgo.Scene.from_json_text(json.dumps(EDGE_SCENES[name]))
+    for seed in (1, 2):
+        st = make_settings(rtgo, {"samples": 4}, seed)
+        lin_g, rgba_g = _render_gpu(scene, 72, 48, st)
+        lin_r, rgba_r, _ = oracle.render(scene, 72, 48, st)
+        rmse, maxd, rgba_mis = _compare(lin_g, rgba_g, lin_r, rgba_r)
+        print(f"{name} seed={seed} rmse={rmse} max|d|={maxd:.3e} lit={np.mean(rgba_r[..., :3] > 0):.3f}")
+        assert maxd == 0.0 and rgba_mis == 0.0, (name, seed, maxd, rgba_mis)
+
+
+SKY_CASES = [("all_materials", ("json", None), 64, 48, "default"), ("silver_facing",
+             ("file", "final_silver_prism_purple_cube_facing.json"), 64, 48, "sunset"),
+             ("spheres_facing", ("file", "sphere_reflections_light_facing.json"), 64, 48, "night"),
+             ("spheres_facing_white", ("file", "sphere_reflections_light_facing.json"), 48, 32, "white")]
+
+
+@pytest.mark.parametrize("case", SKY_CASES, ids=[c[0] for c in SKY_CASES])
+def test_opt_in_sky_matches_oracle(case):
+    """rt_settings.sky (off by default): a miss returns GetSkyColor
+    (atmosphere.go:100-135) instead of black, on the megakernel path.
+    Tolerance: the sky's exp / pow come from the device and host libm,
+    which may differ in the last bit of a binary64; asserted per-channel
+    RMSE < 1e-7 of the float32 output (the north star allows 1e-4)."""
+    name, loader, w, h, sky = case
+    scene = load_case(rtgo, loader)
+    st = make_settings(rtgo, {"samples": 4}, 3)
+    st.sky = rtgo.SKIES[sky]
+    lin_g, rgba_g = _render_gpu(scene, w, h, st)
+    lin_r, rgba_r, _ = oracle.render(scene, w, h, st)
+    rmse, maxd, rgba_mis = _compare(lin_g, rgba_g, lin_r, rgba_r)
+    print(f"sky {sky} {name}: rmse={rmse} max|d|={maxd:.3e} rgba_mismatch={rgba_mis:.2e}")
+    assert np.all(rmse < 1e-7) and maxd < 1e-6 and rgba_mis < 1e-3
+    assert np.all(lin_r[0, :, :] >= 0.0) and (rgba_r[..., :3] > 0).mean() > 0.9  # the sky is visible
+
+
+def test_opt_in_sky_on_the_wavefront_path():
+    """The same on the BVH + wavefront path (a 300-sphere field)."""
+    import json
+
+    from test_gpu_paths import _sphere_field
+
+    scene = rtgo.Scene.from_json_text(json.dumps(_sphere_field(300, seed=5)))
+    st = make_settings(rtgo, {"samples": 3}, 2)
+    st.sky = rtgo.SKIES["default"]
+    lin_g, rgba_g = _render_gpu(scene, 60, 40, st)
+    lin_r, rgba_r, _ = oracle.render(scene, 60, 40, st)
+    rmse, maxd, rgba_mis = _compare(lin_g, rgba_g, lin_r, rgba_r)
+    print(f"wavefront sky: rmse={rmse} max|d|={maxd:.3e} rgba_mismatch={rgba_mis:.2e}")
+    assert np.all(rmse < 1e-7) and maxd < 1e-6 and rgba_mis < 1e-3

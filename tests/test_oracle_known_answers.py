@@ -245,3 +245,46 @@ def test_perfect_mirror_blend_uses_folded_constant():  # advanced_materials.go:1
     F = f0 + (1.0 - f0) * _pow5(1.0 - 1.0)
     # Go folds the untyped constant (1.0 - 0.9) to exactly float64(0.1)
     assert ok and draws == 0 and att == tuple(c * 0.1 + F * 0.9 for c in col)
+
+
+def _go_sky(preset, d):
+    """GetSkyColor (internal/atmosphere/atmosphere.go:100-135) restated in
+    Python, FastVec3* as the Vec3 methods (a.Lerp(b, t) = a + (b - a) t)."""
+    import math
+
+    P = {  # atmosphere.go:28-98: top, bottom, sun dir, sun colour, sun intensity, size, rayleigh, mie, depth,
+        #    fog density, fog colour, time of day
+        1: ((0.6, 0.8, 1.0), (0.9, 0.95, 1.0), (0.0, 0.8, -0.6), (1.0, 0.98, 0.95), 1.2, 0.015, (0.6, 0.8, 1.0),
+            (1.0, 0.98, 0.95), 0.3, 0.0, (0.9, 0.92, 0.95), 0.6),
+        3: ((1.0, 0.4, 0.2), (1.0, 0.8, 0.6), (0.0, 0.3, -0.9), (1.0, 0.6, 0.3), 1.2, 0.03, (1.0, 0.4, 0.2),
+            (1.0, 0.8, 0.6), 0.8, 0.1, (1.0, 0.8, 0.6), 0.8),
+    }[preset]
+    top, bot, sd, sc, si_, ss, ray, mie, depth_k, fog, fogc, tod = P
+    lerp = lambda a, b, t: tuple(x + (y - x) * t for x, y in zip(a, b))  # noqa: E731
+    ln = math.sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2])
+    u = tuple(x / ln for x in d)
+    c = lerp(bot, top, 0.5 * (u[1] + 1.0))
+    atm = math.exp(-max(0.0, u[1]) * depth_k)
+    c = lerp(c, lerp(ray, mie, atm), 0.25)
+    dot = u[0] * sd[0] + u[1] * sd[1] + u[2] * sd[2]
+    if dot > 1.0 - ss:
+        s = min((dot - (1.0 - ss)) / ss ** 1.0, 1e300) ** 1.5
+        c = lerp(c, sc, min(s, 1.0) * si_ * 0.9)
+    tf = tod if tod <= 0.5 else 1.0 - tod
+    c = tuple(x * (1.0 - tf * 2.0 * 0.3) for x in c)
+    if fog > 0:
+        c = lerp(fogc, c, math.exp(-fog))
+    return tuple(max(0.1, min(0.98, x)) for x in c)
+
+
+@pytest.mark.parametrize("preset", [1, 3])
+@pytest.mark.parametrize("d", [(0, 1, 0), (0, -1, 0), (0.3, 0.2, -1), (0.0, 0.8, -0.6), (0.0, 0.31, -0.9),
+                               (1e-3, 0.8, -0.6)])
+def test_sky_color_matches_restatement(preset, d):
+    import ctypes
+
+    out = (ctypes.c_double * 3)()
+    oracle.lib().oracle_sky_color.argtypes = [ctypes.c_int, ctypes.c_double * 3, ctypes.c_double * 3]
+    oracle.lib().oracle_sky_color(preset, (ctypes.c_double * 3)(*d), out)
+    want = _go_sky(preset, d)
+    assert max(abs(a - b) for a, b in zip(out, want)) < 1e-14, (tuple(out), want)

@@ -44,3 +44,19 @@ def test_ten_thousand_spheres_load(tmp_path):
     v = s.view
     assert v.num_objects == 10000 and v.num_lights == 2
     assert json.loads(p.read_text())["camera"]["aspectRatio"] == 1.78
+
+
+def test_edge_scenes_are_not_black():
+    """The culling edge scenes (GPU parity) actually show their objects."""
+    import json
+
+    import numpy as np
+
+    import oracle
+    import rtgo
+    from scene_cases import EDGE_SCENES, make_settings
+
+    for name, sc in EDGE_SCENES.items():
+        scene = rtgo.Scene.from_json_text(json.dumps(sc))
+        lin, rgba, _ = oracle.render(scene, 36, 24, make_settings(rtgo, {"samples": 1, "max_depth": 8}))
+        assert np.mean(rgba[..., :3] > 0) > 0.2, name
