@@ -96,7 +96,7 @@ double oracle_go_pow(double x, double y) {
       ae += xe;
     }
     x1 *= x1;
-    xe <<= 1;
+    xe *= 2; /* Go's xe <<= 1 on a negative int (two's complement); a left shift of a negative value is UB in C */
     if (x1 < .5) {
       x1 += x1;
       xe--;
