@@ -153,7 +153,7 @@ int rt_context_set_tuning(rt_context* c, const rt_tuning* t) {
     set_error("tuning.path must be RT_PATH_AUTO or RT_PATH_MEGAKERNEL");
     return RT_E_INVALID;
   }
-  if (t->pilot_depth < 0 || t->bvh_leaf < 0 || t->bvh_leaf > 7 || t->bvh_bins < 0 || t->block_work < 0 || t->block_samples < 0 ||
+  if (t->pilot_depth < 0 || t->split_samples < 0 || t->split_samples > 64 || t->bvh_leaf < 0 || t->bvh_leaf > 7 || t->bvh_bins < 0 || t->block_work < 0 || t->block_samples < 0 ||
       t->wf_paths < 0 || t->wf_chunk < 0 || t->wf_trav_block < 0 || t->wf_trav_block > 1024 || t->wf_trav_wgs < 0) {
     set_error("tuning value out of range");
     return RT_E_INVALID;
@@ -363,7 +363,8 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
   const bool frustum = tn.frustum != 0 && !sky;
   const int64_t key[13] = {(int64_t)c->scene_gen, w, h, rank, world, st->samples, st->max_depth,
                            st->recursive_reflections, st->soft_shadows, bigP, (int64_t)(block_work * 16),
-                           pilot ? 1 + tn.pilot_depth : 0, (frustum ? 1 : 0) | (sky ? 2 : 0)};
+                           (pilot ? 1 + tn.pilot_depth : 0) | (int64_t)tn.split_samples << 16,
+                           (frustum ? 1 : 0) | (sky ? 2 : 0)};
   const bool masks = f.bvh.empty() && f.spheres.size() <= 64 && f.tris.size() <= 64;
   if (memcmp(key, c->order_key, sizeof key) != 0) {
     int rc = quiesce(c);  // the last render may still read the blocks, masks and split rows
@@ -402,6 +403,7 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
     sp.spp = st->samples;
     sp.big_pixels = bigP;
     sp.frustum = frustum;
+    sp.split_samples = tn.split_samples > 0 ? std::min(64, tn.split_samples) : 64;
     sp.block_work = block_work;
     sp.tile_masks = c->d_masks;
     sp.tile_cost = d_cost;

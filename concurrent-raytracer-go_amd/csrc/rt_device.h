@@ -640,7 +640,9 @@ __device__ __forceinline__ double go_min2(double x, double y) {
 // methods (vector.go): Normalize (0 for a zero vector), a.Lerp(b, t) =
 // a + (b - a) * t, Dot, MulScalar; Max / Min with Go's NaN rules; Clamp(0.1, 0.98).
 __device__ __forceinline__ d3 sky_lerp(d3 a, d3 b, double t) { return a + muls(b - a, t); }
-__device__ __noinline__ d3 sky_color(const DSky* __restrict__ a, d3 dir) {
+// (inlined: a call in the bounce loop would impose the call ABI's register
+// split on the whole kernel; this code only runs on a miss with a sky)
+__device__ __forceinline__ d3 sky_color(const DSky* __restrict__ a, d3 dir) {
   const d3 u = normalize(dir);
   const double t = 0.5 * (u.y + 1.0);
   d3 sky = sky_lerp(ld3(a->bottom), ld3(a->top), t);

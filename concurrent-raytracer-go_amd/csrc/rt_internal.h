@@ -60,6 +60,7 @@ struct SchedParams {
   double vw;                   // viewport width 2 * aspect (getRay, renderer.go:377-390)
   int32_t W, H, rank, world, tiles_x, ntiles, local;
   int32_t spp, big_pixels, frustum;
+  int32_t split_samples;       // samples per sub-block of a split pixel (<= 64: one path per lane)
   double block_work;
   const unsigned long long* tile_masks;  // per local tile (2 u64) or null (no primary culling)
   const float* tile_cost;      // per local tile: projected primitives (estimate without a pilot)

@@ -44,8 +44,9 @@
 
 // waves per SIMD of render_kernel: measured best of 2/3/4 (4 spills the FP64 path state)
 #define RT_WAVES_PER_SIMD 3
-// cooperative soft shadows when at most this many lanes need them (best of 0/2/4/8)
-#define RT_COOP_MAX 8
+// cooperative soft shadows when at most this many lanes need them (measured
+// best of 0/2/4/8 in round 1; 4 and 16 within noise in round 2)
+constexpr int kCoopMax = 8;
 
 namespace rtgo {
 
@@ -293,7 +294,7 @@ __device__ __forceinline__ CoopOut soft_coop(const Geo p, bool masks, bool trace
   return CoopOut{x, unocc, tries};
 }
 
-// Queue form for many owners (more than RT_COOP_MAX lanes need soft
+// Queue form for many owners (more than kCoopMax lanes need soft
 // shadows for this light), executed by the whole converged wave.  Each
 // owner runs its own rejection tries on its own stream, in order (the same
 // draws as 16 calls of RandomVec3InUnitSphere); an accepted point is
@@ -488,7 +489,7 @@ __device__ __forceinline__ void camera_ray(KArg k, int x, int y, int s, rt_rng& 
 //       linear + RGBA8).
 constexpr int kRound = 128;  // list entries shaded per round (LDS radiance slots)
 
-template <bool kCount, bool kStage, bool kPilot>
+template <bool kCount, bool kStage, bool kPilot, bool kSky>
 __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KParams pk) {
   __shared__ uint32_t hbits[kMaxBlockSamples / 32];  // hit samples of the block
   __shared__ int hoff[kMaxBlockSamples / 32 + 1];    // list offset of each bit word; [words] = #hits
@@ -574,7 +575,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     const int NL = kCount ? NB : (loc.black ? 0 : nlive * ns);
     // with an opted-in sky a miss returns the sky (not +0): every camera
     // sample is shaded (no culling applies: the host disables the masks)
-    const bool sky = k->sky != nullptr;
+    constexpr bool sky = kSky;
     for (int j = lane; j < NL; j += 64) {
       // j -> (pixel, sample): every sample of the block (kCount) or of its
       // live pixels, in order
@@ -779,9 +780,8 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
         }
         if (done) {
           fin = true;
-          if (missed) {  // an opted-in sky instead of black (rt_settings.sky)
-            const DSky* sky = fresh()->sky;
-            if (sky) L = L + mul(T, sky_color(sky, d));
+          if constexpr (kSky) {  // an opted-in sky instead of black (rt_settings.sky)
+            if (missed) L = L + mul(T, sky_color(fresh()->sky, d));
           }
         } else {
           shade = true;
@@ -881,9 +881,10 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
 #endif
           if (owners != 0) {
 #ifdef RT_WG_TIMING
-            if (__popcll(owners) <= RT_COOP_MAX) dbg_coop += __popcll(owners); else ++dbg_seq;
+            if (__popcll(owners) <= kCoopMax) dbg_coop += __popcll(owners); else ++dbg_seq;
 #endif
-            if (__popcll(owners) <= RT_COOP_MAX) {
+            // cooperative soft shadows when at most kCoopMax lanes need them
+            if (__popcll(owners) <= kCoopMax) {
               for (unsigned long long b = owners; b; b &= b - 1) {
                 const int ow = __builtin_ctzll(b);
                 const CoopOut r = soft_coop<kCount>(
@@ -1087,19 +1088,26 @@ int launch_render(const KParams& p, bool count, void* stream) {
   const size_t shmem = render_shmem(p);
   const bool stage = p.stage_bytes > 0;
   const dim3 g(p.num_wgs), b(64);
+  // (the opted-in sky has instantiations of its own: its code would cost the
+  // others registers; the pilot and the counting variant ignore it -- path
+  // lengths and counts do not depend on what a miss returns)
   if (p.tile_work) {  // the scheduler's pilot render: its own instantiation (and kernel name)
     if (stage)
-      hipLaunchKernelGGL((render_kernel<false, true, true>), g, b, shmem, st, p);
+      hipLaunchKernelGGL((render_kernel<false, true, true, false>), g, b, shmem, st, p);
     else
-      hipLaunchKernelGGL((render_kernel<false, false, true>), g, b, shmem, st, p);
+      hipLaunchKernelGGL((render_kernel<false, false, true, false>), g, b, shmem, st, p);
   } else if (count && stage) {
-    hipLaunchKernelGGL((render_kernel<true, true, false>), g, b, shmem, st, p);
+    hipLaunchKernelGGL((render_kernel<true, true, false, false>), g, b, shmem, st, p);
   } else if (count) {
-    hipLaunchKernelGGL((render_kernel<true, false, false>), g, b, shmem, st, p);
+    hipLaunchKernelGGL((render_kernel<true, false, false, false>), g, b, shmem, st, p);
+  } else if (p.sky && stage) {
+    hipLaunchKernelGGL((render_kernel<false, true, false, true>), g, b, shmem, st, p);
+  } else if (p.sky) {
+    hipLaunchKernelGGL((render_kernel<false, false, false, true>), g, b, shmem, st, p);
   } else if (stage) {
-    hipLaunchKernelGGL((render_kernel<false, true, false>), g, b, shmem, st, p);
+    hipLaunchKernelGGL((render_kernel<false, true, false, false>), g, b, shmem, st, p);
   } else {
-    hipLaunchKernelGGL((render_kernel<false, false, false>), g, b, shmem, st, p);
+    hipLaunchKernelGGL((render_kernel<false, false, false, false>), g, b, shmem, st, p);
   }
   return (int)hipGetLastError();
 }

@@ -300,7 +300,7 @@ __global__ __launch_bounds__(64) void sched_blocks(const SchedParams p) {
         if ((m >> k) & 1) q = s_J[k][q];
       const int e = s_J[0][q];
       if (p.spp > 1 && S * (double)est[q] > bw) {  // a split pixel (e == q + 1): sample ranges of <= 64
-        const int nsub = (p.spp + 63) / 64;
+        const int nsub = (p.spp + p.split_samples - 1) / p.split_samples;
         const int ord = atomicAdd(&s_nsplit, 1);
         for (int j = 0; j < nsub; ++j) {
           const int s0 = (int)((long long)p.spp * j / nsub), s1 = (int)((long long)p.spp * (j + 1) / nsub);

@@ -59,7 +59,11 @@ constexpr int kTravBlock = kWfTravBlock;
 constexpr int kLdsBytes = 160 * 1024;    // LDS per CU (MI355X), all of it available to one workgroup
 constexpr int kRefill = 16;              // persistent traversal: refill once this many lanes are idle
 constexpr int kChunk = 256;              // persistent traversal: jobs a wave takes per atomic
-constexpr uint32_t kHardBit = 1u << 16;  // lstate: the hard shadow ray is blocked (low bits: blocked soft rays)
+constexpr uint32_t kHardBit = 1u << 16;
+// hidx of a path whose ray hit nothing while a sky is opted in: wf_shade1
+// ends it with the sky's radiance (GetSkyColor, atmosphere.go:100-135) --
+// kept out of the traversal kernel, whose registers it would cost
+constexpr int kSkyMiss = -2;  // lstate: the hard shadow ray is blocked (low bits: blocked soft rays)
 
 extern __shared__ __attribute__((aligned(16))) unsigned char wf_lds[];
 
@@ -413,13 +417,10 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
           }
         }
         if (miss) {
-          p.hidx[slot] = -1;
-          if (sid != kDeadSid) {
-            d3 L = mk(a.lx[slot], a.ly[slot], a.lz[slot]);
-            if (p.sky && a.depth[slot] < p.max_depth)  // the root box missed: the sky (opt-in)
-              L = L + mul(mk(a.tx[slot], a.ty[slot], a.tz[slot]), sky_color(p.sky, ld_d(a, slot)));
-            finish(p, sid, L);
-          }
+          // the root box missed: with an opted-in sky, shade1 adds it (kSkyMiss)
+          const bool sky = p.sky && sid != kDeadSid && a.depth[slot] < p.max_depth;
+          p.hidx[slot] = sky ? kSkyMiss : -1;
+          if (sid != kDeadSid && !sky) finish(p, sid, mk(a.lx[slot], a.ly[slot], a.lz[slot]));
         }
       }
     }
@@ -453,11 +454,11 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
         if (best_obj >= 0) {
           p.hidx[slot] = bidx;
           p.hnum[slot] = bnum;
+        } else if (p.sky) {  // a miss with an opted-in sky: shade1 adds it
+          p.hidx[slot] = kSkyMiss;
         } else {
           p.hidx[slot] = -1;
-          d3 L = mk(a.lx[slot], a.ly[slot], a.lz[slot]);
-          if (p.sky) L = L + mul(mk(a.tx[slot], a.ty[slot], a.tz[slot]), sky_color(p.sky, d));  // opt-in sky
-          finish(p, a.sid[slot], L);
+          finish(p, a.sid[slot], mk(a.lx[slot], a.ly[slot], a.lz[slot]));
         }
       }
     }
@@ -486,6 +487,11 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade1(const WfParams p) {
     slot = dense_at(dn, j, p.shard_cap);
     const int hi = p.hidx[slot];
     hit = hi >= 0;
+    if (hi == kSkyMiss) {  // (opt-in sky) the path ends: L + T * sky(direction)
+      const WfPaths& a = p.cur;
+      const d3 L = mk(a.lx[slot], a.ly[slot], a.lz[slot]), T = mk(a.tx[slot], a.ty[slot], a.tz[slot]);
+      finish(p, a.sid[slot], L + mul(T, sky_color(p.sky, ld_d(a, slot))));
+    }
     if (hit) {
       cnt<kCount>(c, C_SHADE);
       const WfPaths& a = p.cur;

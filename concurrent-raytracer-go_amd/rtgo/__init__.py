@@ -136,6 +136,8 @@ class Tuning(ctypes.Structure):
         ("wf_trav_block", ctypes.c_int32),
         ("wf_trav_wgs", ctypes.c_int32),
         ("pilot_depth", ctypes.c_int32),
+        ("split_samples", ctypes.c_int32),
+        ("_pad", ctypes.c_int32),
     ]
 
 

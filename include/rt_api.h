@@ -261,6 +261,8 @@ typedef struct {
   int32_t wf_trav_block;  /* threads per traversal workgroup (64..1024); 0: 1024 */
   int32_t wf_trav_wgs;    /* traversal workgroups sharing a CU's LDS; 0: 1 */
   int32_t pilot_depth;    /* bounces the pilot render follows a path at most (default 12); 0: max_depth */
+  int32_t split_samples;  /* samples per sub-block of a split (heavy) pixel, 1..64; 0: 64 */
+  int32_t _pad;
 } rt_tuning;
 void rt_tuning_default(rt_tuning* t);
 /* Applies to later rt_context_set_scene (BVH shape) and render calls. */

@@ -19,6 +19,9 @@ import rtgo  # noqa: E402
 scene = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "scenes", "sphere_reflections_light_facing.json")
 W, H, SPP = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (800, 600, 100)
 ctx = rtgo.Context(0)
+if os.environ.get("WG_TUNING"):  # e.g. WG_TUNING="split_samples=16,block_work=256"
+    ctx.set_tuning(rtgo.default_tuning(**{k: float(v) if "." in v else int(v) for k, v in
+                                          (kv.split("=") for kv in os.environ["WG_TUNING"].split(","))}))
 if scene == "spheres10k":  # config C4/C5 scene (scenes/gen_spheres.py)
     import importlib.util
     _spec = importlib.util.spec_from_file_location("g", os.path.join(ROOT, "scenes", "gen_spheres.py"))

@@ -20,6 +20,7 @@ SCHEDULES = [
     ("every_pixel_split", {"block_work": 1}),         # nearly every pixel split into sample ranges
     ("huge_blocks", {"block_work": 1e6}),            # the largest blocks everywhere
     ("small_blocks", {"block_samples": 100}),        # few samples per large block
+    ("split_by_8", {"block_work": 64, "split_samples": 8}),  # heavy pixels in sub-blocks of <= 8 samples
     ("no_pilot", {"pilot": 0}),                      # geometric estimate only
     ("no_frustum_no_stage", {"frustum": 0, "stage": 0}),
 ]
