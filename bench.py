@@ -83,9 +83,9 @@ CONFIGS = {
     "c5": ("gen:10000", 3840, 2160, 256, "procedural 10k spheres (scenes/gen_spheres.py, BVH)", 1, 1),
 }
 KERNELS = {  # the dominant kernel of each config (rocprofv3 --stats, profiles/)
-    "c2": "rtgo::render_kernel<false, true, false>",
-    "c2_committed": "rtgo::render_kernel<false, true, false>",
-    "c3": "rtgo::render_kernel<false, true, false>",
+    "c2": "rtgo::render_kernel<false, true, false, false>",
+    "c2_committed": "rtgo::render_kernel<false, true, false, false>",
+    "c3": "rtgo::render_kernel<false, true, false, false>",
     "c4": "wavefront bounce loop (wf_occlude<false, true, true> dominant)",
     "c5": "wavefront bounce loop (wf_occlude<false, true, true> dominant)",
 }

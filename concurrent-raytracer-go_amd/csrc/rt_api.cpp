@@ -124,8 +124,14 @@ struct rt_context {
   int32_t nsplit = 0;       // split pixels of the current schedule
   char* d_split = nullptr;  // their per-sample radiance rows + sub-block counters
   size_t split_cap = 0;
-  char* d_pilot = nullptr;  // pilot render scratch: packed float3 + rgba + path lengths
+  char* d_pilot = nullptr;  // pilot render scratch: packed float3 + rgba + path lengths (max, sum)
   size_t pilot_cap = 0;
+  // measured schedule (rt_tuning.measure): 0 none, 1 the next render measures
+  // every pixel's paths into d_meas (max | sum), 2 measured (the next
+  // schedule is re-cut from them), 3 done
+  int meas_state = 0;
+  char* d_meas = nullptr;
+  size_t meas_cap = 0;
   char* d_sched = nullptr;  // scheduler scratch (sched_layout) + the per-tile inputs
   size_t sched_cap = 0;
   int32_t* h_totals = nullptr;  // pinned: block and split counts of the last schedule
@@ -213,6 +219,7 @@ void rt_context_destroy(rt_context* c) {
 
   if (c->d_blocks) (void)hipFree(c->d_blocks);
   if (c->d_pilot) (void)hipFree(c->d_pilot);
+  if (c->d_meas) (void)hipFree(c->d_meas);
   if (c->d_split) (void)hipFree(c->d_split);
   if (c->d_sched) (void)hipFree(c->d_sched);
   if (c->h_totals) (void)hipHostFree(c->h_totals);
@@ -354,7 +361,10 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
   // path bounces per block: 8 full-wave bounce steps; 16x that with a BVH,
   // whose bounces are long divergent traversals that need full waves more
   // than short blocks (C4: 2.10 s at 512, 1.77 s at 8192)
-  double block_work = f.bvh.empty() ? 512.0 : 8192.0;
+  // (triangle scenes: 256 -- a bounce there tests 12 triangles per cube, so
+  // fewer bounces make a block: silver C3 0.56 -> 0.46 ms; the sphere
+  // headline is best at 512: 0.80 vs 0.93 ms at 256)
+  double block_work = !f.bvh.empty() ? 8192.0 : (f.tris.empty() ? 512.0 : 256.0);
   if (tn.block_work > 0) block_work = std::max(1.0, tn.block_work);
   const bool pilot = tn.pilot != 0;
   // a sky makes every camera sample count (a miss returns the sky, not +0):
@@ -364,9 +374,12 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
   const int64_t key[13] = {(int64_t)c->scene_gen, w, h, rank, world, st->samples, st->max_depth,
                            st->recursive_reflections, st->soft_shadows, bigP, (int64_t)(block_work * 16),
                            (pilot ? 1 + tn.pilot_depth : 0) | (int64_t)tn.split_samples << 16,
-                           (frustum ? 1 : 0) | (sky ? 2 : 0)};
+                           (frustum ? 1 : 0) | (sky ? 2 : 0) | (tn.measure ? 4 : 0) | (int64_t)tn.split_depth << 8};
   const bool masks = f.bvh.empty() && f.spheres.size() <= 64 && f.tris.size() <= 64;
-  if (memcmp(key, c->order_key, sizeof key) != 0) {
+  const bool new_key = memcmp(key, c->order_key, sizeof key) != 0;
+  // a measured re-cut: the previous frame of this key measured every pixel
+  const bool remeasured = !new_key && c->meas_state == 2;
+  if (new_key || remeasured) {
     int rc = quiesce(c);  // the last render may still read the blocks, masks and split rows
     if (rc) return rc;
     const int local = rt_tiles_for_rank(w, h, rank, world);
@@ -412,11 +425,16 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
       set_error(std::string("schedule launch failed: ") + hipGetErrorString((hipError_t)e));
       return RT_E_DEVICE;
     }
-    if (pilot && local > 0 && st->samples > 0 && st->max_depth > 0) {
+    sp.split_depth = tn.split_depth > 0 ? tn.split_depth : 16;
+    if (remeasured) {  // every sample's path of the last frame (the measuring render)
+      sp.work_max = (const unsigned int*)c->d_meas;
+      sp.work_sum = sp.work_max + (size_t)local * 1024;
+      sp.work_n = st->samples;
+    } else if (pilot && local > 0 && st->samples > 0 && st->max_depth > 0) {
       // one sample per pixel, blocks of 64 pixels, packed output into scratch
       const size_t npx = (size_t)local * 1024;
-      rc = grow(&c->d_pilot, &c->pilot_cap, npx * 20 + 256);
-    if (rc) return rc;
+      rc = grow(&c->d_pilot, &c->pilot_cap, npx * 24 + 256);
+      if (rc) return rc;
       float* plin = (float*)c->d_pilot;
       uint8_t* prgba = (uint8_t*)c->d_pilot + npx * 12;
       unsigned int* plen = (unsigned int*)((uint8_t*)c->d_pilot + npx * 16);
@@ -430,20 +448,23 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
       q.out_rgba = prgba;
       q.counts = nullptr;
       q.dbg = nullptr;
-      q.tile_work = plen;
+      q.work_max = plen;
+      q.work_sum = plen + npx;
       q.soft = 0;  // path lengths only (see above)
       if (tn.pilot_depth > 0) q.max_depth = std::min(q.max_depth, tn.pilot_depth);
       q.tile_masks = c->d_masks;
       q.split_rad = nullptr;
       q.split_hits = nullptr;
       q.split_cnt = nullptr;
-      HIP_TRY(hipMemsetAsync(plen, 0, npx * sizeof(unsigned int), s));
+      HIP_TRY(hipMemsetAsync(plen, 0, 2 * npx * sizeof(unsigned int), s));
       e = launch_render(q, false, s);
       if (e != hipSuccess) {
         set_error(std::string("pilot launch failed: ") + hipGetErrorString((hipError_t)e));
         return RT_E_DEVICE;
       }
-      sp.plen = plen;
+      sp.work_max = plen;
+      sp.work_sum = plen + npx;
+      sp.work_n = 1;
     }
     e = sched_launch_blocks(sp, false, s);
     if (e != hipSuccess) {
@@ -467,6 +488,8 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
     c->num_blocks = nblocks;
     c->nsplit = nsplit;
     memcpy(c->order_key, key, sizeof key);
+    // a new key's first frame measures (state 1), the next re-cuts (2 -> 3)
+    c->meas_state = remeasured ? 3 : (tn.measure && local > 0 ? 1 : 0);
   }
   p->blocks = c->d_blocks;
   p->num_blocks = c->num_blocks;
@@ -731,9 +754,22 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
     if (rc) return rc;
   }
   p.num_wgs = p.num_blocks;
+  // the first frame of a new schedule measures every pixel's paths (the same
+  // image; a separate instantiation records the lengths): the next frame's
+  // blocks are cut from them (prepare_schedule)
+  bool measuring = false;
+  if (!wf && c->meas_state == 1 && !counts && st->sky == RT_SKY_NONE && p.num_blocks > 0) {
+    const size_t npx = (size_t)rt_tiles_for_rank(w, h, rank, world) * 1024;
+    rc = grow(&c->d_meas, &c->meas_cap, npx * 8);
+    if (rc) return rc;
+    p.work_max = (unsigned int*)c->d_meas;
+    p.work_sum = p.work_max + npx;
+    measuring = true;
+  }
   if (counts) HIP_TRY(hipMemsetAsync(c->d_counts, 0, 16 * sizeof(unsigned long long), s));
   if (!wf && c->nsplit)  // split pixels: hit bits and sub-block counters start at zero
     HIP_TRY(hipMemsetAsync(p.split_hits, 0, split_flags_bytes(c->nsplit, st->samples), s));
+  if (measuring) HIP_TRY(hipMemsetAsync(c->d_meas, 0, (size_t)rt_tiles_for_rank(w, h, rank, world) * 1024 * 8, s));
   HIP_TRY(hipEventRecord(c->ev0, s));
   if (wf) {
     rc = render_wavefront(c, p, st, s, counts != nullptr);
@@ -746,6 +782,7 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
     }
   }
   HIP_TRY(hipEventRecord(c->ev1, s));
+  if (measuring) c->meas_state = 2;
   c->last_stream = s;
   c->have_timing = true;
   if (counts) {

@@ -64,7 +64,10 @@ struct SchedParams {
   double block_work;
   const unsigned long long* tile_masks;  // per local tile (2 u64) or null (no primary culling)
   const float* tile_cost;      // per local tile: projected primitives (estimate without a pilot)
-  const unsigned int* plen;    // pilot path length per local pixel, or null (no pilot)
+  const unsigned int* work_max;  // measured per local pixel: the longest path (bounces + 1) ...
+  const unsigned int* work_sum;  // ... and the sum over the measured samples, or null (no measurement)
+  int32_t work_n;              // samples measured per pixel (1..16: a pilot; spp: a whole frame)
+  int32_t split_depth;         // a pixel whose longest path has this many bounces is split (measured frames)
   // scratch (sched_layout)
   unsigned long long* pixmask; // per local pixel: 2 u64
   float* est;                  // per local pixel: estimated work of one sample
@@ -115,7 +118,8 @@ struct KParams {
   double* split_rad;           // split pixels: [slot][spp][3] radiance of the hit samples
   uint32_t* split_hits;        // split pixels: [slot][(spp+31)/32] hit-sample bits (zeroed per launch)
   int32_t* split_cnt;          // split pixels: sub-blocks finished (zeroed per launch)
-  unsigned int* tile_work;     // pilot renders (spp 1, 64-pixel blocks): per pixel, its path length (else null)
+  unsigned int* work_max;      // measuring renders: per local pixel, its longest path (bounces + 1) ...
+  unsigned int* work_sum;      // ... and the bounces + 1 of all its samples' paths (else null)
   const unsigned long long* tile_masks;  // per local tile: primary-ray candidate masks (spheres, tris) or null
   const DSky* sky;             // miss radiance (rt_settings.sky) or null: black (renderer.go:170-173)
   const void* stage_src;       // start of the scene prefix staged into LDS (spheres..lights)

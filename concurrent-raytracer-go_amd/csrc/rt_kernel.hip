@@ -951,8 +951,13 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
 #endif
       }
       if (fin) {  // the path's radiance goes to its entry's ring slot
-        if constexpr (kPilot)  // pilot render (one sample per pixel): the path's length
-          fresh()->tile_work[blockIdx.x * 64 + entry_id(entry)] = depth + 1;
+        if constexpr (kPilot) {  // a measuring render: the pixel's longest path and its bounces
+          KArg k = fresh();
+          const BlockLoc loc = block_loc(k, blockIdx.x);
+          const size_t px = (size_t)loc.lt * 1024 + loc.p0 + entry_id(entry) / loc.ns;
+          atomicMax(k->work_max + px, (unsigned)depth + 1u);
+          atomicAdd(k->work_sum + px, (unsigned)depth + 1u);
+        }
         const int q = entry & (kRound - 1);
         slot[q][0] = L.x;
         slot[q][1] = L.y;
@@ -1091,7 +1096,7 @@ int launch_render(const KParams& p, bool count, void* stream) {
   // (the opted-in sky has instantiations of its own: its code would cost the
   // others registers; the pilot and the counting variant ignore it -- path
   // lengths and counts do not depend on what a miss returns)
-  if (p.tile_work) {  // the scheduler's pilot render: its own instantiation (and kernel name)
+  if (p.work_max) {  // a measuring render (pilot or first frame): its own instantiation (and kernel name)
     if (stage)
       hipLaunchKernelGGL((render_kernel<false, true, true, false>), g, b, shmem, st, p);
     else

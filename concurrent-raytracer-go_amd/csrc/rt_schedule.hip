@@ -146,8 +146,11 @@ __global__ __launch_bounds__(256) void sched_est(const SchedParams p) {
   if (i >= (size_t)p.local * 1024) return;
   const int lt = (int)(i >> 10), q = (int)(i & 1023);
   float e;
-  if (p.plen) {  // one sample is a noisy estimate of a pixel's mean: take the neighbourhood's longest
-    const unsigned int* L = p.plen + (size_t)lt * 1024;
+  bool heavy = false;
+  if (p.work_max && p.work_n < p.spp) {
+    // a pilot of a few samples is a noisy estimate of a pixel's mean: take
+    // the neighbourhood's longest path
+    const unsigned int* L = p.work_max + (size_t)lt * 1024;
     const int x = q & 31, y = q >> 5;
     unsigned int m = L[q];
     if (x > 0) m = max(m, L[q - 1]);
@@ -155,11 +158,21 @@ __global__ __launch_bounds__(256) void sched_est(const SchedParams p) {
     if (y > 0) m = max(m, L[q - 32]);
     if (y < 31) m = max(m, L[q + 32]);
     e = (float)m + 0.02f;
+  } else if (p.work_max) {
+    // a measured frame: every sample's path length, so the pixel's mean work
+    // per sample; a pixel with a long path is split whatever its mean (its
+    // block would otherwise run that path's chain of bounces with many other
+    // paths: the launch's tail)
+    const size_t i0 = (size_t)lt * 1024 + q;
+    e = (float)((double)p.work_sum[i0] / (double)p.work_n) + 0.02f;
+    heavy = (int)p.work_max[i0] > p.split_depth;
+    if (heavy) e = fmaxf(e, (float)p.work_max[i0]);  // its sub-blocks go first: they hold the long chains
   } else {  // no pilot: every pixel of a tile with geometry weighs half a block
     const float c = p.tile_cost[lt];
     e = c > 0 ? (float)(p.block_work / (2.0 * max(1, p.spp))) * (1.0f + 1e-3f * fminf(c, 100.0f)) : 0.0f;
   }
-  p.est[i] = e;
+  // the sign bit marks a pixel to split (est >= 0 otherwise)
+  p.est[i] = heavy ? -e - 1e-30f : e;
 }
 
 // One record: the block's pixels and samples, the union of its pixels'
@@ -211,7 +224,10 @@ __global__ __launch_bounds__(64) void sched_blocks(const SchedParams p) {
     }
     return;
   }
-  const float* est = p.est + (size_t)lt * 1024;
+  const float* est_raw = p.est + (size_t)lt * 1024;
+  // (a negative estimate marks a pixel measured as heavy: split it; its work is -est)
+  auto est_of = [&](int q) { return fabsf(est_raw[q]); };
+  auto heavy_of = [&](int q) { return p.spp > 1 && (S * (double)fabsf(est_raw[q]) > bw || est_raw[q] < 0.0f); };
   // prefix sums (16 consecutive pixels per lane, then a wave scan) and the
   // suffix minimum of the heavy pixels
   const int q0 = lane * 16;
@@ -219,7 +235,7 @@ __global__ __launch_bounds__(64) void sched_blocks(const SchedParams p) {
   double acc = 0;
   int big = 1024;
   for (int k = 0; k < 16; ++k) {
-    v[k] = S * (double)est[q0 + k];
+    v[k] = S * (double)est_of(q0 + k);
     acc += v[k];
   }
   double excl = acc;
@@ -229,7 +245,7 @@ __global__ __launch_bounds__(64) void sched_blocks(const SchedParams p) {
   }
   excl -= acc;
   for (int k = 15; k >= 0; --k)
-    if (v[k] > bw) big = q0 + k;
+    if (v[k] > bw || heavy_of(q0 + k)) big = q0 + k;
   int sbig = big;  // suffix minimum over the lanes above
   for (int off = 1; off < 64; off <<= 1) {
     const int t = __shfl_down(sbig, off);
@@ -240,7 +256,7 @@ __global__ __launch_bounds__(64) void sched_blocks(const SchedParams p) {
     int nb = lane + 1 < 64 ? __shfl_down(sbig, 1) : 1024;
     if (lane == 63) nb = 1024;
     for (int k = 15; k >= 0; --k) {
-      if (v[k] > bw) nb = q0 + k;
+      if (v[k] > bw || heavy_of(q0 + k)) nb = q0 + k;
       s_big[q0 + k] = (uint16_t)nb;
     }
     for (int k = 0; k < 16; ++k) {
@@ -257,7 +273,7 @@ __global__ __launch_bounds__(64) void sched_blocks(const SchedParams p) {
   for (int q = lane; q <= 1024; q += 64) {
     int nx = 1024;
     if (q < 1024) {
-      if (p.spp > 1 && S * (double)est[q] > bw) {
+      if (heavy_of(q)) {
         nx = q + 1;  // split pixel: a block of its own
       } else {
         int hi = min(min(q + p.big_pixels, 1024), (int)s_big[min(q + 1, 1024)]);
@@ -299,12 +315,12 @@ __global__ __launch_bounds__(64) void sched_blocks(const SchedParams p) {
       for (int k = 0; k < kLevels; ++k)
         if ((m >> k) & 1) q = s_J[k][q];
       const int e = s_J[0][q];
-      if (p.spp > 1 && S * (double)est[q] > bw) {  // a split pixel (e == q + 1): sample ranges of <= 64
+      if (heavy_of(q)) {  // a split pixel (e == q + 1): sample ranges of <= split_samples
         const int nsub = (p.spp + p.split_samples - 1) / p.split_samples;
         const int ord = atomicAdd(&s_nsplit, 1);
         for (int j = 0; j < nsub; ++j) {
           const int s0 = (int)((long long)p.spp * j / nsub), s1 = (int)((long long)p.spp * (j + 1) / nsub);
-          f(bucket_of((s1 - s0) * (double)est[q]), q, 1, s0, s1 - s0, ord, nsub);
+          f(bucket_of((s1 - s0) * (double)est_of(q)), q, 1, s0, s1 - s0, ord, nsub);
         }
       } else {
         f(bucket_of(s_pre[e] - s_pre[q]), q, e - q, 0, p.spp, -1, 1);

@@ -292,6 +292,10 @@ void rt_tuning_default(rt_tuning* t) {
   // 12-bounce path instead of a 50-bounce one (C2 first frame 1.39 -> 1.07 ms,
   // the main launch unchanged; scripts/first_frame_probe.py)
   t->pilot_depth = 12;
+  // measured re-cuts are exact but do not shorten the launch: its tail is
+  // the chains of the longest paths, not the block sizes (C2 0.80 pilot-only
+  // vs 0.84 ms measured, C3 0.59 vs 0.56; scripts/tuning_sweep.py)
+  t->measure = 0;
 }
 
 int32_t rt_num_tiles(int32_t w, int32_t h) {

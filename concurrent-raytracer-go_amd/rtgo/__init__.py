@@ -137,7 +137,8 @@ class Tuning(ctypes.Structure):
         ("wf_trav_wgs", ctypes.c_int32),
         ("pilot_depth", ctypes.c_int32),
         ("split_samples", ctypes.c_int32),
-        ("_pad", ctypes.c_int32),
+        ("measure", ctypes.c_int32),
+        ("split_depth", ctypes.c_int32),
     ]
 
 

@@ -251,7 +251,7 @@ typedef struct {
   int32_t pilot;          /* 1: block sizes from a one-sample pilot render; 0: geometric estimate */
   int32_t frustum;        /* 1: primary-ray candidate masks (cull, black tiles) */
   int32_t stage;          /* 1: small scenes staged into LDS */
-  double block_work;      /* path bounces x samples per block; 0: default (512; 8192 with a BVH) */
+  double block_work;      /* path bounces x samples per block; 0: default (512; 256 with triangles; 8192 BVH) */
   int32_t block_samples;  /* pixels x samples of a large block at most; 0: 1024 */
   int32_t bvh_bins;       /* SAH bins per axis; 0: 32 */
   int32_t bvh_leaf;       /* spheres per BVH leaf at most (1..7); 0: 4 */
@@ -262,7 +262,9 @@ typedef struct {
   int32_t wf_trav_wgs;    /* traversal workgroups sharing a CU's LDS; 0: 1 */
   int32_t pilot_depth;    /* bounces the pilot render follows a path at most (default 12); 0: max_depth */
   int32_t split_samples;  /* samples per sub-block of a split (heavy) pixel, 1..64; 0: 64 */
-  int32_t _pad;
+  int32_t measure;        /* 1: the first frame of a schedule measures every pixel's path lengths and the
+                             next frame re-cuts the blocks from them; 0: pilot schedule only (default) */
+  int32_t split_depth;    /* measured schedules split a pixel with a path of more bounces than this; 0: 16 */
 } rt_tuning;
 void rt_tuning_default(rt_tuning* t);
 /* Applies to later rt_context_set_scene (BVH shape) and render calls. */

@@ -17,7 +17,7 @@ import os
 import statistics
 import sys
 
-KERNEL = "render_kernel<false, true, false>"
+KERNEL = "render_kernel<false, true, false, false>"
 
 
 def per_dispatch(d, counter):

@@ -3,12 +3,12 @@
 # two PMC passes (FETCH_SIZE, WRITE_SIZE) of the bench workload.
 # usage: scripts/profile.sh r01   (writes gpurun_out/prof_r01*; copy gpurun_out/profiles_r01/* into profiles/)
 set -eu
-R=${1:-r01}
+R=${1:-r02}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/profiles_${R}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${R}_trace -o run --output-format csv \
-  -- python3 bench.py --no-cpu-baseline > gpurun_out/prof_${R}_bench.json
+  -- python3 bench.py --no-cpu-baseline --no-e2e > gpurun_out/prof_${R}_bench.json
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_${R}_fetch -o run --output-format csv \
   -- python3 scripts/pmc_workload.py 5
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_${R}_write -o run --output-format csv \

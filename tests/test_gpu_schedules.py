@@ -40,3 +40,23 @@ def test_schedule_does_not_change_the_image(name, tun, spp):
     ref, ref_rgba, _ = oracle.render(scene, w, h, st)
     assert lin.tobytes() == ref.astype(np.float32).tobytes(), name
     assert rgba.tobytes() == ref_rgba.tobytes(), name
+
+
+@pytest.mark.parametrize("tun", [{"measure": 1}, {"measure": 1, "split_depth": 4, "split_samples": 16}, {}],
+                         ids=["measured", "measured_deep_split", "pilot_only"])
+def test_measured_recut_does_not_change_the_image(tun):
+    """The first frame of a schedule measures every pixel's paths and the
+    second frame's blocks are cut from them (rt_tuning.measure): frames 1, 2
+    and 3 of one renderer (pilot schedule, measuring frame, measured
+    schedule) all equal the oracle."""
+    scene = load_case(rtgo, ("file", "sphere_reflections_light_facing.json"))
+    w, h = 96, 72
+    r = rtgo.ParallelRenderer()
+    r.set_tuning(rtgo.default_tuning(**tun))
+    for seed in (5, 6, 5):
+        st = make_settings(rtgo, {"samples": 24}, seed=seed)
+        r.settings = st
+        rgba = r.render(scene, w, h)
+        ref, ref_rgba, _ = oracle.render(scene, w, h, st)
+        assert r.last_linear.tobytes() == ref.astype(np.float32).tobytes(), seed
+        assert rgba.tobytes() == ref_rgba.tobytes(), seed
