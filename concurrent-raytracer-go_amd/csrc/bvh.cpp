@@ -236,18 +236,9 @@ void build_sphere_bvh(FlatScene* fs, int bins, int leaf) {
     }
     fs->bvh_depth = maxd;
   }
-  // quantized 4-wide copy for the wavefront traversal (rt_wavefront.hip):
-  // every internal node of the binary tree that is a child's child of
-  // another is collapsed into its parent, so a traversal step tests up to 4
-  // boxes and a ray needs about half the dependent node loads.  A group is 4
-  // consecutive DQNode slots {box of child k, child code}: an internal child
-  // points to its own group (slot index << 3), a leaf is (first sphere << 3
-  // | count), an empty slot has an empty box and kNoChild.  Groups are
-  // numbered breadth-first (the top of the tree is a prefix, which the
-  // kernels stage in LDS).  Boxes are quantized to a grid of 65000 steps per
-  // axis over the root box with 4 steps of margin: lo rounded down, hi up,
-  // one more step each way, and the decoded box checked to contain the float
-  // box.
+  // quantized copy: a grid of 65000 steps per axis over the root box with 4
+  // steps of margin; lo rounded down, hi up, one more step each way, and the
+  // decoded box checked to contain the float box
   {
     const DBVHNode& r = nodes[0];
     for (int k = 0; k < 3; ++k) {
@@ -255,83 +246,29 @@ void build_sphere_bvh(FlatScene* fs, int bins, int leaf) {
       fs->qd[k] = ext > 0 ? ext / 65000.0 : 1.0;
       fs->q0[k] = (double)r.lo[k] - 4 * fs->qd[k];
     }
-    auto area = [&](int i) {
-      double e[3];
-      for (int k = 0; k < 3; ++k) e[k] = std::max(0.0, (double)nodes[i].hi[k] - (double)nodes[i].lo[k]);
-      return e[0] * e[1] + e[1] * e[2] + e[2] * e[0];
-    };
-    // the (up to 4) children of binary internal node ni after collapsing:
-    // the internal child with the largest surface is replaced by its two
-    // children while there is room
-    auto collapse = [&](int ni) {
-      std::vector<int> ch = {nodes[ni].left_or_first, nodes[ni].left_or_first + 1};
-      while (ch.size() < 4) {
-        int best = -1;
-        double ba = -1;
-        for (size_t i = 0; i < ch.size(); ++i)
-          if (nodes[ch[i]].count == 0 && area(ch[i]) > ba) {
-            ba = area(ch[i]);
-            best = (int)i;
-          }
-        if (best < 0) break;
-        const int x = ch[best];
-        ch.erase(ch.begin() + best);
-        ch.insert(ch.begin() + best, {nodes[x].left_or_first, nodes[x].left_or_first + 1});
-      }
-      return ch;
-    };
-    auto quantize = [&](const DBVHNode& nd, DQNode* q) {
+    fs->qbvh.resize(nodes.size());
+    for (size_t i = 0; i < nodes.size(); ++i) {
+      const DBVHNode& nd = nodes[i];
       uint32_t ql[3], qh[3];
       for (int k = 0; k < 3; ++k) {
         double a = floor(((double)nd.lo[k] - fs->q0[k]) / fs->qd[k]) - 1;
         double b = ceil(((double)nd.hi[k] - fs->q0[k]) / fs->qd[k]) + 1;
         a = std::min(std::max(a, 0.0), 65535.0);
         b = std::min(std::max(b, 0.0), 65535.0);
-        if (!(fs->q0[k] + a * fs->qd[k] <= (double)nd.lo[k]) || !(fs->q0[k] + b * fs->qd[k] >= (double)nd.hi[k]))
-          return false;  // cannot happen for finite boxes
+        if (!(fs->q0[k] + a * fs->qd[k] <= (double)nd.lo[k]) || !(fs->q0[k] + b * fs->qd[k] >= (double)nd.hi[k])) {
+          fs->bvh.clear();  // cannot happen for finite boxes; keep the linear scan rather than cull wrongly
+          fs->qbvh.clear();
+          return;
+        }
         ql[k] = (uint32_t)a;
         qh[k] = (uint32_t)b;
       }
-      for (int k = 0; k < 3; ++k) q->w[k] = ql[k] | (qh[k] << 16);  // per axis (lo, hi)
-      return true;
-    };
-    fs->qbvh.clear();
-    fs->root_code = nodes[0].count ? (int32_t)((nodes[0].left_or_first << 3) | nodes[0].count) : 0;
-    std::vector<int> groups;           // binary internal node of each group, breadth-first
-    std::vector<int> pending_at;       // stack entries a traversal may hold on entering the group
-    int max_pending = 1;
-    if (nodes[0].count == 0) {
-      groups.push_back(0);
-      pending_at.push_back(0);
+      DQNode& q = fs->qbvh[i];
+      q.w[0] = ql[0] | (qh[0] << 16);  // per axis (lo, hi): the kernel picks near / far per ray
+      q.w[1] = ql[1] | (qh[1] << 16);
+      q.w[2] = ql[2] | (qh[2] << 16);
+      q.w[3] = (uint32_t)((nd.left_or_first << 3) | nd.count);
     }
-    for (size_t gi = 0; gi < groups.size(); ++gi) {
-      const std::vector<int> ch = collapse(groups[gi]);
-      const int here = pending_at[gi] + (int)ch.size() - 1;  // the other hit children wait on the stack
-      max_pending = std::max(max_pending, here);
-      for (int k = 0; k < 4; ++k) {
-        DQNode q;
-        if (k >= (int)ch.size()) {
-          q.w[0] = q.w[1] = q.w[2] = 0x0000FFFFu;  // lo 65535 > hi 0: no ray meets it
-          q.w[3] = kNoChild;
-        } else {
-          const DBVHNode& nd = nodes[ch[k]];
-          if (!quantize(nd, &q)) {
-            fs->bvh.clear();  // keep the linear scan rather than cull wrongly
-            fs->qbvh.clear();
-            return;
-          }
-          if (nd.count) {
-            q.w[3] = (uint32_t)((nd.left_or_first << 3) | nd.count);
-          } else {
-            q.w[3] = (uint32_t)((groups.size() * 4) << 3);
-            groups.push_back(ch[k]);
-            pending_at.push_back(here);
-          }
-        }
-        fs->qbvh.push_back(q);
-      }
-    }
-    fs->bvh4_stack = max_pending;
   }
   std::vector<DSphere> reordered(n);
   for (int i = 0; i < n; ++i) reordered[i] = fs->spheres[idx[i]];

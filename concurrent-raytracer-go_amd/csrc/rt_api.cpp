@@ -587,9 +587,9 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   p.tiles_x = kp.tiles_x;
   p.ntiles = kp.ntiles;
   p.layout = kp.layout;
-  // the most hit children a lane can leave pending on its way to a leaf (bvh.cpp)
-  p.stack_depth = std::max(1, f.bvh4_stack);
-  p.root_code = f.root_code;
+  // a lane holds at most one pending child per internal node above its leaf:
+  // depth - 1 entries (leaves at level bvh_depth, the root at level 1)
+  p.stack_depth = std::max(1, f.bvh_depth - 1);
   // traversal workgroups: trav_block threads (64..1024), LDS shared by
   // trav_wgs of them per CU (tuning; default one of 1024)
   const rt_tuning& tn = c->tun;
@@ -599,8 +599,8 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   if (tn.wf_trav_wgs > 0) trav_wgs = std::min(32, tn.wf_trav_wgs);
   p.bvh_nodes = (int)f.qbvh.size();
   p.lds_nodes = wf_lds_nodes(p.stack_depth, (int)f.qbvh.size(), p.trav_block, trav_wgs);
-  if (tn.wf_lds_nodes >= 0)  // stage fewer slots (whole groups of 4)
-    p.lds_nodes = std::min(p.lds_nodes, tn.wf_lds_nodes & ~3);
+  if (tn.wf_lds_nodes >= 0)  // stage fewer nodes (an odd count: child pairs never split)
+    p.lds_nodes = std::min(p.lds_nodes, tn.wf_lds_nodes | 1);
   p.shard_cap = shard_cap;
   p.hard_cap = (int64_t)qcap;
   p.soft_cap = (int64_t)qcap * 16;

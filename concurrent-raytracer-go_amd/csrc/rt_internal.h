@@ -23,9 +23,7 @@ struct FlatScene {
   std::vector<DLight> lights;
   std::vector<DBVHNode> bvh;  // empty => linear scan
   int32_t bvh_depth = 0;      // levels of the BVH (root = 1): the traversal stack holds fewer entries
-  std::vector<DQNode> qbvh;   // the 4-wide quantized BVH of the wavefront traversal: groups of 4 slots
-  int32_t root_code = 0;      // its start: the root's group (0) or, for a one-leaf tree, the leaf
-  int32_t bvh4_stack = 1;     // stack entries its traversal can hold at most
+  std::vector<DQNode> qbvh;   // the BVH with quantized bounds (same node order)
   double q0[3] = {0, 0, 0}, qd[3] = {1, 1, 1};  // its grid: coordinate = q0 + q * qd
   double cam_pos[3] = {0, 0, 0};
   double aspect = 0;
@@ -192,10 +190,9 @@ struct WfParams {
   const DSky* sky;           // miss radiance or null (black)
   int32_t nl, max_depth, recursive, soft, spp;
   int32_t W, H, rank, world, tiles_x, ntiles, layout;
-  int32_t stack_depth;       // BVH stack entries per lane (FlatScene::bvh4_stack)
-  int32_t lds_nodes;         // leading slots of the 4-wide tree (breadth-first: the top levels) staged in LDS
-  int32_t bvh_nodes;         // slots in all
-  int32_t root_code;         // traversal start (FlatScene::root_code)
+  int32_t stack_depth;       // BVH stack entries per lane (the tree's depth - 1)
+  int32_t lds_nodes;         // leading quantized nodes (breadth-first: the top levels) staged in LDS
+  int32_t bvh_nodes;         // quantized nodes in all
   int32_t trav_block;        // threads per workgroup of the traversal kernels (<= kWfTravBlock)
   int32_t shard_cap;         // path slots per shard
   int64_t hard_cap, soft_cap;  // queue entries per shard
@@ -218,8 +215,8 @@ struct WfParams {
   uint8_t* out_rgba;
 };
 int wf_launch_bounce(const WfParams& p, bool first, bool count, void* stream);
-// Slots of the 4-wide tree the traversal kernels can stage in LDS next to
-// their stacks (all of them when they fit; else whole groups of 4).
+// Quantized nodes the traversal kernels can stage in LDS next to their stacks
+// (all of them when they fit; else an odd count, so no child pair is split).
 int wf_lds_nodes(int stack_depth, int nodes, int block, int wgs_per_cu);
 int wf_launch_resolve(const WfParams& p, int npix, void* stream);
 

@@ -103,15 +103,13 @@ struct alignas(16) DBVHNode {  // 32 B
   int32_t count;          // 0 = internal node
 };
 
-// One child slot of the 4-wide quantized BVH of the wavefront kernels
-// (bvh.cpp, rt_wavefront.hip): its box as grid indices q (coordinate =
-// q0 + q * qd per axis, FlatScene), rounded outward, w[k] = lo_k | hi_k << 16
-// for axes k = 0..2; w[3] = traversal code: an internal child's group (first
-// slot << 3), a leaf (first sphere << 3 | count 1..7), or kNoChild.  A group
-// is 4 consecutive slots: one 64-B load per traversal step.
+// The same BVH with 16-bit quantized bounds (the wavefront kernels,
+// rt_wavefront.hip): bounds are grid indices q (coordinate = q0 + q * qd per
+// axis, FlatScene), rounded outward; 16 B per node, a child pair in one
+// 32-B load.  w[0] = lo.x | lo.y << 16, w[1] = lo.z | hi.x << 16,
+// w[2] = hi.y | hi.z << 16, w[3] = traversal code (first << 3 | count).
 struct alignas(16) DQNode {  // 16 B
   uint32_t w[4];
 };
-constexpr uint32_t kNoChild = 0xFFFFFFFFu;  // an empty slot of a group
 
 }  // namespace rtgo

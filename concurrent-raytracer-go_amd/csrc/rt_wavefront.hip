@@ -275,71 +275,43 @@ __device__ __forceinline__ bool box_q(const uint4 n, const RayQ& r, float tmin, 
   return tn <= tf;
 }
 
-// One step of the while-while traversal of a lane over the 4-wide tree
-// (bvh.cpp): descend internal groups until `cur` is a leaf (count 1..7) or
-// -1 (done).  A step loads one group (4 slots, 64 B) and tests its 4 boxes;
-// the hit children wait on the lane's stack.  kNear (closest hit): the
-// nearest child is taken first and the others are pushed far to near (a
-// 5-comparator sorting network), so closer boxes shrink tmax sooner; any-hit
-// queries take them in slot order.  The leaf tests are exact and resolve
-// exact-t ties by hittable index, so the visiting order never changes a
-// result.  Groups below `nlds` (a multiple of 4) come from the LDS copy
-// `lt` (stage_tree), the rest from global memory.
+// One step of the while-while traversal of a lane (the closest_hit / any_hit
+// order of rt_device.h over the same tree): descend internal nodes, nearer
+// child first, until `cur` is a leaf (count 1..4) or -1 (done).
+// Node pairs below `nlds` come from the LDS copy `lt` (stage_tree), the rest
+// from global memory.
 // kFull: the whole tree is staged (no global-memory branch).
 template <bool kFull>
-__device__ __forceinline__ void load_group(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds, int first,
-                                           uint4* n) {
-  if (kFull || first < nlds) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) n[k] = as_uint4(lt[first + k]);
+__device__ __forceinline__ void load_pair(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds, int first,
+                                          uint4& L, uint4& R) {
+  if (kFull || first < nlds) {  // nlds is odd or the whole tree: a staged pair is whole
+    L = as_uint4(lt[first]);
+    R = as_uint4(lt[first + 1]);
   } else {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) n[k] = as_uint4(qb[first + k]);
+    L = as_uint4(qb[first]);
+    R = as_uint4(qb[first + 1]);
   }
 }
-__device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
-  const bool sw = tb < ta;
-  const float t = sw ? tb : ta;
-  const int c = sw ? cb : ca;
-  tb = sw ? ta : tb;
-  cb = sw ? ca : cb;
-  ta = t;
-  ca = c;
-}
-template <bool kCount, bool kFull, bool kNear>
+template <bool kCount, bool kFull>
 __device__ __forceinline__ void descend(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
                                         const RayQ& r, float tminf, float tmaxf, int& cur, int& sp, int* stack,
                                         Counters& c) {
-  constexpr float kMissT = __builtin_huge_valf();
   while ((cur & 7) == 0) {
-    uint4 n[4];
-    load_group<kFull>(qb, lt, nlds, cur >> 3, n);
-    cnt<kCount>(c, C_BOX, 4);
-    float t[4];
-    int code[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float tn;
-      const bool h = box_q(n[k], r, tminf, tmaxf, tn) && n[k].w != kNoChild;
-      t[k] = h ? tn : kMissT;
-      code[k] = (int)n[k].w;
-    }
-    if constexpr (kNear) {  // ascending t: (0,1) (2,3) (0,2) (1,3) (1,2)
-      cswap(t[0], code[0], t[1], code[1]);
-      cswap(t[2], code[2], t[3], code[3]);
-      cswap(t[0], code[0], t[2], code[2]);
-      cswap(t[1], code[1], t[3], code[3]);
-      cswap(t[1], code[1], t[2], code[2]);
-    }
-    int nxt = -1;
-#pragma unroll
-    for (int k = 3; k >= 0; --k) {
-      if (t[k] != kMissT) {
-        if (nxt != -1) stack[sp++ * 64] = nxt;
-        nxt = code[k];
+    uint4 L, R;
+    load_pair<kFull>(qb, lt, nlds, cur >> 3, L, R);
+    cnt<kCount>(c, C_BOX, 2);
+    float tl, tr;
+    const bool hl = box_q(L, r, tminf, tmaxf, tl), hr = box_q(R, r, tminf, tmaxf, tr);
+    if (hl || hr) {
+      const bool lfirst = hl && (!hr || tl <= tr);
+      if (hl && hr) {
+        stack[sp * 64] = lfirst ? (int)R.w : (int)L.w;
+        ++sp;
       }
+      cur = lfirst ? (int)L.w : (int)R.w;
+    } else {
+      cur = sp == 0 ? -1 : stack[--sp * 64];
     }
-    cur = nxt != -1 ? nxt : (sp == 0 ? -1 : stack[--sp * 64]);
   }
 }
 
@@ -438,7 +410,7 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
           if (box_hit(p.g.bvh[0], o, id, tmin, closest)) {
             r32 = ray_q(p, o, id);
             tminf = t_lo32(tmin);
-            cur = p.root_code;
+            cur = bvh_code(p.g.bvh[0]);
             sp = 0;
             busy = true;
             miss = false;
@@ -457,8 +429,7 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
       continue;
     }
     if (busy) {
-      descend<kCount, kFull, true>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, t_hi32(closest), cur, sp, stack,
-                                   c);
+      descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, t_hi32(closest), cur, sp, stack, c);
       if (cur != -1) {  // a leaf: the exact Sphere.Hit tests, in hittable order
         const int first = cur >> 3, count = cur & 7;
         DSphere ls[kLeafBatch];
@@ -628,7 +599,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
           r32 = ray_q(p, o, id);
           tminf = t_lo32(tmin);
           tmaxf = t_hi32(tmax);
-          cur = p.root_code;
+          cur = bvh_code(p.g.bvh[0]);
           sp = 0;
           busy = true;
         }
@@ -639,7 +610,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
       continue;
     }
     if (busy) {
-      descend<kCount, kFull, false>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, tmaxf, cur, sp, stack, c);
+      descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, tmaxf, cur, sp, stack, c);
       bool blocked = false;
       if (cur != -1) {
         const int first = cur >> 3, count = cur & 7;
@@ -953,8 +924,8 @@ int wf_lds_nodes(int stack_depth, int nodes, int block, int wgs_per_cu) {
       ((long long)kLdsBytes / std::max(1, wgs_per_cu) - (long long)block * stack_depth * (long long)sizeof(int)) /
       (long long)sizeof(uint4);
   if (room >= nodes) return nodes;
-  if (room < 4) return 0;
-  return (int)(room & ~3ll);  // whole groups
+  if (room < 1) return 0;
+  return (int)(room % 2 ? room : room - 1);
 }
 
 template <bool kCount>
