@@ -77,8 +77,10 @@ def test_c5_rank_shares_match_oracle(rank):
     world = 8
     scene = spheres10k_scene(rtgo)
     lin, rgba, _, _ = render_dev(scene, w, h, st, rank=rank, world=world)
-    local = rtgo.tiles_for_rank(w, h, rank, world)
-    assert not np.isnan(lin[:local * 1024]).any()
+    from rtgo import shard
+
+    inside = shard.packed_index(w, h, rank, world) >= 0  # (the last tile row is clipped: 2160 = 67 * 32 + 16)
+    assert not np.isnan(lin[inside]).any() and np.isnan(lin[~inside]).all()
     mine = [(i, int(t)) for i, t in enumerate(g["tiles"]) if int(t) % world == rank]
     assert len(mine) == 2
     for i, t in mine:
