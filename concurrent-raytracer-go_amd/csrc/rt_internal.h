@@ -95,6 +95,7 @@ constexpr int kJump = 64 + 1;
 // radiance slots live in LDS: 24 KB); the host picks P = floor(1024 / spp)
 // pixels per block (at most 64), so spp <= 1024.
 constexpr int kMaxBlockSamples = 1024;
+constexpr int kDbgStride = 48;  // RT_WG_TIMING: 64-bit words per workgroup in the debug buffer
 // Deepest BVH the kernels accept (per-lane LDS stack entries; bvh.cpp keeps
 // the linear scan for deeper trees).  The stacks are allocated per launch for
 // the scene's actual depth (10k spheres: 15 levels).

@@ -465,6 +465,187 @@ __device__ __forceinline__ void camera_ray(KArg k, int x, int y, int s, rt_rng& 
   camera_ray_c<kCount>(cam_k(k), x, y, s, rng, o, d, c);
 }
 
+// ------------------------------------------------------------ solo paths
+// When a single path is left running in a wave (the end of a block, where
+// a long metal-metal interreflection sets the launch's critical path), the
+// idle lanes join it: every lane holds the path's state and computes the
+// same binary64 values (the serial parts need no cross-lane traffic), while
+// the loops over primitives run in parallel, one primitive per lane, with
+// exact merges:
+//   closest hit - every lane tests its primitives over [0.001, +inf); the
+//     hits are then replayed in hittable scan order with hitWorld's rule
+//     (accept t <= closest; an equal t only for a hittable index not below
+//     the current one).  A root that Sphere.Hit rejects against a smaller
+//     tMax is larger than that tMax, and so is the other root, so the replay
+//     accepts exactly what the sequential scan accepts (renderer.go:333-346);
+//   shadow cones and the hard shadow ray - a ballot of per-primitive tests
+//     (an occlusion query has no order);
+//   soft shadows - soft_coop (already wave-wide for one owner).
+// The path runs to its end; then the main loop takes over again.  Linear-
+// scan scenes with at most 64 spheres and 64 triangles (the staged scenes);
+// the counting and pilot variants keep the per-lane loop.  (Lone bounce,
+// 2 lights with soft shadows: 9.8 -> 6.1 us, scripts/latency_probe.py.
+// Two paths in 32-lane groups, same scheme with shuffles, measured slower:
+// headline 0.82 vs 0.775 ms, the group form's registers spill.)
+__device__ __forceinline__ bool solo_closest(const Geo& g, d3 o, d3 d, HitSel& hs) {
+  const int lane = (int)(threadIdx.x & 63);
+  const double a = len2(d);
+  const double inv_a = approx_rcp(a);
+  double closest = __builtin_inf();
+  int best_obj = -1;
+  bool found = false;
+  // lane i tests sphere i, then triangle i; the hits are replayed in
+  // hittable scan order (spheres before triangles)
+#pragma unroll
+  for (int tri = 0; tri < 2; ++tri) {
+    double t = 0, nm = 0, u = 0, v = 0;
+    bool f;
+    if (!tri) {
+      f = lane < g.ns && sphere_query(g.spheres[lane], o, d, a, inv_a, 0.001, __builtin_inf(), nm) != 0;
+      if (f) t = nm / a;
+    } else {
+      f = lane < g.nt && tri_test(g.tris[lane], o, d, 0.001, __builtin_inf(), t, u, v);
+    }
+    for (unsigned long long b = __ballot(f); b; b &= b - 1) {
+      const int i = __builtin_ctzll(b);
+      const double ti = rld(t, i);
+      const int obj = tri ? g.tris[i].obj : g.spheres[i].obj;
+      if (closest < ti || (ti == closest && best_obj > obj)) continue;
+      closest = ti;
+      best_obj = obj;
+      hs.num = tri ? ti : rld(nm, i);
+      if (tri) {
+        hs.u = rld(u, i);
+        hs.v = rld(v, i);
+      }
+      hs.idx = i;
+      hs.is_tri = tri;
+      found = true;
+    }
+  }
+  return found;
+}
+
+// The path of lane `ow`, run to its end by the whole wave: its radiance.
+template <bool kSky>
+__device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t rx, int depth, int* stack) {
+  const int lane = (int)(threadIdx.x & 63);
+  o = rl3(o, ow);
+  d = rl3(d, ow);
+  T = rl3(T, ow);
+  L = rl3(L, ow);
+  rt_rng rng{rl64(rx, ow)};
+  depth = (int)rl32((uint32_t)depth, ow);
+  Counters c;
+  for (;;) {
+    const Hot h = hot<true>();
+    const Geo& g = h.g;
+    if (depth >= h.max_depth) return L;  // traceRay depth cut-off: contributes 0
+    // (1) closest hit (hitWorld, renderer.go:170)
+    HitSel hs;
+    if (!solo_closest(g, o, d, hs)) {  // miss -> black (or the opted-in sky)
+      if constexpr (kSky) L = L + mul(T, sky_color(fresh()->sky, d));
+      return L;
+    }
+    d3 P, N;
+    bool front;
+    int mi, self;
+    if (!hs.is_tri) {  // sphere.go:42-58
+      const DSphere& S0 = g.spheres[hs.idx];
+      const double t = hs.num / len2(d);
+      P = o + muls(d, t);
+      d3 outward = divs(P - ld3(S0.c), S0.r);
+      front = dot(d, outward) < 0;
+      N = front ? outward : neg(outward);
+      mi = S0.mat;
+      self = S0.obj;
+    } else {  // triangle.go:68-81
+      const DTri& T0 = g.tris[hs.idx];
+      P = o + muls(d, hs.num);
+      double w = 1.0 - hs.u - hs.v;
+      d3 n = ld3(T0.n);
+      N = normalize((muls(n, w) + muls(n, hs.u)) + muls(n, hs.v));
+      front = dot(d, N) < 0;
+      if (!front) N = neg(N);
+      mi = T0.mat;
+      self = T0.obj;
+    }
+    // (2) calculateDirectLighting (renderer.go:229-297), light by light
+    const DMat* __restrict__ m = h.mats + mi;
+    d3 D = mk(m->ambient, m->ambient, m->ambient);
+    for (int li = 0; li < h.nl; ++li) {
+      const DLight& Lt = h.lights[li];
+      const d3 lv = ld3(Lt.pos) - P;
+      const double ldist = sqrt(lv.x * lv.x + lv.y * lv.y + lv.z * lv.z);
+      const d3 ldir = ldist == 0 ? mk(0, 0, 0) : divs(lv, ldist);
+      if (ldist < 0.001) continue;  // renderer.go:252-254
+      // the shadow cone's candidates, one primitive per lane (cone_candidates)
+      const bool self_out = front && dot(N, ldir) >= KC(0.1015);
+      bool cs = false, cb = false;
+      if (lane < g.ns) {
+        const DSphere& S = g.spheres[lane];
+        cs = !(self_out && S.obj == self && S.r > 0) && in_cone(S.c, S.r, P, ldir, ldist);
+      }
+      if (lane < g.nb) {  // (nb <= 5: 12 triangles per cube)
+        const DBox& B = g.boxes[lane];
+        cb = !(self_out && B.obj == self) && in_cone(B.bc, B.br, P, ldir, ldist);
+      }
+      Cand cm{__ballot(cs), 0ull};
+      for (unsigned long long b = __ballot(cb); b; b &= b - 1) cm.t |= 0xFFFull << g.boxes[__builtin_ctzll(b)].first;
+      // the hard shadow ray (renderer.go:305), the candidates in parallel
+      bool blk = false;
+      if ((cm.s >> lane) & 1ull) {
+        const double a = len2(ldir);
+        double num;
+        blk = sphere_query(g.spheres[lane], P, ldir, a, approx_rcp(a), 0.001, ldist, num) != 0;
+      }
+      if ((cm.t >> lane) & 1ull) {
+        double t, u, v;
+        blk = blk || tri_test(g.tris[lane], P, ldir, 0.001, ldist, t, u, v);
+      }
+      const bool occl = __ballot(blk) != 0;
+      int unocc = 0;
+      if (!occl && h.soft) {
+        // the 16 soft rays (renderer.go:311-327); `quiet` as in the main loop
+        const bool quiet = gmax0(dot(N, ldir)) == 0.0 && D.x != 0.0 && D.y != 0.0 && D.z != 0.0 &&
+                           __builtin_isfinite(Lt.intensity) &&
+                           __builtin_isfinite(Lt.color[0] + Lt.color[1] + Lt.color[2]) &&
+                           __builtin_isfinite(m->albedo[0] + m->albedo[1] + m->albedo[2]) &&
+                           __builtin_isfinite(m->metallic);
+        const bool trace = (cm.s | cm.t) != 0 && !quiet;
+        const CoopOut r = soft_coop<false>(g, true, trace, P, ldir, ldist, cm, rng.x, h.jump, stack, c);
+        unocc = r.unocc;
+        rng.x = r.x;
+      }
+      const double sf = occl ? 0.0 : (h.soft ? (double)unocc / 16.0 : 1.0);  // shadowSum / 16
+      if (sf > 0.0) {
+        const double metallic = m->metallic;
+        double cos_t = gmax0(dot(N, ldir));
+        double intensity = cos_t * Lt.intensity / (ldist * ldist);
+        D = D + muls(ld3(m->albedo), m->diffuse_strength * intensity * sf);
+        if (metallic > 0.5) {
+          d3 view = normalize(neg(P));
+          d3 half = normalize(ldir + view);
+          double hc = gmax0(dot(N, half));
+          const int sp = m->spec_pow;
+          double si = sp == 64 ? pow_n<64>(hc) : (sp == 48 ? pow_n<48>(hc) : pow_n<32>(hc));
+          D = D + muls(ld3(Lt.color), si * intensity * sf * metallic * 3.0);
+        }
+      }
+    }
+    // (3) Material.Scatter and the traceRay combination (renderer.go:181-226)
+    const d3 E = ld3(m->emit);
+    const Scat sc = scatter<false>(m, d, N, front, rng, c);
+    if (!sc.ok) return L + mul(T, E + D);
+    L = L + mul(T, E + muls(D, m->dw));
+    if (!h.recursive || depth + 1 >= h.max_depth) return L;
+    T = mul(T, muls(sc.A, m->rw));
+    o = P;
+    d = sc.nd;
+    depth += 1;
+  }
+}
+
 // Render kernel: one wave (64 lanes) per block, three phases.  A one-wave
 // workgroup needs no barriers and leaves the CU as soon as its own work is
 // done (4-wave workgroups held their slots until their slowest wave ended).
@@ -530,6 +711,9 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   unsigned long long dbg_hit = 0, dbg_light = 0, dbg_soft = 0, dbg_vis = 0;
   // cone + hard shadow, scatter, lane-iterations alive, coop owners served, soft_seq passes
   unsigned long long dbg_hard = 0, dbg_scat = 0, dbg_alive = 0, dbg_coop = 0, dbg_seq = 0;
+  // shade-iteration clocks and counts by live lanes: 1, 2, 3-4, 5-8, > 8
+  unsigned long long dbg_bclk[5] = {0, 0, 0, 0, 0}, dbg_bcnt[5] = {0, 0, 0, 0, 0}, dbg_bts = 0;
+  int dbg_bprev = -1;
   const unsigned long long tv0 = __builtin_amdgcn_s_memtime();
 #endif
   const Cand all{~0ull, ~0ull};
@@ -738,10 +922,36 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
 #ifdef RT_WG_TIMING
       ++dbg_iter;
       dbg_alive += __popcll(__ballot(alive));
+      {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        if (dbg_bprev >= 0) dbg_bclk[dbg_bprev] += now - dbg_bts;
+        const int nal = __popcll(__ballot(alive));
+        dbg_bprev = nal == 1 ? 0 : (nal == 2 ? 1 : (nal <= 4 ? 2 : (nal <= 8 ? 3 : 4)));
+        dbg_bcnt[dbg_bprev] += 1;
+        dbg_bts = now;
+      }
       if (dbg_iter % 4 == 0 && dbg_iter / 4 < 16 && lane == 0 && fresh()->dbg)
-        fresh()->dbg[(size_t)blockIdx.x * 32 + 16 + dbg_iter / 4] = __builtin_amdgcn_s_memrealtime();
+        fresh()->dbg[(size_t)blockIdx.x * kDbgStride + 16 + dbg_iter / 4] = __builtin_amdgcn_s_memrealtime();
       const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
 #endif
+      if constexpr (kStage && !kCount && !kPilot) {
+        // one path left (no free lane found an entry to start): the whole
+        // wave runs it to its end (solo_path)
+        const unsigned long long am = __ballot(alive);
+        // (two or three paths run one after the other this way measured
+        // slower: 0.79 / 0.93 vs 0.78 ms)
+        if (__popcll(am) == 1 && hot<kStage>().masks) {
+          const d3 Lr = solo_path<kSky>(__builtin_ctzll(am), o, d, T, L, rng.x, depth, stack);
+          if (lane == __builtin_ctzll(am)) {
+            const int q = entry & (kRound - 1);
+            slot[q][0] = Lr.x;
+            slot[q][1] = Lr.y;
+            slot[q][2] = Lr.z;
+            alive = false;
+          }
+          continue;
+        }
+      }
 
       // (1) closest hit (hitWorld, renderer.go:170)
       bool shade = false, front = false, fin = false;
@@ -971,6 +1181,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   }
 #ifdef RT_WG_TIMING
   const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
+  if (dbg_bprev >= 0) dbg_bclk[dbg_bprev] += __builtin_amdgcn_s_memtime() - dbg_bts;
 #endif
 
   // ---- phase 3 (final): mean, tone map, one write per pixel
@@ -1038,7 +1249,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   }
 #ifdef RT_WG_TIMING
   if (k->dbg && lane == 0) {
-    unsigned long long* r = k->dbg + (size_t)blockIdx.x * 32;
+    unsigned long long* r = k->dbg + (size_t)blockIdx.x * kDbgStride;
     r[0] = t_start;
     r[1] = t_loop;
     r[2] = __builtin_amdgcn_s_memrealtime();
@@ -1054,6 +1265,10 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     r[12] = dbg_seq;
     r[13] = (unsigned long long)blk.np * 65536ull + (unsigned long long)blk.ns;
     r[14] = (unsigned long long)(blk.slot + 1);
+    for (int i = 0; i < 5; ++i) {
+      r[32 + i] = dbg_bclk[i];
+      r[37 + i] = dbg_bcnt[i];
+    }
   }
 #endif
 }

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Build an experiment variant of librtgo.so (dev tool): the kernel sources
+# recompiled with extra defines, linked with the host objects of the main
+# build.  usage: scripts/build_variant.sh NAME "-DFOO -DBAR=2"
+# -> concurrent-raytracer-go_amd/build/var_NAME/librtgo.so (time it with
+#    scripts/ab_bench.py or RTGO_LIB=... python bench.py)
+set -eu
+NAME=$1
+DEFS=${2:-}
+cd "$(dirname "$0")/../concurrent-raytracer-go_amd"
+make -s -j8 >/dev/null
+OUT=build/var_$NAME
+mkdir -p "$OUT"
+HIPFLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -Wall -Wno-unused-function -munsafe-fp-atomics"
+for k in rt_kernel rt_wavefront rt_schedule; do
+  /opt/rocm/bin/hipcc $HIPFLAGS $DEFS -x hip -c csrc/$k.hip -o "$OUT/$k.o" &
+done
+wait
+OBJS="$OUT/rt_kernel.o $OUT/rt_wavefront.o $OUT/rt_schedule.o"
+for o in rt_api scene_json image_io bvh schedule rt_multi scene_flat; do OBJS="$OBJS build/$o.o"; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/librtgo.so" $OBJS -L/opt/rocm/lib -lrccl -lz \
+  -Wl,-soname,librtgo.so -Wl,-rpath,/opt/rocm/lib
+echo "$OUT/librtgo.so"

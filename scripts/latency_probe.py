@@ -66,7 +66,7 @@ if os.environ.get("PROBE_SECTIONS"):  # with an RT_WG_TIMING build (RTGO_LIB): s
         ctx.set_scene(sc)
         st = rtgo.default_settings()
         st.samples, st.max_depth, st.soft_shadows = 1, 51, soft
-        dbg = torch.zeros(64 * 32, dtype=torch.int64, device="cuda")
+        dbg = torch.zeros(64 * 48, dtype=torch.int64, device="cuda")
         ctx.set_debug_buffer(dbg.data_ptr())
         lin = torch.zeros(W * 3, dtype=torch.float32, device="cuda")
         rgba = torch.zeros(W * 4, dtype=torch.uint8, device="cuda")
@@ -74,7 +74,7 @@ if os.environ.get("PROBE_SECTIONS"):  # with an RT_WG_TIMING build (RTGO_LIB): s
             dbg.zero_()
             ctx.render_async(W, 1, st, lin.data_ptr(), rgba.data_ptr(), torch.cuda.current_stream().cuda_stream)
             torch.cuda.synchronize()
-        d = dbg.cpu().numpy().reshape(-1, 32)
+        d = dbg.cpu().numpy().reshape(-1, 48)
         d = d[d[:, 0] != 0]
         for r in d:
             it = max(int(r[7]), 1)

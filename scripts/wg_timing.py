@@ -35,7 +35,7 @@ st.samples = SPP
 lin = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
 rgba = torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda")
 nwg_max = 200_000
-dbg = torch.zeros(nwg_max * 32, dtype=torch.int64, device="cuda")
+dbg = torch.zeros(nwg_max * 48, dtype=torch.int64, device="cuda")
 ctx.set_debug_buffer(dbg.data_ptr())
 RANK, WORLD = int(os.environ.get("WG_RANK", "0")), int(os.environ.get("WG_WORLD", "1"))
 if os.environ.get("WG_DEPTH"):
@@ -49,7 +49,7 @@ for _ in range(2):
     torch.cuda.synchronize()
 print(f"kernel {e0.elapsed_time(e1):.3f} ms (rank {RANK}/{WORLD}, depth {st.max_depth})")
 WPG = int(os.environ.get("WG_WAVES", "1"))  # waves per workgroup of the kernel
-d = dbg.cpu().numpy().reshape(-1, WPG, 32)
+d = dbg.cpu().numpy().reshape(-1, WPG, 48)
 used = d[:, 0, 0] != 0
 d = d[used]
 nwg = d.shape[0]
@@ -100,3 +100,10 @@ print(f"  WGs ending after 70% of the span: {int(late.sum())}; of them split {in
       f"mean iters {it[late].mean():.0f}, mean start {start[late].mean():.0f} us")
 busy = dur.sum()
 print(f"  mean waves in flight {busy / span:.1f}")
+bclk = d[:, 0, 32:37].astype(np.float64)
+bcnt = d[:, 0, 37:42].astype(np.float64)
+names = ["1", "2", "3-4", "5-8", ">8"]
+for label, sel in (("all WGs", np.ones(nwg, bool)), ("WGs ending after 70% of the span", late)):
+    c, n = bclk[sel].sum(axis=0), bcnt[sel].sum(axis=0)
+    print(f"  {label}: shade iterations by live lanes " + ", ".join(
+        f"{names[i]}: {int(n[i])} it {c[i] / max(c.sum(), 1):.0%} clk ({c[i] / max(n[i], 1):.0f}/it)" for i in range(5)))
