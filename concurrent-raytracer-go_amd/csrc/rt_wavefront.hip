@@ -513,6 +513,12 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade1(const WfParams p) {
   }
   const int shard = blockIdx.x % kWfShards;
   uint32_t* hq = p.hardq + (size_t)shard * p.hard_cap;
+  // The hard ray is first tested against the hit sphere itself: a ray that
+  // leaves through the sphere (the light behind the surface, or a path
+  // inside a glass sphere) is blocked by it, and an occlusion query's answer
+  // does not depend on which hittable blocks it, so it is settled here
+  // without a traversal (exact: the same Sphere.Hit test).
+  const DSphere* S0 = hit ? &p.g.spheres[p.hidx[slot]] : nullptr;
   // lights in chunks of 32 (one bit each; any number of lights)
   for (int base = 0; base < p.nl; base += 32) {
     uint32_t lit = 0;
@@ -522,12 +528,19 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade1(const WfParams p) {
         d3 ldir;
         double ldist;
         light_vec(p.lights[li], P, ldir, ldist);
-        p.lstate[slot * p.nl + li] = 0;
+        uint32_t st = 0;
         if (!(ldist < 0.001)) {
           cnt<kCount>(c, C_LIGHT);
           cnt<kCount>(c, C_SHADOW);
-          lit |= 1u << (li - base);
+          cnt<kCount>(c, C_SPH);
+          const double a = len2(ldir);
+          double num;
+          if (sphere_query(*S0, P, ldir, a, approx_rcp(a), 0.001, ldist, num))
+            st = kHardBit;
+          else
+            lit |= 1u << (li - base);
         }
+        p.lstate[slot * p.nl + li] = st;
       }
     }
     int q = block_append(__popc(lit), &p.ctl->hard_cnt[shard * 32], s_wave, &s_base);
