@@ -321,7 +321,7 @@ void rt_comm_destroy(rt_comm* comm);
 int rt_comm_gather_tiles_async(rt_comm* comm, int32_t width, int32_t height, const void* d_share, void* d_gathered,
                                void* hip_stream);
 
-/* Debug hook: a device buffer of 32 u64 per workgroup (8 per wave) that
+/* Debug hook: a device buffer of 48 u64 per workgroup that
  * RT_WG_TIMING builds of the kernel fill: s_memrealtime at start / loop end
  * / end, then s_memtime clocks spent in closest hit, lighting and soft
  * shadows, coop/sequential soft-shadow counts and loop iterations
