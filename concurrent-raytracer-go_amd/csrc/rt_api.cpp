@@ -77,8 +77,10 @@ static int validate_settings(const rt_settings* st, int32_t w, int32_t h) {
     set_error("invalid image size " + std::to_string(w) + "x" + std::to_string(h));
     return RT_E_INVALID;
   }
-  if (st->samples < 0 || st->samples > kMaxBlockSamples) {
-    set_error("samples must be in [0, " + std::to_string(kMaxBlockSamples) + "]");
+  // (any count: more than kMaxBlockSamples render in sample passes; the
+  // bound keeps pixel x sample ids of a frame in 32 bits on every path)
+  if (st->samples < 0 || (long long)st->samples * w * h >= (1LL << 40) || st->samples > (1 << 24)) {
+    set_error("samples must be in [0, 2^24] with width * height * samples < 2^40");
     return RT_E_INVALID;
   }
   if (st->sky < RT_SKY_NONE || st->sky > RT_SKY_NIGHT) {
@@ -124,6 +126,8 @@ struct rt_context {
   int32_t nsplit = 0;       // split pixels of the current schedule
   char* d_split = nullptr;  // their per-sample radiance rows + sub-block counters
   size_t split_cap = 0;
+  void* d_acc = nullptr;  // sample passes: running per-pixel sums (KParams.acc)
+  size_t acc_cap = 0;
   char* d_pilot = nullptr;  // pilot render scratch: packed float3 + rgba + path lengths (max, sum)
   size_t pilot_cap = 0;
   // measured schedule (rt_tuning.measure): 0 none, 1 the next render measures
@@ -219,6 +223,7 @@ void rt_context_destroy(rt_context* c) {
 
   if (c->d_blocks) (void)hipFree(c->d_blocks);
   if (c->d_pilot) (void)hipFree(c->d_pilot);
+  if (c->d_acc) (void)hipFree(c->d_acc);
   if (c->d_meas) (void)hipFree(c->d_meas);
   if (c->d_split) (void)hipFree(c->d_split);
   if (c->d_sched) (void)hipFree(c->d_sched);
@@ -456,6 +461,10 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
       q.split_rad = nullptr;
       q.split_hits = nullptr;
       q.split_cnt = nullptr;
+      q.acc = nullptr;
+      q.acc_mode = 0;
+      q.sample_base = 0;
+      q.spp_total = 1;
       HIP_TRY(hipMemsetAsync(plen, 0, 2 * npx * sizeof(unsigned int), s));
       e = launch_render(q, false, s);
       if (e != hipSuccess) {
@@ -749,36 +758,63 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   hipStream_t s = (hipStream_t)stream;
   if (c->have_timing && s != c->last_stream) HIP_TRY(hipStreamWaitEvent(s, c->ev1, 0));
   const bool wf = use_wavefront(c);
-  if (!wf) {
-    rc = prepare_schedule(c, &p, st, s);
+  // The megakernel holds at most kMaxBlockSamples samples of a pixel in one
+  // block: more samples per pixel render as consecutive SAMPLE PASSES of at
+  // most that many, each continuing every pixel's running sum in sample
+  // order (KParams.acc), so the sum is tracePixel's bit for bit.
+  const int spp = st->samples;
+  const int npass = wf ? 1 : std::max(1, (spp + kMaxBlockSamples - 1) / kMaxBlockSamples);
+  p.spp_total = spp;
+  if (npass > 1) {
+    rc = grow(&c->d_acc, &c->acc_cap, (size_t)rt_tiles_for_rank(w, h, rank, world) * 1024 * 3 * sizeof(double));
     if (rc) return rc;
+    p.acc = (double*)c->d_acc;
   }
-  p.num_wgs = p.num_blocks;
-  // the first frame of a new schedule measures every pixel's paths (the same
-  // image; a separate instantiation records the lengths): the next frame's
-  // blocks are cut from them (prepare_schedule)
+  unsigned long long total[16] = {0};
   bool measuring = false;
-  if (!wf && c->meas_state == 1 && !counts && st->sky == RT_SKY_NONE && p.num_blocks > 0) {
-    const size_t npx = (size_t)rt_tiles_for_rank(w, h, rank, world) * 1024;
-    rc = grow(&c->d_meas, &c->meas_cap, npx * 8);
-    if (rc) return rc;
-    p.work_max = (unsigned int*)c->d_meas;
-    p.work_sum = p.work_max + npx;
-    measuring = true;
-  }
-  if (counts) HIP_TRY(hipMemsetAsync(c->d_counts, 0, 16 * sizeof(unsigned long long), s));
-  if (!wf && c->nsplit)  // split pixels: hit bits and sub-block counters start at zero
-    HIP_TRY(hipMemsetAsync(p.split_hits, 0, split_flags_bytes(c->nsplit, st->samples), s));
-  if (measuring) HIP_TRY(hipMemsetAsync(c->d_meas, 0, (size_t)rt_tiles_for_rank(w, h, rank, world) * 1024 * 8, s));
-  HIP_TRY(hipEventRecord(c->ev0, s));
-  if (wf) {
-    rc = render_wavefront(c, p, st, s, counts != nullptr);
-    if (rc) return rc;
-  } else {
-    int e = launch_render(p, counts != nullptr, s);
-    if (e != hipSuccess) {
-      set_error(std::string("render launch failed: ") + hipGetErrorString((hipError_t)e));
-      return RT_E_DEVICE;
+  for (int pass = 0; pass < npass; ++pass) {
+    rt_settings ps = *st;
+    const int s0 = (int)((long long)spp * pass / npass), s1 = (int)((long long)spp * (pass + 1) / npass);
+    ps.samples = s1 - s0;
+    p.spp = ps.samples;
+    p.sample_base = s0;
+    p.acc_mode = npass > 1 ? ((pass > 0 ? 1 : 0) | (pass < npass - 1 ? 2 : 0)) : 0;
+    if (!wf) {
+      rc = prepare_schedule(c, &p, &ps, s);
+      if (rc) return rc;
+    }
+    p.num_wgs = p.num_blocks;
+    // the first frame of a new schedule measures every pixel's paths (the same
+    // image; a separate instantiation records the lengths): the next frame's
+    // blocks are cut from them (prepare_schedule)
+    if (!wf && npass == 1 && c->meas_state == 1 && !counts && st->sky == RT_SKY_NONE && p.num_blocks > 0) {
+      const size_t npx = (size_t)rt_tiles_for_rank(w, h, rank, world) * 1024;
+      rc = grow(&c->d_meas, &c->meas_cap, npx * 8);
+      if (rc) return rc;
+      p.work_max = (unsigned int*)c->d_meas;
+      p.work_sum = p.work_max + npx;
+      measuring = true;
+    }
+    if (counts) HIP_TRY(hipMemsetAsync(c->d_counts, 0, 16 * sizeof(unsigned long long), s));
+    if (!wf && c->nsplit)  // split pixels: hit bits and sub-block counters start at zero
+      HIP_TRY(hipMemsetAsync(p.split_hits, 0, split_flags_bytes(c->nsplit, ps.samples), s));
+    if (measuring) HIP_TRY(hipMemsetAsync(c->d_meas, 0, (size_t)rt_tiles_for_rank(w, h, rank, world) * 1024 * 8, s));
+    if (pass == 0) HIP_TRY(hipEventRecord(c->ev0, s));
+    if (wf) {
+      rc = render_wavefront(c, p, st, s, counts != nullptr);
+      if (rc) return rc;
+    } else {
+      int e = launch_render(p, counts != nullptr, s);
+      if (e != hipSuccess) {
+        set_error(std::string("render launch failed: ") + hipGetErrorString((hipError_t)e));
+        return RT_E_DEVICE;
+      }
+    }
+    if (counts) {
+      unsigned long long h_c[16];
+      HIP_TRY(hipMemcpyAsync(h_c, c->d_counts, sizeof h_c, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      for (int i = 0; i < 16; ++i) total[i] += h_c[i];
     }
   }
   HIP_TRY(hipEventRecord(c->ev1, s));
@@ -786,9 +822,7 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   c->last_stream = s;
   c->have_timing = true;
   if (counts) {
-    unsigned long long h_c[16];
-    HIP_TRY(hipMemcpyAsync(h_c, c->d_counts, sizeof h_c, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    const unsigned long long* h_c = total;
     counts->camera_rays = h_c[0];
     counts->bounce_rays = h_c[1];
     counts->shadow_rays = h_c[2];

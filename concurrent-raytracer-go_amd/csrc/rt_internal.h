@@ -139,6 +139,14 @@ struct KParams {
   int32_t num_blocks;        // this rank's blocks (one workgroup each)
   int32_t layout;     // RT_LAYOUT_*
   int32_t num_wgs;         // = num_blocks
+  // sample passes (more samples per pixel than a block holds, DESIGN.md
+  // §4.1): this launch renders samples [sample_base, sample_base + spp) of
+  // spp_total; acc holds each local pixel's running sum (lt * 1024 + pixel,
+  // 3 doubles) between passes.  acc_mode: bit 0 = start from acc (not the
+  // first pass), bit 1 = store the sum to acc instead of writing the image
+  // (not the last pass).  Single pass: acc_mode 0, spp_total = spp.
+  double* acc;
+  int32_t sample_base, spp_total, acc_mode;
 };
 
 // Enqueue the render kernel; returns hipError_t as int.

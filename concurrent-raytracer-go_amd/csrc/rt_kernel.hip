@@ -686,9 +686,19 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   // a black block (up to 64 pixels x spp samples) sets no hit bits
   const int nwords = blk.black ? 0 : (blk.np * blk.ns + 31) >> 5;
   if (lane < nwords) hbits[lane] = 0;
-  psum[lane][0] = 0;
-  psum[lane][1] = 0;
-  psum[lane][2] = 0;
+  {
+    // a later sample pass continues each pixel's running sum (acc_mode bit 0)
+    double a0 = 0, a1 = 0, a2 = 0;
+    if ((pk.acc_mode & 1) && blk.slot < 0 && lane < blk.np && blk.p0 + lane < 1024) {
+      const double* a = pk.acc + ((size_t)blk.lt * 1024 + blk.p0 + lane) * 3;
+      a0 = a[0];
+      a1 = a[1];
+      a2 = a[2];
+    }
+    psum[lane][0] = a0;
+    psum[lane][1] = a1;
+    psum[lane][2] = a2;
+  }
   if constexpr (kStage) {
     // LDS-staged scene primitives: spheres | triangles | boxes | materials |
     // lights [| jump table] (one contiguous prefix of the device scene buffer), so the
@@ -747,7 +757,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     const int W = k->W, H = k->H;
     // traceRay's depth cut-off comes first: with max_depth <= 0 every sample is black
     const bool live = loc.tile < k->ntiles, trace = k->max_depth > 0;
-    const int x0 = loc.tx * 32, y0 = loc.ty * 32, p0 = loc.p0, s0 = loc.s0;
+    const int x0 = loc.tx * 32, y0 = loc.ty * 32, p0 = loc.p0, s0 = loc.s0, sbase = k->sample_base;
     const Hot h = hot<kStage>();
     // id / ns by a multiply-high with m = floor((2^32 - 1) / ns) + 1: exact
     // for id, ns < 2^16 (NB <= kMaxBlockSamples); ns == 1 has no 32-bit m
@@ -771,7 +781,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       cnt<kCount>(c, C_CAM);
       rt_rng rng;
       d3 o, d;
-      camera_ray_c<kCount>(ck, x, y, s, rng, o, d, c);
+      camera_ray_c<kCount>(ck, x, y, sbase + s, rng, o, d, c);
       if (!trace) continue;
       cnt<kCount>(c, C_BOUNCE);
       // hit or miss is all this phase needs: an any-hit query over
@@ -904,7 +914,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
         KArg k = fresh();
         const BlockLoc loc = block_loc(k, blockIdx.x);
         const int id = entry_id(e), ns = loc.ns;
-        const int p = id / ns, s = loc.s0 + id - p * ns;
+        const int p = id / ns, s = k->sample_base + loc.s0 + id - p * ns;
         const int tp = loc.p0 + p;
         Counters nc;  // phase 1 counted this camera ray and its draws
         camera_ray<false>(k, loc.tx * 32 + (tp & 31), loc.ty * 32 + (tp >> 5), s, rng, o, d, nc);
@@ -1201,7 +1211,8 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       const uint32_t* hw = k->split_hits + (size_t)blk.slot * ((k->spp + 31) >> 5);
       // chunks of kRound samples: all lanes load (in parallel) into the LDS
       // slots, misses as +0, then one lane per channel adds them in order
-      double a = 0;
+      double a = 0;  // (a later sample pass continues the running sum)
+      if ((k->acc_mode & 1) && lane < 3) a = k->acc[((size_t)blk.lt * 1024 + blk.p0) * 3 + lane];
       for (int c0 = 0; c0 < k->spp; c0 += kRound) {
         const int cn = min(kRound, k->spp - c0);
         for (int i = lane; i < cn; i += 64) {
@@ -1225,8 +1236,13 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     const int p = lane;
     const int tp = loc.p0 + p;
     const int x = loc.tx * 32 + (tp & 31), y = loc.ty * 32 + (tp >> 5);
-    if (p < loc.np && tp < 1024 && loc.tile < k->ntiles && x < k->W && y < k->H) {
-      const double n = (double)k->spp;
+    if ((k->acc_mode & 2) && p < loc.np && tp < 1024) {  // not the last sample pass: keep the running sum
+      double* a = k->acc + ((size_t)loc.lt * 1024 + tp) * 3;
+      a[0] = psum[p][0];
+      a[1] = psum[p][1];
+      a[2] = psum[p][2];
+    } else if (p < loc.np && tp < 1024 && loc.tile < k->ntiles && x < k->W && y < k->H) {
+      const double n = (double)k->spp_total;
       const double mx = psum[p][0] / n, my = psum[p][1] / n, mz = psum[p][2] / n;  // DivScalar(float64(samples))
       const size_t oi = k->layout == RT_LAYOUT_IMAGE ? (size_t)y * k->W + x : (size_t)loc.lt * 1024 + (size_t)tp;
       if (k->out_linear) {

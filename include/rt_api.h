@@ -113,7 +113,8 @@ typedef struct {
 /* Renderer settings — the ParallelRenderer fields (renderer.go:20-29) and
  * their setters (settings.go:3-25).  Defaults: rt_settings_default(). */
 typedef struct {
-  int32_t samples;               /* SetSamples; default 100 */
+  int32_t samples;               /* SetSamples; default 100; any count in [0, 2^24] with W*H*samples < 2^40
+                                    (past 1024 the linear-scan kernel renders in sample passes) */
   int32_t max_depth;             /* SetMaxDepth; default 50 */
   int32_t anti_aliasing;         /* SetAntiAliasing; inert in the reference (jitter is unconditional, renderer.go:155-156) */
   int32_t recursive_reflections; /* SetRecursiveReflections; default 1 */

@@ -197,3 +197,16 @@ def test_image_size_bounds_are_checked_before_the_device():
         with pytest.raises(rtgo.RenderError) as e:
             r.render(s, w, h)
         assert "image size" in str(e.value)
+
+
+def test_sample_counts_beyond_one_block_are_accepted():
+    """SetSamples takes any count in the reference (settings.go:3-5): more
+    samples than a block holds are rendered in sample passes, so rt_validate
+    accepts them; only negative or absurd counts are rejected."""
+    lib = rtgo.lib()
+    s = rtgo.Scene.load_from_file(os.path.join(ROOT, "scenes", "sphere_reflections_light_facing.json"))
+    st = rtgo.default_settings()
+    for n, ok in ((0, True), (1024, True), (1025, True), (4096, True), (-1, False), ((1 << 24) + 1, False)):
+        st.samples = n
+        rc = lib.rt_validate(ctypes.byref(s.view), 64, 48, ctypes.byref(st))
+        assert (rc == 0) == ok, (n, rc)

@@ -144,3 +144,25 @@ def test_opt_in_sky_on_the_wavefront_path():
     rmse, maxd, rgba_mis = _compare(lin_g, rgba_g, lin_r, rgba_r)
     print(f"wavefront sky: rmse={rmse} max|d|={maxd:.3e} rgba_mismatch={rgba_mis:.2e}")
     assert np.all(rmse < 1e-7) and maxd < 1e-6 and rgba_mis < 1e-3
+
+
+@pytest.mark.parametrize("case,spp", [(("spheres_facing", ("file", "sphere_reflections_light_facing.json")), 2100),
+                                      (("silver_facing", ("file", "final_silver_prism_purple_cube_facing.json")),
+                                       1500)], ids=["spheres_2100spp", "silver_1500spp"])
+def test_sample_passes_match_oracle(case, spp):
+    """More samples per pixel than a block holds (1024) render as sample
+    passes that continue every pixel's running sum (rt_api.cpp,
+    KParams.acc): SetSamples takes any count in the reference
+    (settings.go:3-5), and the image is still tracePixel's sum in sample
+    order, bit for bit.  The frames are crops around the objects, where
+    pixels are heavy enough to be split into sample ranges too."""
+    name, loader = case
+    scene = load_case(rtgo, loader)
+    w, h = 20, 14
+    st = make_settings(rtgo, {"samples": spp}, 6)
+    lin_g, rgba_g = _render_gpu(scene, w, h, st)
+    lin_r, rgba_r, _ = oracle.render(scene, w, h, st)
+    rmse, maxd, rgba_mis = _compare(lin_g, rgba_g, lin_r, rgba_r)
+    print(f"{name} {spp} spp: rmse={rmse} max|d|={maxd:.3e} lit={np.mean(rgba_r[..., :3] > 0):.2f}")
+    assert (rgba_r[..., :3] > 0).any()
+    assert maxd == 0.0 and rgba_mis == 0.0, (name, maxd, rgba_mis)
