@@ -148,14 +148,14 @@ def test_opt_in_sky_on_the_wavefront_path():
 
 @pytest.mark.parametrize("case,spp", [(("spheres_facing", ("file", "sphere_reflections_light_facing.json")), 2100),
                                       (("silver_facing", ("file", "final_silver_prism_purple_cube_facing.json")),
-                                       1500)], ids=["spheres_2100spp", "silver_1500spp"])
+                                       1501)], ids=["spheres_2100spp", "silver_1501spp"])
 def test_sample_passes_match_oracle(case, spp):
     """More samples per pixel than a block holds (1024) render as sample
     passes that continue every pixel's running sum (rt_api.cpp,
     KParams.acc): SetSamples takes any count in the reference
     (settings.go:3-5), and the image is still tracePixel's sum in sample
-    order, bit for bit.  The frames are crops around the objects, where
-    pixels are heavy enough to be split into sample ranges too."""
+    order, bit for bit.  1501 = 750 + 751: the passes differ in size, so the
+    work schedule is rebuilt between them on the same stream."""
     name, loader = case
     scene = load_case(rtgo, loader)
     w, h = 20, 14
