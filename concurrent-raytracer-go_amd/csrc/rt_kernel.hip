@@ -43,7 +43,9 @@
 #include "rt_internal.h"
 
 // waves per SIMD of render_kernel: measured best of 2/3/4 (4 spills the FP64 path state)
+#ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 3
+#endif
 // cooperative soft shadows when at most this many lanes need them (measured
 // best of 0/2/4/8 in round 1; 4 and 16 within noise in round 2)
 constexpr int kCoopMax = 8;
@@ -881,11 +883,26 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     }
   };
   if (nh > 0) {
-    d3 o = mk(0, 0, 0), d = mk(0, 0, 0), T = mk(1, 1, 1), L = mk(0, 0, 0);
+    d3 o = mk(0, 0, 0), d = mk(0, 0, 0), T = mk(1, 1, 1);
     rt_rng rng{0};
     int depth = 0, entry = 0;
     bool alive = false;
     int next = 0, resolved = 0;  // wave-uniform: next entry to start; entries [0, resolved) summed
+    // The path's radiance L lives in its entry's ring slot (the slot is the
+    // path's own until it finishes, and resolve_entries reads it only then):
+    // read and written once per bounce, in VGPRs it held 6 registers through
+    // the lighting section and pushed the loop into scratch spills
+    // (scratch 40 -> 28 B/lane; headline 0.79 -> 0.775 ms).  Macros: the
+    // same accessors as lambdas came out with 40 B/lane of scratch again.
+#define path_L() mk(slot[entry & (kRound - 1)][0], slot[entry & (kRound - 1)][1], slot[entry & (kRound - 1)][2])
+#define set_path_L(v)                    \
+  do {                                   \
+    const d3 v_ = (v);                   \
+    const int q_ = entry & (kRound - 1); \
+    slot[q_][0] = v_.x;                  \
+    slot[q_][1] = v_.y;                  \
+    slot[q_][2] = v_.z;                  \
+  } while (0)
     for (;;) {
       const unsigned long long freem = __ballot(!alive);
       int limit = min(nh, resolved + kRound);
@@ -918,10 +935,10 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
         const int tp = loc.p0 + p;
         Counters nc;  // phase 1 counted this camera ray and its draws
         camera_ray<false>(k, loc.tx * 32 + (tp & 31), loc.ty * 32 + (tp >> 5), s, rng, o, d, nc);
-        T = mk(1, 1, 1);
-        L = mk(0, 0, 0);
-        depth = 0;
         entry = e;
+        T = mk(1, 1, 1);
+        set_path_L(mk(0, 0, 0));
+        depth = 0;
         alive = true;
       }
       next = min(limit, next + __popcll(freem));
@@ -951,7 +968,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
         // (two or three paths run one after the other this way measured
         // slower: 0.79 / 0.93 vs 0.78 ms)
         if (__popcll(am) == 1 && hot<kStage>().masks) {
-          const d3 Lr = solo_path<kSky>(__builtin_ctzll(am), o, d, T, L, rng.x, depth, stack);
+          const d3 Lr = solo_path<kSky>(__builtin_ctzll(am), o, d, T, path_L(), rng.x, depth, stack);
           if (lane == __builtin_ctzll(am)) {
             const int q = entry & (kRound - 1);
             slot[q][0] = Lr.x;
@@ -1001,7 +1018,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
         if (done) {
           fin = true;
           if constexpr (kSky) {  // an opted-in sky instead of black (rt_settings.sky)
-            if (missed) L = L + mul(T, sky_color(fresh()->sky, d));
+            if (missed) set_path_L(path_L() + mul(T, sky_color(fresh()->sky, d)));
           }
         } else {
           shade = true;
@@ -1153,10 +1170,10 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
           d3 E = ld3(m->emit);
           const Scat sc = scatter<kCount>(m, d, N, front, rng, c);
           if (!sc.ok) {
-            L = L + mul(T, E + D);
+            set_path_L(path_L() + mul(T, E + D));
             fin = true;
           } else {
-            L = L + mul(T, E + muls(D, m->dw));
+            set_path_L(path_L() + mul(T, E + muls(D, m->dw)));
             fin = !h.recursive || depth + 1 >= h.max_depth;
             if (!fin) {
               T = mul(T, muls(sc.A, m->rw));
@@ -1178,17 +1195,15 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
           atomicMax(k->work_max + px, (unsigned)depth + 1u);
           atomicAdd(k->work_sum + px, (unsigned)depth + 1u);
         }
-        const int q = entry & (kRound - 1);
-        slot[q][0] = L.x;
-        slot[q][1] = L.y;
-        slot[q][2] = L.z;
-        alive = false;
+        alive = false;  // (its radiance is in its slot already)
       }
     }
     __syncthreads();
     resolve_entries(resolved, nh);
     __syncthreads();
   }
+#undef path_L
+#undef set_path_L
 #ifdef RT_WG_TIMING
   const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
   if (dbg_bprev >= 0) dbg_bclk[dbg_bprev] += __builtin_amdgcn_s_memtime() - dbg_bts;

@@ -27,6 +27,8 @@ if SCENE == "spheres10k":
     g = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(g)
     ctx.set_scene(rtgo.Scene.from_json_text(g.dumps(g.generate(10000))))
+elif SCENE == "committed":  # the as-committed headline scene: black blocks only (the epilogue's stores alone)
+    ctx.set_scene(rtgo.Scene.load_from_file(os.path.join(ROOT, "scenes", "sphere_reflections_light.json")))
 else:
     ctx.set_scene(rtgo.Scene.load_from_file(os.path.join(ROOT, "scenes", "sphere_reflections_light_facing.json")))
 lin = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
