@@ -494,6 +494,11 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
     const size_t need = (size_t)nsplit * st->samples * 3 * sizeof(double) + split_flags_bytes(nsplit, st->samples);
     rc = grow(&c->d_split, &c->split_cap, need + 256);
     if (rc) return rc;
+    // split pixels' hit bits and sub-block counters start at zero; each
+    // launch's last sub-block of a pixel zeroes them again (rt_kernel.hip)
+    if (nsplit)
+      HIP_TRY(hipMemsetAsync((char*)c->d_split + (size_t)nsplit * st->samples * 3 * sizeof(double), 0,
+                             split_flags_bytes(nsplit, st->samples), s));
     c->num_blocks = nblocks;
     c->nsplit = nsplit;
     memcpy(c->order_key, key, sizeof key);
@@ -796,8 +801,6 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
       measuring = true;
     }
     if (counts) HIP_TRY(hipMemsetAsync(c->d_counts, 0, 16 * sizeof(unsigned long long), s));
-    if (!wf && c->nsplit)  // split pixels: hit bits and sub-block counters start at zero
-      HIP_TRY(hipMemsetAsync(p.split_hits, 0, split_flags_bytes(c->nsplit, ps.samples), s));
     if (measuring) HIP_TRY(hipMemsetAsync(c->d_meas, 0, (size_t)rt_tiles_for_rank(w, h, rank, world) * 1024 * 8, s));
     if (pass == 0) HIP_TRY(hipEventRecord(c->ev0, s));
     if (wf) {

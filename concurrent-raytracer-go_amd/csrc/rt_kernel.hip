@@ -1223,7 +1223,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     if (resolve) {
       __threadfence();
       const double* row = k->split_rad + (size_t)blk.slot * k->spp * 3;
-      const uint32_t* hw = k->split_hits + (size_t)blk.slot * ((k->spp + 31) >> 5);
+      uint32_t* hw = k->split_hits + (size_t)blk.slot * ((k->spp + 31) >> 5);
       // chunks of kRound samples: all lanes load (in parallel) into the LDS
       // slots, misses as +0, then one lane per channel adds them in order
       double a = 0;  // (a later sample pass continues the running sum)
@@ -1243,6 +1243,10 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
         __syncthreads();
       }
       if (lane < 3) psum[0][lane] = a;
+      // the slot's hit bits and counter are left zeroed for the next launch
+      // (the host clears them only when it builds a schedule: no memset per frame)
+      for (int i = lane; i < ((k->spp + 31) >> 5); i += 64) hw[i] = 0u;
+      if (lane == 0) k->split_cnt[blk.slot] = 0;
       __syncthreads();
     }
   }
