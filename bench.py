@@ -327,6 +327,31 @@ def cpu_baseline(args, rtgo, scene, W, H, st, cfg):
     }
 
 
+def cpu_baseline_bvh(args, rtgo, scene, W, H, st):
+    """Secondary CPU baseline of the 10k-sphere configs: the
+    oracle with a sphere BVH and any-hit shadow rays (oracle_render_ex, the
+    same image), on the same tile sample as cpu_baseline but at the config's
+    full spp, so the GPU speedup's algorithmic share is visible."""
+    import oracle
+
+    threads, aff = host_threads(args)
+    ntl = 2 * threads
+    world = max(1, rtgo.num_tiles(W, H) // ntl)
+    t0 = time.perf_counter()
+    oracle.render(scene, W, H, st, rank=0, world=world, nthreads=threads, max_tiles=ntl, bvh=True)
+    secs = time.perf_counter() - t0
+    rays = ntl * 1024 * st.samples
+    return {
+        "value": round(rays / secs / 1e6, 3),
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port+bvh",
+        "sample": f"{ntl} tiles (every {world}th tile from tile 0) of the {W}x{H} frame at {st.samples} spp, depth "
+                  f"{st.max_depth}, one run ({secs:.1f} s); oracle/oracle.c with a median-split sphere BVH and "
+                  f"any-hit shadow rays on {threads} threads (not the reference's linear scans; same image)",
+    }
+
+
 def pmc_traffic(workload):
     """HBM bytes per launch from the committed rocprofv3 PMC passes
     (profiles/r02_pmc_traffic.json, scripts/pmc_traffic.py, with the gfx950
@@ -417,9 +442,10 @@ def main():
     achieved_gbs = hbm_bytes / kernel1_s / 1e9
     workload = "%s %dx%d %dspp depth %d" % (label, W, H, args.spp, args.depth)
 
-    cpu = None
+    cpu = cpu_bvh = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, rtgo, scene, W, H, sts[0], cfg)
+        cpu_bvh = cpu_baseline_bvh(args, rtgo, scene, W, H, sts[0]) if cfg in ("c4", "c5") else None
 
     if rank == 0:
         out = {
@@ -485,6 +511,9 @@ def main():
             out["gpu_over_cpu"] = round(value / cpu["value"], 1)
             if e2e:
                 out["render_e2e"]["vs_cpu"] = round(e2e["value"] / cpu["value"], 1)
+        if cpu_bvh:
+            out["cpu_baseline_bvh"] = cpu_bvh
+            out["gpu_over_cpu_bvh"] = round(value / cpu_bvh["value"], 1)
         print(json.dumps(out), flush=True)
     for c in comms:
         if c is not None:

@@ -47,6 +47,8 @@ def lib():
         ctypes.POINTER(rt.SceneView), i32, i32, ctypes.POINTER(rt.Settings), i32, i32, i32, i32, vp, vp,
         ctypes.POINTER(rt.Counts),
     ]
+    L.oracle_render_ex.restype = ctypes.c_int
+    L.oracle_render_ex.argtypes = L.oracle_render.argtypes + [i32]
     L.oracle_go_pow.restype = ctypes.c_double
     L.oracle_go_pow.argtypes = [ctypes.c_double, ctypes.c_double]
     L.oracle_go_max.restype = ctypes.c_double
@@ -84,8 +86,12 @@ def d3(v):
     return (ctypes.c_double * 3)(*v)
 
 
-def render(scene, width, height, settings, rank=0, world=1, nthreads=None, max_tiles=-1, counts=False):
-    """Render with the oracle. Returns (linear float64 (H,W,3), rgba uint8 (H,W,4), counts|None)."""
+def render(scene, width, height, settings, rank=0, world=1, nthreads=None, max_tiles=-1, counts=False, bvh=False):
+    """Render with the oracle. Returns (linear float64 (H,W,3), rgba uint8 (H,W,4), counts|None).
+
+    bvh=True: the secondary CPU baseline (sphere BVH + any-hit shadow rays,
+    oracle_render_ex) -- the same image, not the reference's algorithm; its
+    counts are not the reference's either."""
     rt = _rtgo()
     if nthreads is None:
         # the CPUs this process may run on, at most 16 (a GPU box's share)
@@ -96,9 +102,9 @@ def render(scene, width, height, settings, rank=0, world=1, nthreads=None, max_t
     lin = np.full((height, width, 3), np.nan, np.float64)
     rgba = np.zeros((height, width, 4), np.uint8)
     c = rt.Counts()
-    rc = lib().oracle_render(
+    rc = lib().oracle_render_ex(
         ctypes.byref(scene.view), width, height, ctypes.byref(settings), rank, world, nthreads, max_tiles,
-        lin.ctypes.data, rgba.ctypes.data, ctypes.byref(c),
+        lin.ctypes.data, rgba.ctypes.data, ctypes.byref(c), 1 if bvh else 0,
     )
     if rc != 0:
         raise RuntimeError(f"oracle_render failed: {rc}")

@@ -234,6 +234,9 @@ typedef struct {
   uint64_t seed_key;
   int W, H;
   int sky; /* RT_SKY_*: 0 = a miss is black (renderer.go:170-173) */
+  /* CPU-baseline variant only (oracle_render_ex use_bvh): a sphere BVH */
+  struct obvh_node* bvh;
+  int* bvh_prims; /* hittable index per leaf slot */
 } oscene;
 
 /* ------------------------------------------------------------ sky (opt-in)
@@ -551,8 +554,148 @@ static void make_cube(vec3 pos, vec3 size, otri out[12]) {
   }
 }
 
+/* ------------------------------------------------------------ CPU BVH
+ * NOT the reference: the reference scans every hittable (renderer.go:333-346).
+ * This median-split sphere BVH exists only for bench.py's secondary CPU
+ * baseline of the 10k-sphere configs ("cpu_ref with the
+ * build's BVH"), so the GPU speedup's algorithmic share is visible.  It
+ * returns the linear scan's closest hit: boxes are padded and tested with a
+ * slack, every sphere in a box the ray meets gets the exact Sphere.Hit, and
+ * equal t resolve to the larger hittable index as in the scan (the root a
+ * sphere contributes does not depend on the scan order: a root rejected
+ * against a smaller tMax is larger than it, and so is the other root). */
+typedef struct obvh_node {
+  double lo[3], hi[3];
+  int first, count; /* count 0: internal node, children first and first + 1 */
+} obvh_node;
+
+typedef struct {
+  obvh_node* nodes;
+  int n, cap;
+} obvh_build;
+
+static int bvh_axis;
+static const oscene* bvh_sc;
+static int bvh_cmp(const void* a, const void* b) {
+  double ca = (&bvh_sc->objs[*(const int*)a].center.x)[bvh_axis];
+  double cb = (&bvh_sc->objs[*(const int*)b].center.x)[bvh_axis];
+  return ca < cb ? -1 : (ca > cb ? 1 : 0);
+}
+
+static void bvh_bounds(const oscene* sc, const int* prims, int n, double lo[3], double hi[3]) {
+  for (int k = 0; k < 3; k++) {
+    lo[k] = INFINITY;
+    hi[k] = -INFINITY;
+  }
+  for (int i = 0; i < n; i++) {
+    const ohittable* h = &sc->objs[prims[i]];
+    const double* c = &h->center.x;
+    double r = fabs(h->radius);
+    for (int k = 0; k < 3; k++) {
+      double pad = 1e-9 * (fabs(c[k]) + r) + 1e-12;
+      if (c[k] - r - pad < lo[k]) lo[k] = c[k] - r - pad;
+      if (c[k] + r + pad > hi[k]) hi[k] = c[k] + r + pad;
+    }
+  }
+}
+
+/* node `at` covers prims[0, n): split at the median of the longest axis */
+static void bvh_split(obvh_build* b, const oscene* sc, int* prims, int base, int n, int at) {
+  obvh_node* nd = &b->nodes[at];
+  bvh_bounds(sc, prims + base, n, nd->lo, nd->hi);
+  if (n <= 4) {
+    nd->first = base;
+    nd->count = n;
+    return;
+  }
+  int axis = 0;
+  for (int k = 1; k < 3; k++)
+    if (nd->hi[k] - nd->lo[k] > nd->hi[axis] - nd->lo[axis]) axis = k;
+  bvh_axis = axis;
+  bvh_sc = sc;
+  qsort(prims + base, (size_t)n, sizeof(int), bvh_cmp);
+  const int child = b->n;
+  b->n += 2;
+  nd->first = child;
+  nd->count = 0;
+  bvh_split(b, sc, prims, base, n / 2, child);
+  bvh_split(b, sc, prims, base + n / 2, n - n / 2, child + 1);
+}
+
+static double slab_enter(const obvh_node* nd, oray r, const double* inv, double tmin, double tmax) {
+  double tn = tmin, tf = tmax;
+  for (int k = 0; k < 3; k++) {
+    const double o = (&r.o.x)[k];
+    double t0 = (nd->lo[k] - o) * inv[k], t1 = (nd->hi[k] - o) * inv[k];
+    if (t0 > t1) {
+      double t = t0;
+      t0 = t1;
+      t1 = t;
+    }
+    if (t0 > tn) tn = t0;
+    if (t1 < tf) tf = t1;
+  }
+  return tn <= tf + fabs(tf) * 1e-9 + 1e-12 ? tn : INFINITY;
+}
+
+/* closest hit (any = 0) or any hit (any = 1) in [tmin, tmax] through the BVH */
+static int hit_world_bvh(const oscene* sc, oray r, double tmin, double tmax, hitrec* out, int any) {
+  double inv[3];
+  for (int k = 0; k < 3; k++) {
+    const double d = (&r.d.x)[k];
+    inv[k] = 1.0 / (d != 0 ? d : 1e-300);
+  }
+  int stack[64], sp = 0, found = 0, best = -1;
+  double closest = tmax;
+  hitrec rec;
+  if (slab_enter(&sc->bvh[0], r, inv, tmin, closest) == INFINITY) return 0;
+  int cur = 0;
+  for (;;) {
+    const obvh_node* nd = &sc->bvh[cur];
+    if (nd->count == 0) {
+      const double tl = slab_enter(&sc->bvh[nd->first], r, inv, tmin, closest);
+      const double tr = slab_enter(&sc->bvh[nd->first + 1], r, inv, tmin, closest);
+      if (tl != INFINITY || tr != INFINITY) {
+        const int lfirst = tl <= tr;
+        if (tl != INFINITY && tr != INFINITY && sp < 64) stack[sp++] = lfirst ? nd->first + 1 : nd->first;
+        cur = lfirst ? nd->first : nd->first + 1;
+        continue;
+      }
+    } else {
+      for (int i = nd->first; i < nd->first + nd->count; i++) {
+        const int hi = sc->bvh_prims[i];
+        if (!sphere_hit(&sc->objs[hi], r, tmin, closest, &rec)) continue;
+        if (any) return 1;
+        if (rec.t == closest && found && best > hi) continue;
+        closest = rec.t;
+        best = hi;
+        *out = rec;
+        found = 1;
+      }
+    }
+    if (sp == 0) break;
+    cur = stack[--sp];
+  }
+  return found;
+}
+
+static void bvh_make(oscene* sc) {
+  for (int i = 0; i < sc->n; i++)
+    if (sc->objs[i].type != RT_OBJ_SPHERE || !isfinite(sc->objs[i].radius)) return;  /* spheres only */
+  if (sc->n < 2) return;
+  obvh_build b;
+  b.cap = 2 * sc->n + 1;
+  b.nodes = (obvh_node*)calloc((size_t)b.cap, sizeof(obvh_node));
+  b.n = 1;
+  sc->bvh_prims = (int*)malloc(sizeof(int) * (size_t)sc->n);
+  for (int i = 0; i < sc->n; i++) sc->bvh_prims[i] = i;
+  bvh_split(&b, sc, sc->bvh_prims, 0, sc->n, 0);
+  sc->bvh = b.nodes;
+}
+
 /* hitWorld, renderer.go:333-346 (+ Mesh.Hit, scene.go:196-209) */
 static int hit_world(const oscene* sc, oray r, double tmin, double tmax, hitrec* out, ocounts* c) {
+  if (sc->bvh) return hit_world_bvh(sc, r, tmin, tmax, out, 0);
   int found = 0;
   double closest = tmax;
   hitrec rec;
@@ -597,7 +740,8 @@ static double smart_shadow(const oscene* sc, const hitrec* h, int li, ostream* s
   oray sr = {h->p, ldir};
   hitrec tmp;
   s->c->shadow_rays++;
-  if (hit_world(sc, sr, 0.001, ldist, &tmp, s->c)) return 0.0;
+  if (sc->bvh ? hit_world_bvh(sc, sr, 0.001, ldist, &tmp, 1) : hit_world(sc, sr, 0.001, ldist, &tmp, s->c))
+    return 0.0;
   if (sc->soft) {
     double sum = 0.0;
     for (int i = 0; i < 16; i++) {
@@ -605,7 +749,8 @@ static double smart_shadow(const oscene* sc, const hitrec* h, int li, ostream* s
       vec3 sdir = vnorm(vadd(ldir, off));
       oray ss = {h->p, sdir};
       s->c->shadow_rays++;
-      if (!hit_world(sc, ss, 0.001, ldist, &tmp, s->c)) sum += 1.0;
+      if (!(sc->bvh ? hit_world_bvh(sc, ss, 0.001, ldist, &tmp, 1) : hit_world(sc, ss, 0.001, ldist, &tmp, s->c)))
+        sum += 1.0;
     }
     return sum / (double)16;
   }
@@ -828,6 +973,13 @@ static void* worker(void* arg) {
 int oracle_render(const rt_scene* scene, int32_t width, int32_t height, const rt_settings* st, int32_t rank,
                   int32_t world, int32_t nthreads, int32_t max_tiles, double* out_linear, uint8_t* out_rgba,
                   rt_counts* counts) {
+  return oracle_render_ex(scene, width, height, st, rank, world, nthreads, max_tiles, out_linear, out_rgba, counts,
+                          0);
+}
+
+int oracle_render_ex(const rt_scene* scene, int32_t width, int32_t height, const rt_settings* st, int32_t rank,
+                     int32_t world, int32_t nthreads, int32_t max_tiles, double* out_linear, uint8_t* out_rgba,
+                     rt_counts* counts, int32_t use_bvh) {
   if (!scene || !st || width <= 0 || height <= 0 || world < 1 || rank < 0 || rank >= world) return RT_E_INVALID;
   if (scene->num_objects < 0 || scene->num_lights < 0) return RT_E_INVALID;
   if (nthreads < 1) nthreads = 1;
@@ -868,6 +1020,7 @@ int oracle_render(const rt_scene* scene, int32_t width, int32_t height, const rt
   sc.seed_key = rt_rng_seed_key(st->seed);
   sc.W = width;
   sc.H = height;
+  if (use_bvh) bvh_make(&sc);
 
   ojob job;
   memset(&job, 0, sizeof job);
@@ -897,6 +1050,8 @@ int oracle_render(const rt_scene* scene, int32_t width, int32_t height, const rt
     counts->light_evals = job.total.light_evals;
     counts->rng_draws = job.total.rng_draws;
   }
+  free(sc.bvh);
+  free(sc.bvh_prims);
   free(sc.objs);
   free(sc.mats);
   free(sc.lpos);

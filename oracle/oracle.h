@@ -35,6 +35,14 @@ int oracle_render(const rt_scene* scene, int32_t width, int32_t height, const rt
                   int32_t rank, int32_t world, int32_t nthreads, int32_t max_tiles, double* out_linear,
                   uint8_t* out_rgba, rt_counts* counts);
 
+/* The same with use_bvh = 1: a sphere BVH and any-hit shadow rays instead of
+ * the reference's linear scans, for bench.py's secondary CPU baseline of the
+ * 10k-sphere configs -- NOT the reference's algorithm; same
+ * image (tests/test_oracle_render.py).  Scenes with cubes scan linearly. */
+int oracle_render_ex(const rt_scene* scene, int32_t width, int32_t height, const rt_settings* settings,
+                     int32_t rank, int32_t world, int32_t nthreads, int32_t max_tiles, double* out_linear,
+                     uint8_t* out_rgba, rt_counts* counts, int32_t use_bvh);
+
 /* Building blocks exposed for known-answer tests. */
 double oracle_go_pow(double x, double y);            /* math.Pow */
 double oracle_go_max(double x, double y);            /* math.Max */

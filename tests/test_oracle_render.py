@@ -96,3 +96,18 @@ def test_max_tiles_bounds_the_work():
     lin, _, c = oracle.render(scene, 96, 64, make_settings(rtgo, {"samples": 1}), max_tiles=2, counts=True)
     assert c["camera_rays"] == 2 * 32 * 32
     assert np.isnan(lin).any()  # unrendered tiles stay NaN-filled
+
+
+def test_bvh_baseline_renders_the_linear_scan_image():
+    """The secondary CPU baseline (oracle_render_ex with a sphere BVH and
+    any-hit shadow rays, bench.py c4/c5) renders exactly the image of the
+    reference's linear scans: a 2,000-sphere field of the C4 generator."""
+    from scene_cases import spheres10k_scene
+
+    scene = spheres10k_scene(rtgo, 2000)
+    st = make_settings(rtgo, {"samples": 2, "max_depth": 8}, seed=3)
+    lin, rgba, _ = oracle.render(scene, 40, 24, st)
+    lin_b, rgba_b, _ = oracle.render(scene, 40, 24, st, bvh=True)
+    assert (rgba[..., :3] > 0).mean() > 0.3
+    assert lin_b.tobytes() == lin.tobytes()
+    assert rgba_b.tobytes() == rgba.tobytes()
