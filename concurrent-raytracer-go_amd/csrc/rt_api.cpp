@@ -367,9 +367,10 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
   // whose bounces are long divergent traversals that need full waves more
   // than short blocks (C4: 2.10 s at 512, 1.77 s at 8192)
   // (triangle scenes: 256 -- a bounce there tests 12 triangles per cube, so
-  // fewer bounces make a block: silver C3 0.56 -> 0.46 ms; the sphere
-  // headline is best at 512: 0.80 vs 0.93 ms at 256)
-  double block_work = !f.bvh.empty() ? 8192.0 : (f.tris.empty() ? 512.0 : 256.0);
+  // fewer bounces make a block: silver C3 0.56 -> 0.46 ms; sphere scenes:
+  // 384 since solo paths (r02, headline 0.785 -> 0.745 ms; 320: 0.755,
+  // 448: 0.79, 512 was the r01 optimum)
+  double block_work = !f.bvh.empty() ? 8192.0 : (f.tris.empty() ? 384.0 : 256.0);
   if (tn.block_work > 0) block_work = std::max(1.0, tn.block_work);
   const bool pilot = tn.pilot != 0;
   // a sky makes every camera sample count (a miss returns the sky, not +0):
