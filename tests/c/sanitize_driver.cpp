@@ -140,6 +140,9 @@ int main(int argc, char** argv) {
     st.samples = 1;
     std::vector<double> out((size_t)64 * 36 * 3);
     CHECK(oracle_render(rt_scene_view(bigsb), 64, 36, &st, 5, 7, 2, 1, out.data(), nullptr, nullptr) == 0);
+    std::vector<double> outb((size_t)64 * 36 * 3);  // the BVH baseline variant renders the same pixels
+    CHECK(oracle_render_ex(rt_scene_view(bigsb), 64, 36, &st, 5, 7, 2, 1, outb.data(), nullptr, nullptr, 1) == 0);
+    for (size_t i = 0; i < out.size(); ++i) CHECK(memcmp(&out[i], &outb[i], sizeof(double)) == 0 || (out[i] != out[i]));
     rt_scene_free(bigsb);
   }
   printf("sanitize_driver: %d failures\n", failures);

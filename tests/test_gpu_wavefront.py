@@ -117,3 +117,18 @@ def test_more_than_32_lights_match_the_oracle():
     assert rgba.reshape(24, 40, 4).tobytes() == ref_rgba.tobytes()
     mk = _render(scene, 40, 24, st, mega=True)
     assert mk[0].tobytes() == lin.tobytes()
+
+
+def test_more_than_1024_samples_on_both_bvh_paths():
+    """A sample count past one block's 1024 on a BVH scene: the wavefront
+    path (no per-pixel limit) and the megakernel's BVH path (sample passes,
+    rt_api.cpp) both give the oracle's image."""
+    scene = rtgo.Scene.from_json_text(json.dumps(_sphere_field(300, seed=8)))
+    st = make_settings(rtgo, {"samples": 1100, "max_depth": 6}, seed=2)
+    w, h = 16, 12
+    ref, ref_rgba, _ = oracle.render(scene, w, h, st)
+    ref32 = ref.astype(np.float32).reshape(-1, 3)
+    for mega in (False, True):
+        lin, rgba, _ = _render(scene, w, h, st, mega)
+        assert lin.tobytes() == ref32.tobytes(), mega
+        assert rgba.tobytes() == ref_rgba.reshape(-1, 4).tobytes(), mega
