@@ -52,6 +52,11 @@ constexpr int kCoopMax = 8;
 
 namespace rtgo {
 
+// Set bits of a wave mask below the calling lane (v_mbcnt): no 64-bit
+// per-lane "below" mask has to stay live (it was spilled to scratch)
+__device__ __forceinline__ int lanes_below(unsigned long long m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 
 // ------------------------------------------------------------ culling
 // Shadow-cone culling (linear-scan scenes with <= 64 spheres and <= 64
@@ -158,7 +163,7 @@ __device__ __forceinline__ int wide_groups(bool need, unsigned long long qmask, 
                                            int& k, bool& helper) {
   const int lane = (int)(threadIdx.x & 63);
   const int S = nq <= 4 ? 16 : (nq <= 8 ? 8 : 4);
-  if (need) owner_tab[__popcll(qmask & ((1ull << lane) - 1ull))] = lane;
+  if (need) owner_tab[lanes_below(qmask)] = lane;
   __syncthreads();
   const int grp = lane / S;
   k = lane - grp * S;
@@ -217,7 +222,7 @@ __device__ __forceinline__ bool closest_wide(const Geo& g, bool need, unsigned l
       found = true;
     }
   }
-  const int lead = need ? __popcll(qmask & ((1ull << lane) - 1ull)) * S : lane;
+  const int lead = need ? lanes_below(qmask) * S : lane;
   const double fnum = __shfl(bnum, lead);
   const int fidx = __shfl(bidx, lead), ffound = __shfl((int)found, lead);
   fallback = need && !(__builtin_isfinite(o.x + o.y + o.z) && a > 0 && __builtin_isfinite(__shfl(a, lead)));
@@ -250,7 +255,7 @@ __device__ __forceinline__ unsigned long long cone_wide(const Geo& g, bool need,
     }
   }
   for (int off = S >> 1; off >= 1; off >>= 1) m |= __shfl_xor(m, off);
-  const int lead = need ? __popcll(qmask & ((1ull << lane) - 1ull)) * S : lane;
+  const int lead = need ? lanes_below(qmask) * S : lane;
   return __shfl(m, lead);
 }
 
@@ -271,14 +276,13 @@ __device__ __forceinline__ CoopOut soft_coop(const Geo p, bool masks, bool trace
                              const uint64_t* jump, int* stack, Counters& c) {
   const int lane = (int)(threadIdx.x & 63);
   int need = 16, unocc = 0, tries = 0;
-  const unsigned long long below = (1ull << lane) - 1ull;
   while (need > 0) {
     const uint64_t x0 = state_at3(x, jump, lane), x1 = x0 * RT_PCG_MULT + RT_PCG_INC,
                    x2 = x1 * RT_PCG_MULT + RT_PCG_INC;
     const uint32_t o0 = rt_pcg_out(x0), o1 = rt_pcg_out(x1), o2 = rt_pcg_out(x2);
     const bool acc = unit_ball_accept(o0, o1, o2);
     const unsigned long long am = __ballot(acc);
-    const int rank = __popcll(am & below);
+    const int rank = lanes_below(am);
     const bool chosen = acc && rank < need;
     const unsigned long long chm = __ballot(chosen);
     const int nch = __popcll(chm);
@@ -314,7 +318,6 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
   __shared__ uint4 sq[128];   // queued points: raw draws x, y, z, owner lane (a ring)
   __shared__ int sq_unocc[64];  // per owner: unoccluded rays
   const int lane = (int)(threadIdx.x & 63);
-  const unsigned long long below = (1ull << lane) - 1ull;
   sq_unocc[lane] = 0;
   int need = need_soft ? 16 : 0, free_rays = 0;  // free_rays: points of an owner with nothing to trace
   int head = 0, tail = 0;  // wave-uniform ring positions
@@ -334,7 +337,7 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
       }
     }
     const unsigned long long am = __ballot(acc);
-    if (acc) sq[(tail + __popcll(am & below)) & 127] = make_uint4(ux, uy, uz, (uint32_t)lane);
+    if (acc) sq[(tail + lanes_below(am)) & 127] = make_uint4(ux, uy, uz, (uint32_t)lane);
     tail += __popcll(am);
     const bool more = __ballot(need > 0) != 0;
     if (tail - head >= 64 || (!more && tail > head)) {
@@ -682,7 +685,6 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   // dynamic LDS (dyn_lds): [staged scene prefix (kStage)][BVH stack (stack_depth x 64 ints)]
 
   const int lane = threadIdx.x;
-  const unsigned long long below = (1ull << lane) - 1ull;
   int* stack = reinterpret_cast<int*>(dyn_lds + pk.stack_off) + lane;
   const BlockLoc blk = block_loc(fresh(), blockIdx.x);
   // a black block (up to 64 pixels x spp samples) sets no hit bits
@@ -752,7 +754,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       pxlive = loc.live;
     }
     // compact list of the live pixels (block-local indices)
-    if (lane < loc.np && ((pxlive >> lane) & 1ull)) lpix[__popcll(pxlive & below)] = (uint8_t)lane;
+    if (lane < loc.np && ((pxlive >> lane) & 1ull)) lpix[lanes_below(pxlive)] = (uint8_t)lane;
     __syncthreads();
     const int nlive = __popcll(pxlive);
     const CamK ck = cam_k(k);
@@ -926,7 +928,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
         }
       }
       // lanes without a path take the next entries, in lane order
-      const int e = next + __popcll(freem & below);
+      const int e = next + lanes_below(freem);
       if (!alive && e < limit) {
         KArg k = fresh();
         const BlockLoc loc = block_loc(k, blockIdx.x);
@@ -1211,13 +1213,17 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
 
   // ---- phase 3 (final): mean, tone map, one write per pixel
   KArg k = fresh();
+  // the lane id laundered (see resolve_entries): the LDS addresses of this
+  // epilogue are computed here, not kept live (spilled) from the prologue
+  int lane3;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(lane3) : "v"((int)threadIdx.x));
   bool resolve = true;
   if (blk.slot >= 0) {
     // a split pixel: the last of its sub-blocks to finish sums the hit
     // samples of the slot row in sample order (misses add +0) and writes it
     __threadfence();
     int old = 0;
-    if (lane == 0) old = atomicAdd(&k->split_cnt[blk.slot], 1);
+    if (lane3 == 0) old = atomicAdd(&k->split_cnt[blk.slot], 1);
     old = __builtin_amdgcn_readfirstlane(old);
     resolve = old == blk.nsub - 1;
     if (resolve) {
@@ -1227,10 +1233,10 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       // chunks of kRound samples: all lanes load (in parallel) into the LDS
       // slots, misses as +0, then one lane per channel adds them in order
       double a = 0;  // (a later sample pass continues the running sum)
-      if ((k->acc_mode & 1) && lane < 3) a = k->acc[((size_t)blk.lt * 1024 + blk.p0) * 3 + lane];
+      if ((k->acc_mode & 1) && lane3 < 3) a = k->acc[((size_t)blk.lt * 1024 + blk.p0) * 3 + lane3];
       for (int c0 = 0; c0 < k->spp; c0 += kRound) {
         const int cn = min(kRound, k->spp - c0);
-        for (int i = lane; i < cn; i += 64) {
+        for (int i = lane3; i < cn; i += 64) {
           const int s = c0 + i;
           const bool hit = (hw[s >> 5] >> (s & 31)) & 1u;
           slot[i][0] = hit ? row[3 * s + 0] : 0.0;
@@ -1238,21 +1244,21 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
           slot[i][2] = hit ? row[3 * s + 2] : 0.0;
         }
         __syncthreads();
-        if (lane < 3)
-          for (int i = 0; i < cn; ++i) a += slot[i][lane];
+        if (lane3 < 3)
+          for (int i = 0; i < cn; ++i) a += slot[i][lane3];
         __syncthreads();
       }
-      if (lane < 3) psum[0][lane] = a;
+      if (lane3 < 3) psum[0][lane3] = a;
       // the slot's hit bits and counter are left zeroed for the next launch
       // (the host clears them only when it builds a schedule: no memset per frame)
-      for (int i = lane; i < ((k->spp + 31) >> 5); i += 64) hw[i] = 0u;
-      if (lane == 0) k->split_cnt[blk.slot] = 0;
+      for (int i = lane3; i < ((k->spp + 31) >> 5); i += 64) hw[i] = 0u;
+      if (lane3 == 0) k->split_cnt[blk.slot] = 0;
       __syncthreads();
     }
   }
   if (resolve) {
     const BlockLoc loc = block_loc(k, blockIdx.x);
-    const int p = lane;
+    const int p = lane3;
     const int tp = loc.p0 + p;
     const int x = loc.tx * 32 + (tp & 31), y = loc.ty * 32 + (tp >> 5);
     if ((k->acc_mode & 2) && p < loc.np && tp < 1024) {  // not the last sample pass: keep the running sum
@@ -1279,11 +1285,11 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       // wave reduction, then one atomic per counter
       unsigned long long v = c.v[i];
       for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-      if (lane == 0) atomicAdd(&k->counts[i], v);
+      if (lane3 == 0) atomicAdd(&k->counts[i], v);
     }
   }
 #ifdef RT_WG_TIMING
-  if (k->dbg && lane == 0) {
+  if (k->dbg && lane3 == 0) {
     unsigned long long* r = k->dbg + (size_t)blockIdx.x * kDbgStride;
     r[0] = t_start;
     r[1] = t_loop;
