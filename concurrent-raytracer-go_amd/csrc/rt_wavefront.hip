@@ -57,8 +57,18 @@ constexpr int kTravBlock = kWfTravBlock;
 #define RT_WF_TRAV_WAVES 4  // waves per SIMD the traversal kernels are compiled for
 #define RT_TRAV_ATTR __launch_bounds__(kTravBlock) __attribute__((amdgpu_waves_per_eu(RT_WF_TRAV_WAVES)))
 constexpr int kLdsBytes = 160 * 1024;    // LDS per CU (MI355X), all of it available to one workgroup
-constexpr int kRefill = 16;              // persistent traversal: refill once this many lanes are idle
-constexpr int kChunk = 256;              // persistent traversal: jobs a wave takes per atomic
+// (measured r02, C4 per frame: chunk 256 / refill 16 640 ms, 128 / 16 596,
+// 64 / 16 594, 32 / 16 641, 64 / 24 591, 64 / 32 593, 64 / 48 632, 256 / 32
+// 627; smaller chunks shorten each persistent launch's drain, where waves
+// still hold unstarted jobs while others have none)
+#ifndef RT_WF_REFILL
+#define RT_WF_REFILL 24
+#endif
+#ifndef RT_WF_CHUNK
+#define RT_WF_CHUNK 64
+#endif
+constexpr int kRefill = RT_WF_REFILL;    // persistent traversal: refill once this many lanes are idle
+constexpr int kChunk = RT_WF_CHUNK;      // persistent traversal: jobs a wave takes per atomic
 constexpr uint32_t kHardBit = 1u << 16;
 // hidx of a path whose ray hit nothing while a sky is opted in: wf_shade1
 // ends it with the sky's radiance (GetSkyColor, atmosphere.go:100-135) --
