@@ -528,11 +528,16 @@ static bool use_wavefront(const rt_context* c) { return !c->flat.bvh.empty() && 
 
 // path slots per shard (a multiple of kWfBlockSlots: every shard receives the
 // survivors of the workgroups b % kWfShards == shard, at most shard_cap)
-static int wf_shard_cap(int nl, const rt_tuning& tn) {
-  long long cap = 1 << 21;
+// More slots mean fewer, longer bounce iterations (each persistent traversal
+// launch pays a fill and a drain): C4 with 2^20 slots 680 ms per frame, 2^21
+// 589, 2^22 536, 2^23 510, 1.5 * 2^23 501, 2^24 499.  No more slots than the
+// chunk has samples (a path slot holds one sample's path).
+static int wf_shard_cap(int nl, const rt_tuning& tn, uint64_t samples) {
+  long long cap = 1 << 24;
   if (tn.wf_paths > 0) cap = std::min(1ll << 24, (long long)tn.wf_paths);
-  // soft queues: cap * nl * 16 entries of 16 B, at most 2 GB; keys slot * nl + light fit 32 bits
-  cap = std::min<long long>(cap, (1ll << 27) / (16ll * std::max(nl, 1)));
+  cap = std::min<long long>(cap, (long long)std::min<uint64_t>(samples, 1ull << 40));
+  // soft queues: cap * nl * 16 entries of 16 B, at most 8 GB; keys slot * nl + light fit 32 bits
+  cap = std::min<long long>(cap, (1ll << 29) / (16ll * std::max(nl, 1)));
   const long long per = kWfShards * kWfBlockSlots;
   return (int)(std::max(1ll, cap / per) * kWfBlockSlots);
 }
@@ -540,7 +545,13 @@ static int wf_shard_cap(int nl, const rt_tuning& tn) {
 static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings* st, hipStream_t s, bool count) {
   const FlatScene& f = c->flat;
   const int nl = (int)f.lights.size();
-  const int shard_cap = wf_shard_cap(nl, c->tun);
+  const int local = rt_tiles_for_rank(kp.W, kp.H, kp.rank, kp.world);
+  const uint64_t local_px = (uint64_t)local * 1024;
+  const uint64_t spp = (uint64_t)std::max(st->samples, 1);
+  uint64_t max_chunk = kWfMaxChunkSamples;
+  if (c->tun.wf_chunk > 0) max_chunk = std::min<uint64_t>((uint64_t)c->tun.wf_chunk, max_chunk);
+  const uint64_t chunk_px = std::max<uint64_t>(1, std::min<uint64_t>(local_px, max_chunk / spp));
+  const int shard_cap = wf_shard_cap(nl, c->tun, chunk_px * spp);
   const size_t cap = (size_t)shard_cap * kWfShards;
   const size_t nlk = (size_t)std::max(nl, 1);
   const size_t qcap = cap * nlk;  // hard rays per shard: at most every light of every path of its workgroups
@@ -565,12 +576,6 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
     HIP_TRY(hipHostMalloc((void**)&c->wf_host, kWfRing * sizeof(WfCtl), hipHostMallocDefault));
     for (hipEvent_t& e : c->wf_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
-  const int local = rt_tiles_for_rank(kp.W, kp.H, kp.rank, kp.world);
-  const uint64_t local_px = (uint64_t)local * 1024;
-  const uint64_t spp = (uint64_t)std::max(st->samples, 1);
-  uint64_t max_chunk = kWfMaxChunkSamples;
-  if (c->tun.wf_chunk > 0) max_chunk = std::min<uint64_t>((uint64_t)c->tun.wf_chunk, max_chunk);
-  const uint64_t chunk_px = std::max<uint64_t>(1, std::min<uint64_t>(local_px, max_chunk / spp));
   const size_t rad_need = (size_t)(chunk_px * spp * 3 * sizeof(double));
   if (rad_need > c->wf_rad_bytes) {
     int rq = quiesce(c);

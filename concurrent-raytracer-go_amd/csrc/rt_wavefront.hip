@@ -57,15 +57,17 @@ constexpr int kTravBlock = kWfTravBlock;
 #define RT_WF_TRAV_WAVES 4  // waves per SIMD the traversal kernels are compiled for
 #define RT_TRAV_ATTR __launch_bounds__(kTravBlock) __attribute__((amdgpu_waves_per_eu(RT_WF_TRAV_WAVES)))
 constexpr int kLdsBytes = 160 * 1024;    // LDS per CU (MI355X), all of it available to one workgroup
-// (measured r02, C4 per frame: chunk 256 / refill 16 640 ms, 128 / 16 596,
-// 64 / 16 594, 32 / 16 641, 64 / 24 591, 64 / 32 593, 64 / 48 632, 256 / 32
-// 627; smaller chunks shorten each persistent launch's drain, where waves
-// still hold unstarted jobs while others have none)
+// (measured r02, C4 per frame with 2^21 path slots: chunk 256 / refill 16
+// 640 ms, 128 / 16 596, 64 / 16 594, 32 / 16 641, 64 / 24 591, 64 / 32 593,
+// 64 / 48 632, 256 / 32 627; with 2^22 slots: 64 / 24 549, 96 / 24 537,
+// 128 / 24 536, 64 / 32 552; guided chunks, min(256, left / (k waves)) with
+// k = 2, 4, 8: 551-569.  Smaller chunks shorten each persistent launch's
+// drain, where waves still hold unstarted jobs while others have none)
 #ifndef RT_WF_REFILL
 #define RT_WF_REFILL 24
 #endif
 #ifndef RT_WF_CHUNK
-#define RT_WF_CHUNK 64
+#define RT_WF_CHUNK 128
 #endif
 constexpr int kRefill = RT_WF_REFILL;    // persistent traversal: refill once this many lanes are idle
 constexpr int kChunk = RT_WF_CHUNK;      // persistent traversal: jobs a wave takes per atomic
