@@ -676,6 +676,8 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
       HIP_TRY(hipMemcpyAsync(c->wf_ctl, &init, sizeof init, hipMemcpyHostToDevice, s));
       // the first samples, then bounces until every sample has finished; the
       // host reads the loop state one bounce behind the GPU
+      p.live_bound = (int32_t)cap;
+      p.dry = 0;
       int e = wf_launch_bounce(p, true, count, s);
       if (e) return fail(e, "launch");
       std::swap(p.cur, p.next);
@@ -696,6 +698,11 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
           HIP_TRY(hipEventSynchronize(c->wf_ev[pr]));
           const WfCtl& h = c->wf_host[pr];
           if (h.live == 0 && h.dry) break;  // bounce `it` had nothing to do
+          // once dry, live counts only fall: bounce it + 1 has at most h.live paths
+          if (h.dry) {
+            p.live_bound = h.live;
+            p.dry = 1;
+          }
         }
       }
     }

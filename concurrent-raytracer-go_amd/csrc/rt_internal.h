@@ -204,6 +204,8 @@ struct WfParams {
   int32_t bvh_nodes;         // quantized nodes in all
   int32_t trav_block;        // threads per workgroup of the traversal kernels (<= kWfTravBlock)
   int32_t shard_cap;         // path slots per shard
+  int32_t live_bound;        // the host's bound on this bounce's live paths (launch sizes only)
+  int32_t dry;               // 1: every sample of the chunk has started (no regen work left)
   int64_t hard_cap, soft_cap;  // queue entries per shard
   uint32_t lp0;              // first local pixel of the chunk (local tile * 1024 + pixel in tile)
   double cam[3];

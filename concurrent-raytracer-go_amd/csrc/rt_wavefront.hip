@@ -956,7 +956,8 @@ int wf_lds_nodes(int stack_depth, int nodes, int block, int wgs_per_cu) {
 template <bool kCount>
 static int enqueue_regen_book(const WfParams& p, hipStream_t st) {
   const int slots = kWfShards * p.shard_cap;
-  hipLaunchKernelGGL((wf_regen<kCount>), dim3((slots + kWfBlock - 1) / kWfBlock), dim3(kWfBlock), 0, st, p);
+  // (once every sample has started, regen has nothing to do)
+  if (!p.dry) hipLaunchKernelGGL((wf_regen<kCount>), dim3((slots + kWfBlock - 1) / kWfBlock), dim3(kWfBlock), 0, st, p);
   hipLaunchKernelGGL(wf_book, dim3(1), dim3(64), 0, st, p);
   return (int)hipGetLastError();
 }
@@ -983,7 +984,11 @@ static void enqueue_trav(const WfParams& p, hipStream_t st, int which) {
 template <bool kCount>
 static int enqueue_bounce(const WfParams& p, hipStream_t st) {
   const dim3 b(kWfBlock);
-  const dim3 gd((kWfShards * p.shard_cap + kWfBlock - 1) / kWfBlock);  // dense kernels: one thread per slot
+  // dense kernels: one thread per live path, at most one per slot; while the
+  // last paths drain, the host's bound keeps tens of thousands of empty
+  // workgroups out of each launch
+  const long long live = std::min<long long>((long long)kWfShards * p.shard_cap, std::max(p.live_bound, 1));
+  const dim3 gd((unsigned)((live + kWfBlock - 1) / kWfBlock));
   const bool full = p.lds_nodes >= p.bvh_nodes;
   auto trav = [&](int which) {
     if (full)
