@@ -522,7 +522,9 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
 // chunks of whole pixels (all their samples) so the per-sample radiance
 // buffer stays below kWfMaxChunkSamples entries (24 B each).
 constexpr int kWfRing = 4;
-constexpr uint64_t kWfMaxChunkSamples = 1ull << 28;  // 6 GB of radiance (HBM: 288 GB)
+// (each chunk ends in its own drain of long paths: C5 on one GPU, 2.1 G
+// samples, took 7.72 s per frame in chunks of 2^28 samples)
+constexpr uint64_t kWfMaxChunkSamples = 1ull << 30;  // 24 GB of radiance (HBM: 288 GB)
 
 static bool use_wavefront(const rt_context* c) { return !c->flat.bvh.empty() && c->tun.path != RT_PATH_MEGAKERNEL; }
 

@@ -257,7 +257,7 @@ typedef struct {
   int32_t bvh_bins;       /* SAH bins per axis; 0: 32 */
   int32_t bvh_leaf;       /* spheres per BVH leaf at most (1..7); 0: 4 */
   int32_t wf_paths;       /* wavefront path slots (at most 2^24); 0: 2^24, fewer when the frame has fewer samples */
-  int64_t wf_chunk;       /* wavefront samples per chunk; 0: 2^28 */
+  int64_t wf_chunk;       /* wavefront samples per chunk; 0: 2^30 */
   int32_t wf_lds_nodes;   /* BVH nodes staged into LDS; -1: as many as fit */
   int32_t wf_trav_block;  /* threads per traversal workgroup (64..1024); 0: 1024 */
   int32_t wf_trav_wgs;    /* traversal workgroups sharing a CU's LDS; 0: 1 */
