@@ -53,7 +53,7 @@ def main():
         "algorithmic_bytes_per_launch": 800 * 600 * 16 + 4096,
         "note": "median over the profiled launches; FETCH_SIZE x2 per MI355X_MICROARCH.md; WRITE_SIZE is exact for "
                 "this kernel's 12 + 4 B/lane store pattern (calibrated on unpack_kernel, "
-                "profiles/r02_pmc_calibration.json); the bytes beyond the framebuffer are scratch-spill traffic",
+                "profiles/r02_pmc_calibration.json); the kernel has no scratch (r02); the bytes written beyond the framebuffer are the split pixels' per-sample radiance rows",
     }
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
