@@ -668,6 +668,7 @@ template <bool kCount>
 __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
   __shared__ int s_wave[kWfBlock / 64];
   __shared__ int s_base;
+  __shared__ uint32_t s_slot[kWfBlock], s_own[kWfBlock];
   const Dense dn = dense(p.ctl->cur_cnt);
   const int n = dn.start[kWfShards];
   if ((int)(blockIdx.x * kWfBlock) >= n) return;
@@ -684,9 +685,8 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
     if (hit) P = mk(p.px[slot], p.py[slot], p.pz[slot]);
   }
   const int shard = blockIdx.x % kWfShards;
-  rt_rng rng{hit ? p.cur.rng[slot] : 0ull};
-  // lights in chunks of 32 (one bit each; any number of lights), in light order
-  for (int base = 0; base < p.nl; base += 32) {
+  // lights base + i of `own` whose hard ray is clear (i < 32)
+  auto clear_lights = [&](int base) {
     uint32_t own = 0;
     if (hit) {
       const int end = min(p.nl, base + 32);
@@ -697,22 +697,54 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
         if (!(ldist < 0.001) && !(p.lstate[slot * p.nl + li] & kHardBit)) own |= 1u << (li - base);
       }
     }
-    const int q = block_append(16 * __popc(own), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
-    if (own) {
-      uint4* sq = reinterpret_cast<uint4*>(p.softq) + (size_t)shard * p.soft_cap + q;
-      int k = 0;  // entries written (an index, not a bumped pointer)
-      for (uint32_t m = own; m; m &= m - 1) {
-        const uint32_t key = (uint32_t)(slot * p.nl) + (uint32_t)(base + __builtin_ctz(m));
-        cnt<kCount>(c, C_SHADOW, 16);
-        for (const int end = k + 16; k < end;) {
-          const uint32_t ux = rt_rng_next(&rng), uy = rt_rng_next(&rng), uz = rt_rng_next(&rng);
-          cnt<kCount>(c, C_RNG, 3);
-          const bool acc = unit_ball_accept(ux, uy, uz);
-          if (acc) sq[k] = make_uint4(key, ux, uy, uz);
-          k += acc ? 1 : 0;
-        }
+    return own;
+  };
+  // the 16 points of each light of `own`, in light order, at entries q.. of the shard's queue
+  auto gen = [&](size_t sl, uint32_t own, int base, int q, rt_rng& rng) {
+    uint4* sq = reinterpret_cast<uint4*>(p.softq) + (size_t)shard * p.soft_cap + q;
+    int k = 0;  // entries written (an index, not a bumped pointer)
+    for (uint32_t m = own; m; m &= m - 1) {
+      const uint32_t key = (uint32_t)(sl * p.nl) + (uint32_t)(base + __builtin_ctz(m));
+      cnt<kCount>(c, C_SHADOW, 16);
+      for (const int end = k + 16; k < end;) {
+        const uint32_t ux = rt_rng_next(&rng), uy = rt_rng_next(&rng), uz = rt_rng_next(&rng);
+        cnt<kCount>(c, C_RNG, 3);
+        const bool acc = unit_ball_accept(ux, uy, uz);
+        if (acc) sq[k] = make_uint4(key, ux, uy, uz);
+        k += acc ? 1 : 0;
       }
     }
+  };
+  if (p.nl <= 32) {
+    // Most paths have no clear light (C4: 12 % of hard rays are clear): the
+    // paths that have one are gathered to the workgroup's first lanes, so
+    // the rejection sampling runs on full waves and the other waves of the
+    // workgroup skip it (one path per lane either way: same draws, same order)
+    const uint32_t own = clear_lights(0);
+    int total;
+    const int at = block_prefix(own != 0 ? 1 : 0, s_wave, total);
+    if (own) {
+      s_slot[at] = (uint32_t)slot;
+      s_own[at] = own;
+    }
+    __syncthreads();
+    const bool work = (int)threadIdx.x < total;
+    const uint32_t ws = work ? s_slot[threadIdx.x] : 0u, wo = work ? s_own[threadIdx.x] : 0u;
+    const int q = block_append(16 * __popc(wo), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
+    if (work) {
+      rt_rng rng{p.cur.rng[ws]};
+      gen(ws, wo, 0, q, rng);
+      p.cur.rng[ws] = rng.x;
+    }
+    flush_counts<kCount>(p, c);
+    return;
+  }
+  rt_rng rng{hit ? p.cur.rng[slot] : 0ull};
+  // more than 32 lights: in chunks of 32 (one bit each), in light order
+  for (int base = 0; base < p.nl; base += 32) {
+    const uint32_t own = clear_lights(base);
+    const int q = block_append(16 * __popc(own), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
+    if (own) gen(slot, own, base, q, rng);
   }
   if (hit) p.cur.rng[slot] = rng.x;
   flush_counts<kCount>(p, c);
