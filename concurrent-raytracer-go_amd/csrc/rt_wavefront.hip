@@ -72,6 +72,7 @@ constexpr int kLdsBytes = 160 * 1024;    // LDS per CU (MI355X), all of it avail
 constexpr int kRefill = RT_WF_REFILL;    // persistent traversal: refill once this many lanes are idle
 constexpr int kChunk = RT_WF_CHUNK;      // persistent traversal: jobs a wave takes per atomic
 constexpr uint32_t kHardBit = 1u << 16;
+constexpr uint32_t kUnlitBit = 1u << 17;  // lstate: the hit point is within 0.001 of the light (no shadow rays)
 // hidx of a path whose ray hit nothing while a sky is opted in: wf_shade1
 // ends it with the sky's radiance (GetSkyColor, atmosphere.go:100-135) --
 // kept out of the traversal kernel, whose registers it would cost
@@ -540,8 +541,9 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade1(const WfParams p) {
         d3 ldir;
         double ldist;
         light_vec(p.lights[li], P, ldir, ldist);
-        uint32_t st = 0;
+        uint32_t st = kUnlitBit;
         if (!(ldist < 0.001)) {
+          st = 0;
           cnt<kCount>(c, C_LIGHT);
           cnt<kCount>(c, C_SHADOW);
           cnt<kCount>(c, C_SPH);
@@ -678,24 +680,19 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
   const int j = blockIdx.x * kWfBlock + threadIdx.x;
   size_t slot = 0;
   bool hit = false;
-  d3 P = mk(0, 0, 0);
   if (j < n) {
     slot = dense_at(dn, j, p.shard_cap);
     hit = p.hidx[slot] >= 0;
-    if (hit) P = mk(p.px[slot], p.py[slot], p.pz[slot]);
   }
   const int shard = blockIdx.x % kWfShards;
-  // lights base + i of `own` whose hard ray is clear (i < 32)
+  // lights base + i of `own` that are lit (wf_shade1: not within 0.001 of the
+  // hit point) and whose hard ray is clear (i < 32)
   auto clear_lights = [&](int base) {
     uint32_t own = 0;
     if (hit) {
       const int end = min(p.nl, base + 32);
-      for (int li = base; li < end; ++li) {
-        d3 ldir;
-        double ldist;
-        light_vec(p.lights[li], P, ldir, ldist);
-        if (!(ldist < 0.001) && !(p.lstate[slot * p.nl + li] & kHardBit)) own |= 1u << (li - base);
-      }
+      for (int li = base; li < end; ++li)
+        if (!(p.lstate[slot * p.nl + li] & (kHardBit | kUnlitBit))) own |= 1u << (li - base);
     }
     return own;
   };
