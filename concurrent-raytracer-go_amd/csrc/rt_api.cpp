@@ -559,7 +559,7 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   const size_t qcap = cap * nlk;  // hard rays per shard: at most every light of every path of its workgroups
   // one allocation: two path arrays | hit records | per-light state | queues
   const size_t need = 2 * cap * (12 * 8 + 8 + 4 + 4)   // path arrays
-                      + cap * (7 * 8 + 4 + 4)           // hit numerator, point, normal, info, index
+                      + cap * (4 * 8 + 4)               // hit numerator, point, index
                       + cap * nlk * 4                   // lstate
                       + (size_t)kWfShards * qcap * 4    // hard queues
                       + (size_t)kWfShards * qcap * 16 * 16  // soft queues
@@ -650,9 +650,8 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
       a->depth = (int32_t*)take(cap * sizeof(int32_t));
     }
     p.hnum = (double*)take(cap * sizeof(double));
-    double** hh[6] = {&p.px, &p.py, &p.pz, &p.nx, &p.ny, &p.nz};
+    double** hh[3] = {&p.px, &p.py, &p.pz};
     for (double** q : hh) *q = (double*)take(cap * sizeof(double));
-    p.hinfo = (int32_t*)take(cap * sizeof(int32_t));
     p.hidx = (int32_t*)take(cap * sizeof(int32_t));
     p.lstate = (uint32_t*)take(cap * nlk * sizeof(uint32_t));
     p.hardq = (uint32_t*)take((size_t)kWfShards * qcap * sizeof(uint32_t));

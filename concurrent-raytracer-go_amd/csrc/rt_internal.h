@@ -215,8 +215,7 @@ struct WfParams {
   WfCtl* ctl;
   int32_t* hidx;             // per slot of the current array: sphere hit (-1: none)
   double* hnum;              // ... its root numerator
-  double *px, *py, *pz, *nx, *ny, *nz;  // hit point and normal
-  int32_t* hinfo;            // material << 1 | front face
+  double *px, *py, *pz;      // hit point
   uint32_t* lstate;          // [slot][light]: kHardBit | blocked soft rays
   uint32_t* hardq;           // kWfShards queues of hard_cap entries: slot * nl + light
   uint32_t* softq;           // kWfShards queues of soft_cap entries, 4 words: {slot * nl + light, draws x, y, z}

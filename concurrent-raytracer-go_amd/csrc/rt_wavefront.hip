@@ -509,19 +509,14 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade1(const WfParams p) {
       cnt<kCount>(c, C_SHADE);
       const WfPaths& a = p.cur;
       const d3 o = ld_o(a, slot), d = ld_d(a, slot);
-      const DSphere& S0 = p.g.spheres[hi];
       const double t = p.hnum[slot] / len2(d);
       P = o + muls(d, t);
-      const d3 outward = divs(P - ld3(S0.c), S0.r);
-      const bool front = dot(d, outward) < 0;
-      const d3 N = front ? outward : neg(outward);
+      // (the normal and the face are recomputed from P where they are used,
+      // wf_shade: the same operations give the same bits, and 28 B per path
+      // less cross HBM twice)
       p.px[slot] = P.x;
       p.py[slot] = P.y;
       p.pz[slot] = P.z;
-      p.nx[slot] = N.x;
-      p.ny[slot] = N.y;
-      p.nz[slot] = N.z;
-      p.hinfo[slot] = (S0.mat << 1) | (front ? 1 : 0);
     }
   }
   const int shard = blockIdx.x % kWfShards;
@@ -773,11 +768,13 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(const WfParams p) {
     if (p.hidx[slot] >= 0) {
       const WfPaths& a = p.cur;
       P = mk(p.px[slot], p.py[slot], p.pz[slot]);
-      const d3 N = mk(p.nx[slot], p.ny[slot], p.nz[slot]);
-      const int info = p.hinfo[slot];
-      const bool front = info & 1;
-      const DMat* __restrict__ m = p.mats + (info >> 1);
       const d3 d = ld_d(a, slot);
+      // HitRecord (sphere.go:42-58): the outward normal at P, flipped to face the ray
+      const DSphere& S0 = p.g.spheres[p.hidx[slot]];
+      const d3 outward = divs(P - ld3(S0.c), S0.r);
+      const bool front = dot(d, outward) < 0;
+      const d3 N = front ? outward : neg(outward);
+      const DMat* __restrict__ m = p.mats + S0.mat;
       T = mk(a.tx[slot], a.ty[slot], a.tz[slot]);
       L = mk(a.lx[slot], a.ly[slot], a.lz[slot]);
       rng.x = a.rng[slot];
