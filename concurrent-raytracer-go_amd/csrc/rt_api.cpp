@@ -556,7 +556,10 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   const int shard_cap = wf_shard_cap(nl, c->tun, chunk_px * spp);
   const size_t cap = (size_t)shard_cap * kWfShards;
   const size_t nlk = (size_t)std::max(nl, 1);
-  const size_t qcap = cap * nlk;  // hard rays per shard: at most every light of every path of its workgroups
+  // hard rays per shard: at most every light of every path of the workgroups
+  // b % kWfShards == shard of wf_shade1 / wf_softgen, which cover at most
+  // shard_cap paths (their grid has at most cap / kWfBlockSlots workgroups)
+  const size_t qcap = (size_t)shard_cap * nlk;
   // one allocation: two path arrays | hit records | per-light state | queues
   const size_t need = 2 * cap * (12 * 8 + 8 + 4 + 4)   // path arrays
                       + cap * (4 * 8 + 4)               // hit numerator, point, index
