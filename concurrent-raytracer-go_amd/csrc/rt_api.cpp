@@ -562,7 +562,7 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   const size_t qcap = (size_t)shard_cap * nlk;
   // one allocation: two path arrays | hit records | per-light state | queues
   const size_t need = 2 * cap * (12 * 8 + 8 + 4 + 4)   // path arrays
-                      + cap * (4 * 8 + 4)               // hit numerator, point, index
+                      + cap * (3 * 8 + 4)               // hit point, index
                       + cap * nlk * 4                   // lstate
                       + (size_t)kWfShards * qcap * 4    // hard queues
                       + (size_t)kWfShards * qcap * 16 * 16  // soft queues
@@ -652,7 +652,6 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
       a->sid = (uint32_t*)take(cap * sizeof(uint32_t));
       a->depth = (int32_t*)take(cap * sizeof(int32_t));
     }
-    p.hnum = (double*)take(cap * sizeof(double));
     double** hh[3] = {&p.px, &p.py, &p.pz};
     for (double** q : hh) *q = (double*)take(cap * sizeof(double));
     p.hidx = (int32_t*)take(cap * sizeof(int32_t));

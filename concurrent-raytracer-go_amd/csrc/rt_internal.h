@@ -214,7 +214,6 @@ struct WfParams {
   WfPaths cur, next;
   WfCtl* ctl;
   int32_t* hidx;             // per slot of the current array: sphere hit (-1: none)
-  double* hnum;              // ... its root numerator
   double *px, *py, *pz;      // hit point
   uint32_t* lstate;          // [slot][light]: kHardBit | blocked soft rays
   uint32_t* hardq;           // kWfShards queues of hard_cap entries: slot * nl + light

@@ -395,7 +395,7 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
   bool busy = false;
   size_t slot = 0;
   d3 o = mk(0, 0, 0), d = mk(0, 0, 0);
-  double av = 0, inv_a = 0, closest = 0, bnum = 0;
+  double av = 0, inv_a = 0, closest = 0;
   RayQ r32{};
   float tminf = 0;
   int cur = -1, sp = 0, best_obj = -1, bidx = -1;
@@ -455,7 +455,6 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
             const double t = num / av;
             if (t == closest && best_obj > S.obj) continue;
             closest = t;
-            bnum = num;
             bidx = i;
             best_obj = S.obj;
           }
@@ -465,8 +464,13 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
       if (cur == -1) {  // traversal done
         busy = false;
         if (best_obj >= 0) {
+          // the hit point (HitRecord.P, sphere.go:44: t = the root / a, as
+          // kept in `closest`), for shade1, the occlusion kernels and shade
+          const d3 P = o + muls(d, closest);
           p.hidx[slot] = bidx;
-          p.hnum[slot] = bnum;
+          p.px[slot] = P.x;
+          p.py[slot] = P.y;
+          p.pz[slot] = P.z;
         } else if (p.sky) {  // a miss with an opted-in sky: shade1 adds it
           p.hidx[slot] = kSkyMiss;
         } else {
@@ -507,16 +511,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade1(const WfParams p) {
     }
     if (hit) {
       cnt<kCount>(c, C_SHADE);
-      const WfPaths& a = p.cur;
-      const d3 o = ld_o(a, slot), d = ld_d(a, slot);
-      const double t = p.hnum[slot] / len2(d);
-      P = o + muls(d, t);
-      // (the normal and the face are recomputed from P where they are used,
-      // wf_shade: the same operations give the same bits, and 28 B per path
-      // less cross HBM twice)
-      p.px[slot] = P.x;
-      p.py[slot] = P.y;
-      p.pz[slot] = P.z;
+      // (wf_extend stored the hit point; the normal and the face are
+      // recomputed from it where they are used, wf_shade: the same
+      // operations give the same bits, with fewer bytes through HBM)
+      P = mk(p.px[slot], p.py[slot], p.pz[slot]);
     }
   }
   const int shard = blockIdx.x % kWfShards;
