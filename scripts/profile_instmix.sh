@@ -30,7 +30,7 @@ for scene in headline c4; do
       python3 scripts/pmc_instmix.py "$k" gpurun_out/profiles_${R}/${R}_instmix_c4_${tag}.json "${dirs[@]}"
     done
   else
-    python3 scripts/pmc_instmix.py "render_kernel<false, true, false>" gpurun_out/profiles_${R}/${R}_instmix_headline.json "${dirs[@]}"
+    python3 scripts/pmc_instmix.py "render_kernel<false, true, false, false>" gpurun_out/profiles_${R}/${R}_instmix_headline.json "${dirs[@]}"
   fi
 done
 echo "instmix ${R} done"
