@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rt_internal.h"
@@ -297,11 +298,11 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
     const size_t share = rt_packed_bytes(w, h, n), rgba_off = rt_packed_rgba_offset(w, h, n);
     rc = r->gathered.grow(root, share * (size_t)n);
     if (rc) return rc;
+    std::vector<uint8_t*> bufs(n);
     for (int k = 0; k < n; ++k) {
       Rank& q = r->ranks[k];
-      uint8_t* buf;
       if (q.comm_idx == 0) {  // the root's device: straight into the gather buffer
-        buf = (uint8_t*)r->gathered.p + (size_t)k * share;
+        bufs[k] = (uint8_t*)r->gathered.p + (size_t)k * share;
       } else {
         if (share > q.share_cap) {
           HIP_TRY(hipSetDevice(q.device));
@@ -311,12 +312,30 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
           HIP_TRY(hipMalloc(&q.share, share));
           q.share_cap = share;
         }
-        buf = (uint8_t*)q.share;
+        bufs[k] = (uint8_t*)q.share;
       }
-      rc = rt_context_render_async(q.ctx, w, h, st, k, n, RT_LAYOUT_PACKED_TILES, (float*)buf, buf + rgba_off,
-                                   q.stream, nullptr);
-      if (rc) return rc;
     }
+    // One host thread per rank: a BVH scene's wavefront loop is driven from
+    // the host bounce by bounce (rt_context_render_async returns when its
+    // frame is done), so the ranks must not wait for each other.  The
+    // megakernel's launches return at once either way.
+    std::vector<int> rcs(n, RT_OK);
+    std::vector<std::string> errs(n);
+    auto render_rank = [&](int k) {
+      Rank& q = r->ranks[k];
+      rcs[k] = rt_context_render_async(q.ctx, w, h, st, k, n, RT_LAYOUT_PACKED_TILES, (float*)bufs[k],
+                                       bufs[k] + rgba_off, q.stream, nullptr);
+      if (rcs[k]) errs[k] = rt_last_error();  // (the error text is per thread)
+    };
+    std::vector<std::thread> pool;
+    for (int k = 1; k < n; ++k) pool.emplace_back(render_rank, k);
+    render_rank(0);
+    for (std::thread& t : pool) t.join();
+    for (int k = 0; k < n; ++k)
+      if (rcs[k]) {
+        set_error(errs[k]);
+        return rcs[k];
+      }
     if (r->devices.size() > 1) {
       rc = group_gather(r, share);
       if (rc) return rc;

@@ -41,6 +41,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 
 #include "../../include/rt_rng.h"
 #include "rt_device.h"
@@ -991,18 +992,33 @@ template <bool kCount, bool kFull>
 static void enqueue_trav(const WfParams& p, hipStream_t st, int which) {
   const dim3 bt(p.trav_block);
   const size_t sh = trav_shmem(p);
-  static int g_ext = 0, g_occ_h = 0, g_occ_s = 0, g_block = 0;
-  static size_t g_sh = 0;
-  if (g_sh != sh || g_block != p.trav_block || !g_ext) {
-    g_ext = resident_grid(wf_extend<kCount, kFull>, p.trav_block, sh);
-    g_occ_h = resident_grid(wf_occlude<kCount, false, kFull>, p.trav_block, sh);
-    g_occ_s = resident_grid(wf_occlude<kCount, true, kFull>, p.trav_block, sh);
-    g_sh = sh;
-    g_block = p.trav_block;
+  // resident grids (and the LDS attribute) per device: an rt_renderer drives
+  // its devices from one thread each (rt_multi.cpp)
+  struct Grids {
+    int ext = 0, occ_h = 0, occ_s = 0, block = 0;
+    size_t sh = 0;
+  };
+  constexpr int kDevs = 64;
+  static std::mutex mu;
+  static Grids cache[kDevs];
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  Grids g;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    Grids& c = cache[dev % kDevs];
+    if (c.sh != sh || c.block != p.trav_block || !c.ext) {
+      c.ext = resident_grid(wf_extend<kCount, kFull>, p.trav_block, sh);
+      c.occ_h = resident_grid(wf_occlude<kCount, false, kFull>, p.trav_block, sh);
+      c.occ_s = resident_grid(wf_occlude<kCount, true, kFull>, p.trav_block, sh);
+      c.sh = sh;
+      c.block = p.trav_block;
+    }
+    g = c;
   }
-  if (which == 0) hipLaunchKernelGGL((wf_extend<kCount, kFull>), dim3(g_ext), bt, sh, st, p);
-  if (which == 1) hipLaunchKernelGGL((wf_occlude<kCount, false, kFull>), dim3(g_occ_h), bt, sh, st, p);
-  if (which == 2) hipLaunchKernelGGL((wf_occlude<kCount, true, kFull>), dim3(g_occ_s), bt, sh, st, p);
+  if (which == 0) hipLaunchKernelGGL((wf_extend<kCount, kFull>), dim3(g.ext), bt, sh, st, p);
+  if (which == 1) hipLaunchKernelGGL((wf_occlude<kCount, false, kFull>), dim3(g.occ_h), bt, sh, st, p);
+  if (which == 2) hipLaunchKernelGGL((wf_occlude<kCount, true, kFull>), dim3(g.occ_s), bt, sh, st, p);
 }
 
 template <bool kCount>

@@ -90,6 +90,25 @@ def test_renderer_multi_rank_equals_one_rank(devices):
     r.close()
 
 
+def test_renderer_ranks_drive_bvh_frames_concurrently():
+    """A BVH scene runs the wavefront path, whose host loop returns only when
+    the frame is done; rt_renderer_render drives each rank from its own
+    thread.  3 ranks on device 0 (their loops interleaved on one GPU) give
+    the 1-rank image, twice in a row."""
+    scene = spheres10k_scene(rtgo)
+    w, h = 96, 64
+    r = rtgo.ParallelRenderer(devices=[0, 0, 0])
+    for seed in (4, 5):
+        st = make_settings(rtgo, {"samples": 2, "max_depth": 6}, seed=seed)
+        ref_lin, ref_rgba = _gpu(scene, w, h, st)
+        st.num_devices = 3
+        r.settings = st
+        rgba = r.render(scene, w, h)
+        assert r.last_linear.tobytes() == ref_lin.tobytes()
+        assert rgba.tobytes() == ref_rgba.tobytes()
+    r.close()
+
+
 def test_comm_of_one_rank_and_one_shot_render():
     """rt_comm over one rank (ncclCommInitRank, world 1: the gather moves
     nothing) and the one-shot rt_render with num_devices = 1."""
