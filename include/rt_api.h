@@ -219,8 +219,10 @@ int rt_validate(const rt_scene* scene, int32_t width, int32_t height, const rt_s
  * bit-identical for every device count (the random stream is keyed by
  * global pixel and sample).  The renderer keeps each device's scene, work
  * schedule and buffers between calls: a call with the same scene content,
- * size and settings (any seed) re-uploads nothing.  Not thread-safe (nor is
- * the Go renderer: renderer.go:103-112). */
+ * size and settings (any seed) re-uploads nothing.  A call drives every rank
+ * from its own host thread (joined before it returns).  Not thread-safe
+ * itself: one call at a time per renderer (nor is the Go renderer:
+ * renderer.go:103-112). */
 typedef struct rt_renderer rt_renderer;
 int rt_renderer_create(const int32_t* devices, int32_t num_devices, rt_renderer** out);
 /* Render with the renderer's devices (settings->num_devices is ignored). */
