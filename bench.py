@@ -15,33 +15,43 @@ workload: --config c2 (default, the headline): BASELINE configs[1],
           1920x1080x64), c5 (10k spheres 3840x2160x256: the 8-GPU config).
 step    : one render of a whole frame with the scene and output buffers
           resident in HBM; every step renders a DIFFERENT image (seed + i).
-          Frames are rendered with F frames in flight (--frames-in-flight,
-          default 2 for c2/c3): step i runs on context/stream i % F with its
-          own buffers, so a frame's low-occupancy tail (its last 50-bounce
-          paths) overlaps the next frame's start.  The same
-          frames are also timed one at a time (the reference's synchronous
-          Render): "one_frame_in_flight".  For N>1 a step also includes the
-          one RCCL gather of the ranks' packed shares to rank 0
-          (rt_comm_gather_tiles_async: librtgo's own ncclSend/ncclRecv over
-          xGMI) and the unpack kernel there.  The work schedule of a (scene,
-          frame, settings) key is built by the first frame and reused
-          (seeds excluded from the key).
+          Frames are rendered with F frames in flight (--frames-in-flight;
+          default 2 for c2/c3 at one GPU, 8 per rank at N > 1): step i runs
+          on frame slot i % F (own context, stream and buffers), so a frame's
+          low-occupancy tail (its last 50-bounce paths)
+          overlaps the next frames.  The same frames are also timed one at a
+          time (the reference's synchronous Render): "one_frame_in_flight".
+          For N > 1 a step also includes the frame's one RCCL gather of the
+          ranks' packed shares to rank 0 (librtgo's ncclSend/ncclRecv group
+          over xGMI, on one gather stream per rank, in step order) and the
+          unpack kernel there.  The work schedule of a (scene, frame,
+          settings) key is built by the first frame and reused (seeds
+          excluded from the key).
+scaling : STRONG by default: every N renders the config's frame (800x600x100
+          for c2, BASELINE configs[1]), its 32x32 tiles partitioned over the
+          ranks.  Linear-scan scenes use a work-balanced partition
+          (rt_partition_balanced: a whole-frame pilot, tiles dealt heaviest
+          first to the least loaded rank; every rank plans the same one, which
+          is checked); BVH scenes (c4, c5: thousands of busy tiles) the
+          strided deal t % N.  --weak renders 800 x (600 N)
+          instead (per-GPU work fixed).  value = the frame's samples x steps /
+          max-over-ranks time.
 end to end: "render_e2e" (N=1): the blocking Render of the C ABI
           (rt_renderer_render: scene check + upload, schedule, kernels,
           device->host copy of the image), median of 7 calls with distinct
           seeds on one renderer object (NewParallelRenderer once, Render per
           frame, as cmd/raytracer uses it); "oneshot" = rt_render, which also
           creates and destroys the device contexts every call.
-scaling : c2 weak by default: at N GPUs the frame is 800 x (600*N) (per-GPU
-          work fixed at one 800x600x100 frame of samples); --strong keeps
-          800x600.  c4 / c5: strong (the frame is fixed).  Tiles are dealt
-          t -> t % N.  value = all ranks' samples /
-          max-over-ranks time.
+cpu     : the oracle (oracle/oracle.c: the reference's goroutine tile loop
+          restated in C) on runtime.NumCPU() threads = the affinity count of
+          this process (cmd/raytracer/main.go:46, BASELINE configs[0]
+          "workers=host cores"), rank 0 at N=1 only.
 
-usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2_committed|c3|c4|c5]
+usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2_committed|c3|c4|c5] [--weak]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 import argparse
+import hashlib
 import json
 import os
 import statistics
@@ -54,26 +64,32 @@ for p in (ROOT, PKG, os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-# FP64 operations per counted event: the adds, muls,
-# divides and square roots of the reference's formulas, 1 each, for the
-# work the kernel EXECUTES (primitives culled as provably missed are neither
-# executed nor counted).
+# Operations per counted event: the adds, muls, divides
+# and square roots of the reference's formulas, 1 each, for the work the
+# kernel EXECUTES (rt_counts minus rt_counts.culled: primitives and camera
+# samples culled as provably missed are neither executed nor counted).
 FLOPS_PER_EVENT = {
     "camera_rays": 12,     # u, v (2 add + 2 div) + getRay (8)
     "sphere_tests": 20,    # Sphere.Hit up to the discriminant test (+ avg root work)
     "triangle_tests": 46,  # Moller-Trumbore to the t test
-    "box_tests": 12,       # slab test: 6 sub + 6 mul
     "shade_events": 75,    # hit record + scatter + path update
     "light_evals": 60,     # direct-lighting terms per light
     "shadow_rays": 15,     # soft direction: scale, add, normalize
     "rng_draws": 5,        # unit conversion + rejection arithmetic
 }
+# BVH node slab tests run in binary32 on quantized bounds:
+# priced against the FP32 peak, in a term of their own
+FLOPS_PER_BOX = 12          # 6 fma + 6 min/max/compare
+# a ray the soft-shadow traversal kernel sets up: light vector (12), the
+# jittered direction (15), inverse direction (3), the binary64 root box (12)
+SOFT_RAY_SETUP_FLOPS = 42
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) peak: 256 CU x 2.4 GHz x 128 FLOP/clk
+PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")
 
 CONFIGS = {
-    # name: (scene, W, H, spp, label, default steps, default frames in flight)
+    # name: (scene, W, H, spp, label, default steps, default frames in flight at one GPU)
     "c2": ("sphere_reflections_light_facing.json", 800, 600, 100, "sphere_reflections_light_facing", 100, 2),
     "c2_committed": ("sphere_reflections_light.json", 800, 600, 100,
                      "sphere_reflections_light as committed (black: objects behind the -Z camera)", 100, 2),
@@ -82,12 +98,13 @@ CONFIGS = {
     "c4": ("gen:10000", 1920, 1080, 64, "procedural 10k spheres (scenes/gen_spheres.py, BVH)", 3, 1),
     "c5": ("gen:10000", 3840, 2160, 256, "procedural 10k spheres (scenes/gen_spheres.py, BVH)", 1, 1),
 }
+WAVEFRONT = ("c4", "c5")
 KERNELS = {  # the dominant kernel of each config (rocprofv3 --stats, profiles/)
     "c2": "rtgo::render_kernel<false, true, false, false>",
     "c2_committed": "rtgo::render_kernel<false, true, false, false>",
     "c3": "rtgo::render_kernel<false, true, false, false>",
-    "c4": "wavefront bounce loop (wf_occlude<false, true, true> dominant)",
-    "c5": "wavefront bounce loop (wf_occlude<false, true, true> dominant)",
+    "c4": "rtgo::wf_occlude<false, true, true>",
+    "c5": "rtgo::wf_occlude<false, true, true>",
 }
 
 
@@ -100,12 +117,13 @@ def parse():
     ap.add_argument("--spp", type=int, default=0, help="override the config's spp")
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--strong", action="store_true", help="c2: fixed 800x600 frame for every N (strong scaling)")
+    ap.add_argument("--weak", action="store_true", help="c2/c3: frame W x (H*N) (per-GPU work fixed)")
+    ap.add_argument("--strided", action="store_true", help="N > 1: deal tiles t %% N instead of by estimated work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (default: the affinity count)")
     ap.add_argument("--frames-in-flight", type=int, default=0,
-                    help="frames rendered concurrently (own context, stream and buffers each)")
+                    help="frames rendered concurrently per rank (own context, stream and buffers each)")
     return ap.parse_args()
 
 
@@ -117,16 +135,19 @@ def load_scene(rtgo, spec):
     return rtgo.Scene.load_from_file(os.path.join(ROOT, "scenes", spec))
 
 
-class Frame:
-    """Device buffers and one render step of this rank.
+class Slot:
+    """One frame slot of this rank: its context (schedule), render stream and
+    buffers.  world 1: the W*H image.  world > 1: this rank's packed share of
+    the partition; rank 0 renders its share in place into its gather buffer
+    and unpacks the image there."""
 
-    world 1: the W*H image.  world > 1: this rank's packed share
-    (rt_packed_bytes: float3 + RGBA8 per pixel of its tiles); rank 0 renders
-    its share in place into the gather buffer and unpacks the image there."""
-
-    def __init__(self, rtgo, torch, ctx, w, h, rank, world, device, stream, comm):
-        self.rtgo, self.ctx, self.w, self.h = rtgo, ctx, w, h
-        self.rank, self.world, self.stream, self.comm = rank, world, stream, comm
+    def __init__(self, rtgo, torch, scene, w, h, rank, world, device, part):
+        self.rtgo, self.w, self.h, self.rank, self.world, self.part = rtgo, w, h, rank, world, part
+        self.ctx = rtgo.Context(device)
+        self.ctx.set_scene(scene)
+        self.stream = torch.cuda.Stream(device)
+        self.rendered = torch.cuda.Event()
+        self.gathered = None  # event: the share has been sent (and unpacked on rank 0)
         dev = torch.device("cuda", device)
         if world == 1:
             self.layout = rtgo.RT_LAYOUT_IMAGE
@@ -134,37 +155,48 @@ class Frame:
             self.rgba = torch.zeros(w * h * 4, dtype=torch.uint8, device=dev)
             self.p_lin, self.p_rgba = self.lin.data_ptr(), self.rgba.data_ptr()
             return
+        self.ctx.set_partition(part)
         self.layout = rtgo.RT_LAYOUT_PACKED_TILES
-        nb = rtgo.packed_bytes(w, h, world)
+        nb = part.packed_bytes
+        self.share_bytes = nb
         if rank == 0:
-            self.gathered = torch.zeros(world * nb, dtype=torch.uint8, device=dev)
-            self.share = self.gathered[:nb]
+            self.gbuf = torch.zeros(world * nb, dtype=torch.uint8, device=dev)
+            self.share = self.gbuf[:nb]
             self.img_lin = torch.zeros(w * h * 3, dtype=torch.float32, device=dev)
             self.img_rgba = torch.zeros(w * h * 4, dtype=torch.uint8, device=dev)
         else:
-            self.gathered = None
+            self.gbuf = None
             self.share = torch.zeros(nb, dtype=torch.uint8, device=dev)
         self.p_lin = self.share.data_ptr()
-        self.p_rgba = self.share.data_ptr() + rtgo.packed_rgba_offset(w, h, world)
+        self.p_rgba = self.share.data_ptr() + part.rgba_offset
 
     def render(self, st):
+        if self.gathered is not None:  # the share buffer is free again once its last gather is done
+            self.stream.wait_event(self.gathered)
         self.ctx.render_async(self.w, self.h, st, self.p_lin, self.p_rgba, self.stream.cuda_stream, self.rank,
                               self.world, self.layout)
 
-    def gather(self):
-        """The frame's one collective, then the unpack kernel on rank 0."""
+    def gather(self, torch, comm, gstream):
+        """The frame's one collective (on the rank's gather stream, in step
+        order), then the unpack kernel on rank 0."""
         if self.world == 1:
             return
-        s = self.stream.cuda_stream
-        g = self.gathered.data_ptr() if self.gathered is not None else 0
-        self.comm.gather_tiles_async(self.w, self.h, self.share.data_ptr(), g, s)
+        self.rendered.record(self.stream)
+        gstream.wait_event(self.rendered)
+        g = self.gbuf.data_ptr() if self.gbuf is not None else 0
+        comm.gather_bytes_async(self.share_bytes, self.share.data_ptr(), g, gstream.cuda_stream)
         if self.rank == 0:
-            self.rtgo.unpack_tiles_async(self.w, self.h, self.world, g, self.img_lin.data_ptr(),
-                                         self.img_rgba.data_ptr(), s)
+            self.part.unpack_async(g, self.img_lin.data_ptr(), self.img_rgba.data_ptr(), gstream.cuda_stream)
+        if self.gathered is None:
+            self.gathered = torch.cuda.Event()
+        self.gathered.record(gstream)
 
     def counts(self, st):
         return self.ctx.count(self.w, self.h, st, self.p_lin, self.p_rgba, self.stream.cuda_stream, self.rank,
-                              self.world, self.layout)
+                              self.world, self.layout, full=True)
+
+    def close(self):
+        self.ctx.close()
 
 
 def barrier_sync(torch, dist, world):
@@ -182,48 +214,47 @@ def max_over_ranks(torch, dist, world, x):
     return float(t.item())
 
 
-def time_steps(frames, torch, dist, world, sts, warmup):
+def time_steps(slots, torch, dist, world, sts, warmup, comm, gstream):
     """W untimed steps, then K = len(sts) timed steps (step i renders with
     settings sts[i]: its own seed) between barrier + synchronize on both
-    sides; step i runs frames[i % F] on its own stream.  Returns
-    (max-over-ranks seconds, per-launch kernel ms from HIP events recorded on
-    the stream each render runs on)."""
-    F = len(frames)
+    sides; step i runs slots[i % F].  Returns (max-over-ranks seconds,
+    per-launch kernel ms from HIP events recorded on the stream each render
+    runs on)."""
+    F = len(slots)
     for i in range(warmup):
-        fr = frames[i % F]
-        fr.render(sts[i % len(sts)])
-        fr.gather()
+        sl = slots[i % F]
+        sl.render(sts[i % len(sts)])
+        sl.gather(torch, comm, gstream)
     barrier_sync(torch, dist, world)
     evs = []
     t0 = time.perf_counter()
     for i, st in enumerate(sts):
-        fr = frames[i % F]
+        sl = slots[i % F]
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(fr.stream)
-        fr.render(st)
-        e1.record(fr.stream)
+        if sl.gathered is not None:
+            sl.stream.wait_event(sl.gathered)
+        e0.record(sl.stream)
+        sl.render(st)
+        e1.record(sl.stream)
         evs.append((e0, e1))
-        fr.gather()
+        sl.gather(torch, comm, gstream)
     barrier_sync(torch, dist, world)
     elapsed = max_over_ranks(torch, dist, world, time.perf_counter() - t0)
     return elapsed, [a.elapsed_time(b) for a, b in evs]
 
 
-def first_frame_ms(rtgo, torch, dist, scene, W, H, st, rank, world, local, comm):
-    """One frame on a fresh context: it also builds what the timed steps
-    reuse (frustum masks, the one-sample pilot render, block building and
-    upload).  Wall clock, max over ranks."""
-    ctx = rtgo.Context(local)
-    ctx.set_scene(scene)
-    frame = Frame(rtgo, torch, ctx, W, H, rank, world, local, torch.cuda.Stream(), comm)
-    barrier_sync(torch, dist, world)
-    t0 = time.perf_counter()
-    frame.render(st)
-    frame.gather()
+def first_frame_ms(rtgo, torch, scene, W, H, st, local):
+    """One frame on a fresh context (N = 1): it also builds what the timed
+    steps reuse (frustum masks, the one-sample pilot render, block building
+    and upload).  Wall clock."""
+    sl = Slot(rtgo, torch, scene, W, H, 0, 1, local, None)
     torch.cuda.synchronize()
-    ms = max_over_ranks(torch, dist, world, (time.perf_counter() - t0) * 1e3)
-    ctx.close()
+    t0 = time.perf_counter()
+    sl.render(st)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3
+    sl.close()
     return ms
 
 
@@ -269,36 +300,67 @@ def render_e2e(rtgo, scene, W, H, args, local):
     }
 
 
-def flops_of(counts):
-    return sum(FLOPS_PER_EVENT[k] * counts.get(k, 0) for k in FLOPS_PER_EVENT)
+def executed(counts):
+    """{event: executed count} = the reference's counts minus the culled part."""
+    return {k: v - counts.culled_dict()[k] for k, v in counts.as_dict().items()}
 
 
-def host_threads(args):
-    """CPU threads for the baseline: the box's share of host cores."""
+def fp_split(ex, soft=None):
+    """(binary64 ops, binary32 ops) of executed event counts ex.  soft: the
+    soft-shadow traversal kernel's own counts (its ray set-up instead of the
+    generic per-event costs)."""
+    if soft is not None:
+        jobs = soft["shadow_rays"]
+        f64 = jobs * SOFT_RAY_SETUP_FLOPS + soft["sphere_tests"] * FLOPS_PER_EVENT["sphere_tests"]
+        f32 = max(0, soft["box_tests"] - jobs) * FLOPS_PER_BOX  # (the root box per ray is binary64: in the set-up)
+        return f64, f32
+    f64 = sum(FLOPS_PER_EVENT[k] * ex.get(k, 0) for k in FLOPS_PER_EVENT)
+    return f64, ex.get("box_tests", 0) * FLOPS_PER_BOX
+
+
+def cpu_count_info():
+    """The CPUs this process may run on (Go's runtime.NumCPU() is the affinity
+    count) and the cgroup's CPU quota, if any (cpu.max: quota / period)."""
     try:
         aff = len(os.sched_getaffinity(0))
     except AttributeError:
         aff = os.cpu_count() or 1
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    threads = args.cpu_threads or (min(share, aff) if share > 0 else aff)
-    return threads, aff
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return aff, quota
+
+
+def cpu_time(oracle, scene, W, H, st, threads, runs=3):
+    oracle.render(scene, W, H, st, nthreads=threads, max_tiles=min(16, 2 * threads))  # warm-up
+    times = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        oracle.render(scene, W, H, st, nthreads=threads)
+        times.append(time.perf_counter() - t0)
+    return sorted(times)[len(times) // 2]
 
 
 def cpu_baseline(args, rtgo, scene, W, H, st, cfg):
     """The oracle (C restatement of the Go goroutine path, linear hitWorld
-    scan) on the host cores, on a bounded sample of the same workload."""
+    scan) on runtime.NumCPU() threads, on a bounded sample of the same workload."""
     import oracle
 
-    threads, aff = host_threads(args)
+    aff, quota = cpu_count_info()
+    threads = args.cpu_threads or aff
     n_tiles = rtgo.num_tiles(W, H)
-    if cfg in ("c4", "c5"):
-        # 10k-sphere linear scan: ~3 CPU-s per tile-sample-pass; time 2
-        # tiles per thread at 4 spp (every (n/(2T))-th tile, full depth),
-        # scaled per primary sample
+    if cfg in WAVEFRONT:
+        # 10k-sphere linear scan: ~1.4 CPU-s per tile-sample-pass; time 32
+        # tiles at 4 spp (a strided tile sample, full depth: ~180 CPU-s,
+        # ~11 s on a 16-CPU share), scaled per primary sample
         spp = 4
         stb = rtgo.default_settings()
         stb.samples, stb.max_depth, stb.seed = spp, st.max_depth, st.seed
-        ntl = 2 * threads
+        ntl = min(n_tiles, 32)
         world = max(1, n_tiles // ntl)
         t0 = time.perf_counter()
         oracle.render(scene, W, H, stb, rank=0, world=world, nthreads=threads, max_tiles=ntl)
@@ -307,24 +369,42 @@ def cpu_baseline(args, rtgo, scene, W, H, st, cfg):
         sample = (f"{ntl} tiles (every {world}th tile from tile 0) of the {W}x{H} frame at {spp} spp, depth "
                   f"{st.max_depth}, one run ({secs:.1f} s), scaled per primary sample")
     else:
-        oracle.render(scene, W, H, st, nthreads=threads, max_tiles=16)  # warm-up
-        times = []
-        for _ in range(3):
-            t0 = time.perf_counter()
-            oracle.render(scene, W, H, st, nthreads=threads)
-            times.append(time.perf_counter() - t0)
-        secs = sorted(times)[1]
+        secs = cpu_time(oracle, scene, W, H, st, threads)
         rays = W * H * st.samples
-        sample = f"full {W}x{H}x{st.samples}spp frame, median of 3 runs ({secs:.2f} s) after 1 warm-up"
+        sample = f"full {W}x{H}x{st.samples}spp frame, median of 3 runs ({secs:.3f} s) after 1 warm-up"
     return {
         "value": round(rays / secs / 1e6, 3),
         "unit": "Mrays/s",
         "cores": threads,
-        "host_cpus": {"affinity": aff, "os_cpu_count": os.cpu_count()},
+        "host_cpus": {"affinity": aff, "os_cpu_count": os.cpu_count(), "cgroup_cpu_quota": quota},
         "kind": "port",
-        "sample": sample + f"; oracle/oracle.c on {threads} threads (tile queue of renderer.go:67-148; the Go "
-                           f"toolchain is absent, SURVEY.md §8c)",
+        "sample": sample + f"; oracle/oracle.c on {threads} threads = runtime.NumCPU() (the affinity count, "
+                           f"cmd/raytracer/main.go:46) on the tile queue of renderer.go:67-148; the Go toolchain "
+                           f"is absent (SURVEY.md §8c)" + (f"; the cgroup grants {quota} CPUs of time" if quota else ""),
     }
+
+
+def cpu_secondary(args, rtgo, scene, W, H, st, cfg):
+    """Labelled secondary CPU figures: the same frame on 16 threads (the
+    box's per-GPU CPU share), and the as-committed C1 scene (BASELINE
+    configs[0]) on NumCPU threads."""
+    import oracle
+
+    aff, _ = cpu_count_info()
+    out = {}
+    if cfg not in WAVEFRONT and aff != 16:
+        secs = cpu_time(oracle, scene, W, H, st, 16)
+        out["cpu_16_threads"] = {"value": round(W * H * st.samples / secs / 1e6, 3), "unit": "Mrays/s",
+                                 "cores": 16, "sample": f"the same frame on 16 threads, median of 3 ({secs:.3f} s)"}
+    if cfg == "c2":
+        c1 = rtgo.Scene.load_from_file(os.path.join(ROOT, "scenes", "sphere_reflections_light.json"))
+        threads = args.cpu_threads or aff
+        secs = cpu_time(oracle, c1, W, H, st, threads)
+        out["cpu_c1_as_committed"] = {
+            "value": round(W * H * st.samples / secs / 1e6, 3), "unit": "Mrays/s", "cores": threads,
+            "sample": f"BASELINE configs[0]: sphere_reflections_light.json as committed (every camera ray misses, "
+                      f"a black image) {W}x{H}x{st.samples}spp, depth {st.max_depth}, median of 3 ({secs:.3f} s)"}
+    return out
 
 
 def cpu_baseline_bvh(args, rtgo, scene, W, H, st):
@@ -334,9 +414,11 @@ def cpu_baseline_bvh(args, rtgo, scene, W, H, st):
     full spp, so the GPU speedup's algorithmic share is visible."""
     import oracle
 
-    threads, aff = host_threads(args)
-    ntl = 2 * threads
-    world = max(1, rtgo.num_tiles(W, H) // ntl)
+    aff, _ = cpu_count_info()
+    threads = args.cpu_threads or aff
+    n_tiles = rtgo.num_tiles(W, H)
+    ntl = min(n_tiles, 32)
+    world = max(1, n_tiles // ntl)
     t0 = time.perf_counter()
     oracle.render(scene, W, H, st, rank=0, world=world, nthreads=threads, max_tiles=ntl, bvh=True)
     secs = time.perf_counter() - t0
@@ -353,17 +435,35 @@ def cpu_baseline_bvh(args, rtgo, scene, W, H, st):
 
 
 def pmc_traffic(workload):
-    """HBM bytes per launch from the committed rocprofv3 PMC passes
-    (profiles/r02_pmc_traffic.json, scripts/pmc_traffic.py, with the gfx950
-    corrections of MI355X_MICROARCH.md §HBM), if they match this workload."""
+    """HBM bytes per launch of the dominant kernel from the committed
+    rocprofv3 PMC passes (profiles/r03_pmc_traffic.json, scripts/pmc_traffic.py,
+    with the gfx950 corrections of MI355X_MICROARCH.md §HBM), if it holds this
+    workload."""
     try:
         with open(PMC_FILE) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    if d.get("workload") != workload:
-        return None
-    return d.get("hbm_bytes_per_launch")
+    e = d.get(workload) if isinstance(d, dict) else None
+    return e.get("hbm_bytes_per_launch") if e else None
+
+
+def plan_partition(rtgo, torch, dist, scene, W, H, st, rank, world, local, strided):
+    """The frame's tile partition, and the same on every rank: balanced
+    (planned by every rank from the same deterministic pilot, checked by
+    comparing digests) or strided."""
+    if strided:
+        return rtgo.Partition(W, H, world), "strided t % N"
+    ctx = rtgo.Context(local)
+    ctx.set_scene(scene)
+    part = ctx.balanced_partition(W, H, st, world)
+    ctx.close()
+    digest = hashlib.sha256(part.owners(W, H).tobytes()).hexdigest()
+    allg = [None] * world
+    dist.all_gather_object(allg, digest)
+    if len(set(allg)) != 1:
+        raise SystemExit(f"rank {rank}: balanced partitions differ across ranks: {allg}")
+    return part, "balanced (pilot-estimated work, heaviest tile first to the least loaded rank)"
 
 
 def main():
@@ -383,7 +483,8 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         # host-side coordination only (barriers, the max over ranks, the RCCL
-        # id); the frame's data moves through librtgo's RCCL communicator
+        # id, the partition check); the frame's data moves through librtgo's
+        # RCCL communicator
         dist.init_process_group("gloo")
 
     cfg = args.config
@@ -391,63 +492,107 @@ def main():
     args.spp = args.spp or spp
     steps = args.steps or steps_default
     if args.warmup < 0:
-        args.warmup = 1 if cfg in ("c4", "c5") else 3
-    strong = args.strong or cfg in ("c4", "c5")
-    if not strong:
-        H = H * world  # weak scaling: N-fold vertical sample density
+        args.warmup = 1 if cfg in WAVEFRONT else 3
+    weak = args.weak and cfg not in WAVEFRONT
+    if weak:
+        H = H * world  # N-fold vertical sample density
     sts = []
     for i in range(steps):
         st = rtgo.default_settings()
         st.samples, st.max_depth, st.seed = args.spp, args.depth, args.seed + i
         st.num_workers = world
         sts.append(st)
-    F = max(1, args.frames_in_flight or fif_default)
+    if args.frames_in_flight:
+        F = args.frames_in_flight
+    elif world > 1 and cfg not in WAVEFRONT:
+        F = 8  # a rank's share is ~1/N of the frame's work but its longest path is the frame's
+    else:
+        F = fif_default
     scene = load_scene(rtgo, spec)
 
-    comms = [None] * F
+    comm = gstream = part = None
+    part_kind = None
     if world > 1:
-        for j in range(F):  # one communicator per frame slot (frames in flight never share one)
-            uid = [rtgo.Comm.unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
-            comms[j] = rtgo.Comm(uid[0], world, rank, local)
+        uid = [rtgo.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = rtgo.Comm(uid[0], world, rank, local)
+        gstream = torch.cuda.Stream(local)
+        part, part_kind = plan_partition(rtgo, torch, dist, scene, W, H, sts[0], rank, world, local,
+                                         args.strided or cfg in WAVEFRONT)
 
-    frames = []
-    for j in range(F):  # F frames in flight: own context (schedule), stream and buffers each
-        ctx = rtgo.Context(local)
-        ctx.set_scene(scene)
-        fr = Frame(rtgo, torch, ctx, W, H, rank, world, local, torch.cuda.Stream(), comms[j])
-        fr.render(sts[0])  # set-up: builds this context's schedule (like the scene upload)
-        fr.gather()
-        frames.append(fr)
-    counts = frames[0].counts(sts[0])  # algorithmic work of this rank's launch (counting variant, untimed)
+    slots = []
+    for _ in range(F):  # F frames in flight: own context (schedule), stream and buffers each
+        sl = Slot(rtgo, torch, scene, W, H, rank, world, local, part)
+        sl.render(sts[0])  # set-up: builds this context's schedule (like the scene upload)
+        sl.gather(torch, comm, gstream)
+        slots.append(sl)
     barrier_sync(torch, dist, world)
-    elapsed, kms = time_steps(frames, torch, dist, world, sts, args.warmup)
+    counts = slots[0].counts(sts[0])  # algorithmic work of this rank's launch (counting variant, untimed)
+    barrier_sync(torch, dist, world)
+    prof_ctx = slots[0].ctx if cfg in WAVEFRONT else None
+    if prof_ctx is not None:
+        prof_ctx.profile(True)  # per-kernel HIP events in the timed frames (F = 1: every frame on slot 0)
+    elapsed, kms = time_steps(slots, torch, dist, world, sts, args.warmup, comm, gstream)
+    kernel_prof = None
+    if prof_ctx is not None:
+        kernel_prof = prof_ctx.kernel_seconds()
+        prof_ctx.profile(False)
     # the same frames one at a time (the reference's synchronous Render)
-    elapsed1, kms1 = time_steps(frames[:1], torch, dist, world, sts, args.warmup) if F > 1 else (elapsed, kms)
-    first_ms = first_frame_ms(rtgo, torch, dist, scene, W, H, sts[0], rank, world, local, comms[0])
+    elapsed1, kms1 = (time_steps(slots[:1], torch, dist, world, sts, args.warmup, comm, gstream) if F > 1
+                      else (elapsed, kms))
+    first_ms = first_frame_ms(rtgo, torch, scene, W, H, sts[0], local) if world == 1 else None
     e2e = None
     if world == 1 and not args.no_e2e and cfg in ("c2", "c2_committed", "c3"):
         e2e = render_e2e(rtgo, scene, W, H, args, local)
 
-    rays = W * H * args.spp  # all ranks together
+    rays = W * H * args.spp  # the whole frame (all ranks together)
     value = rays * steps / elapsed / 1e6
     kernel1_s = sum(kms1) / len(kms1) / 1e3  # this rank's average launch, one frame at a time
     kernelF_s = sum(kms) / len(kms) / 1e3     # ... with F frames in flight
-    flops = flops_of(counts)
-    achieved_tf = flops / kernel1_s / 1e12
-    npix_local = rtgo.tiles_for_rank(W, H, rank, world) * 1024 if world > 1 else W * H
+    rank_kernel_ms = [kernel1_s * 1e3]
+    if world > 1:
+        allk = [None] * world
+        dist.all_gather_object(allk, kernel1_s * 1e3)
+        rank_kernel_ms = allk
+    ex = executed(counts)
+    npix_local = (part.local_tiles(rank) * 1024) if world > 1 else W * H
     # algorithmic HBM bytes: framebuffer write (float3 + RGBA8 = 16 B/pixel)
     # + the flattened scene read once per workgroup-resident copy (<= 4 KB)
     hbm_bytes = npix_local * 16 + 4096
-    achieved_gbs = hbm_bytes / kernel1_s / 1e9
     workload = "%s %dx%d %dspp depth %d" % (label, W, H, args.spp, args.depth)
+    if cfg in WAVEFRONT:
+        # the dominant kernel: the soft-shadow traversal (wf_occlude<soft>),
+        # its own counts over its own launches (HIP events of the timed frames)
+        soft = counts.soft_occlusion_dict()
+        k_s, k_n = kernel_prof["occlude_soft"]
+        frames_timed = max(1, kernel_prof["resolve"][1])
+        per_frame_s = k_s / frames_timed
+        f64, f32 = fp_split(ex, soft=soft)
+        kern_s, launches_per_frame = per_frame_s, k_n / frames_timed
+        flops_unit = "per frame (%.0f launches)" % launches_per_frame
+        frame64, frame32 = fp_split(ex)
+        whole = {"fp64_flops": frame64, "fp32_flops": frame32,
+                 "frame_kernel_ms": round(kernel1_s * 1e3, 3),
+                 "frac_fp64": round(frame64 / kernel1_s / 1e12 / PEAK_FP64_TFLOPS, 5),
+                 "frac_fp32": round(frame32 / kernel1_s / 1e12 / PEAK_FP32_TFLOPS, 5),
+                 "kernel_ms_per_frame": {k: round(v[0] / frames_timed * 1e3, 3) for k, v in kernel_prof.items()}}
+    else:
+        f64, f32 = fp_split(ex)
+        kern_s = kernel1_s
+        flops_unit = "per launch"
+        whole = None
+    a64, a32 = f64 / kern_s / 1e12, f32 / kern_s / 1e12
+    frac64, frac32 = a64 / PEAK_FP64_TFLOPS, a32 / PEAK_FP32_TFLOPS
+    achieved_gbs = hbm_bytes / kernel1_s / 1e9
 
-    cpu = cpu_bvh = None
+    cpu = cpu_bvh = cpu2 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, rtgo, scene, W, H, sts[0], cfg)
-        cpu_bvh = cpu_baseline_bvh(args, rtgo, scene, W, H, sts[0]) if cfg in ("c4", "c5") else None
+        cpu2 = cpu_secondary(args, rtgo, scene, W, H, sts[0], cfg)
+        cpu_bvh = cpu_baseline_bvh(args, rtgo, scene, W, H, sts[0]) if cfg in WAVEFRONT else None
 
     if rank == 0:
+        parallelism = "1 GPU" if world == 1 else "%d ranks: tiles %s, one RCCL gather per frame" % (world, part_kind)
         out = {
             "metric": "Mrays/sec at 800x600x100spp max_depth=50 (sphere_reflections_light)" if cfg == "c2"
             else "Mrays/sec (%s)" % cfg,
@@ -457,7 +602,7 @@ def main():
             "steps": steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / steps * 1e3, 4),
-            "first_frame_ms": round(first_ms, 4),
+            "first_frame_ms": round(first_ms, 4) if first_ms is not None else None,
             "frames_in_flight": F,
             "one_frame_in_flight": {
                 "value": round(rays * steps / elapsed1 / 1e6, 3),
@@ -466,7 +611,7 @@ def main():
             },
             "render_e2e": e2e,
             "higher_is_better": True,
-            "scaling": "strong" if strong else "weak",
+            "scaling": "weak" if weak else "strong",
             "vs_baseline": None,  # BASELINE.md has no published number on this hardware/config
             "dtype": "f64",
             "data": "synthetic: the reference's scene JSON%s, seeded counter-keyed RNG (seed %d + step: every "
@@ -475,27 +620,35 @@ def main():
             "config": {
                 "workload": workload + ", soft shadows, recursive reflections",
                 "width": W, "height": H, "spp": args.spp, "max_depth": args.depth,
-                "parallelism": "tiles t%%%d + RCCL gather" % world if world > 1 else "1 GPU",
+                "parallelism": parallelism,
                 "frames_in_flight": F,
             },
             "roofline": {
                 "bound": "valu",
-                "achieved": round(achieved_tf, 4),
+                "achieved": round(a64 + a32, 4),
                 "peak": PEAK_FP64_TFLOPS,
                 "unit": "TFLOP/s",
-                "frac": round(achieved_tf / PEAK_FP64_TFLOPS, 5),
+                "frac": round(frac64 + frac32, 5),
+                "frac_fp64": round(frac64, 5),
+                "frac_fp32": round(frac32, 5),
+                "fp64_flops": f64,
+                "fp32_flops": f32,
+                "flops_unit": flops_unit,
                 "traffic": pmc_traffic(workload),
                 "kernel": KERNELS[cfg],
-                "kernel_ms": round(kernel1_s * 1e3, 4),
-                "kernel_ms_frames_in_flight": round(kernelF_s * 1e3, 4),
-                "flops_per_launch": flops,
+                "kernel_ms": round(kern_s * 1e3, 4),
+                "kernel_ms_frames_in_flight": round(kernelF_s * 1e3, 4) if cfg not in WAVEFRONT else None,
                 "note": "FP64 VALU-bound branchy path (binary64 like the Go reference; no matrix shape, no MFMA). "
-                        "achieved = algorithmic FP64 ops of one launch (the kernel's own event counts x DESIGN.md "
-                        "§4.5 per-event costs, executed work only: culled tests are not counted) / average launch "
-                        "time one frame at a time (HIP events on the render stream). kernel_ms_frames_in_flight: "
-                        "the same launches overlapped (they share the GPU with their neighbours' tails). "
-                        "traffic = HBM bytes per launch from rocprofv3 FETCH_SIZE+WRITE_SIZE passes.",
+                        "EXECUTED work only: the counting variant's counts minus rt_counts.culled (the camera "
+                        "samples of culled pixels it walks only to report the reference's counts), x DESIGN.md "
+                        "§4.5 per-event costs; BVH box tests run in binary32 and are priced against the FP32 peak "
+                        "(157.3 TF): frac = frac_fp64 + frac_fp32, the share of the kernel's time the VALU would "
+                        "need at peak rate.  kernel_ms: the dominant kernel's average launch one frame at a time "
+                        "(HIP events on the render stream; for c4/c5 the soft-shadow traversal kernel's time per "
+                        "frame from rt_context_profile's events in the timed frames).  traffic = HBM bytes per "
+                        "launch from rocprofv3 FETCH_SIZE + WRITE_SIZE passes (profiles/r03_pmc_traffic.json).",
             },
+            "roofline_frame": whole,
             "roofline_hbm": {
                 "bound": "hbm",
                 "achieved": round(achieved_gbs, 3),
@@ -504,20 +657,27 @@ def main():
                 "frac": round(achieved_gbs / PEAK_HBM_GBS, 7),
                 "algorithmic_bytes_per_launch": hbm_bytes,
             },
-            "counts_rank0": counts,
+            "rank_kernel_ms": [round(x, 4) for x in rank_kernel_ms],
+            "rank_estimated_work": [round(part.work(r)) for r in range(world)] if world > 1 else None,
+            "counts_rank0": counts.as_dict(),
+            "counts_rank0_executed": ex,
             "cpu_baseline": cpu,
         }
         if cpu:
             out["gpu_over_cpu"] = round(value / cpu["value"], 1)
+            out["gpu_over_cpu_one_frame"] = round(out["one_frame_in_flight"]["value"] / cpu["value"], 1)
+            out.update(cpu2 or {})
             if e2e:
                 out["render_e2e"]["vs_cpu"] = round(e2e["value"] / cpu["value"], 1)
+                out["render_e2e"]["oneshot_vs_cpu"] = round(e2e["oneshot_value"] / cpu["value"], 1)
         if cpu_bvh:
             out["cpu_baseline_bvh"] = cpu_bvh
             out["gpu_over_cpu_bvh"] = round(value / cpu_bvh["value"], 1)
         print(json.dumps(out), flush=True)
-    for c in comms:
-        if c is not None:
-            c.close()
+    for sl in slots:
+        sl.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -119,7 +120,7 @@ struct rt_context {
   unsigned long long* dbg = nullptr;
   // the work schedule (rt_schedule.hip), cached per (scene, W, H, rank, world, settings)
   uint64_t scene_gen = 0;
-  int64_t order_key[13] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+  int64_t order_key[14] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
   int32_t* d_blocks = nullptr;  // work blocks, kBlockInts ints each, heaviest first
   size_t d_blocks_cap = 0;  // bytes
   int32_t num_blocks = 0;
@@ -150,7 +151,84 @@ struct rt_context {
   WfCtl* wf_ctl = nullptr;   // device
   WfCtl* wf_host = nullptr;  // pinned ring of kWfRing snapshots
   hipEvent_t wf_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // tile partition (rt_context_set_partition): its data and every rank's
+  // tile list on this device (null: strided)
+  std::shared_ptr<const PartitionData> part;
+  int32_t* d_part = nullptr;
+  size_t d_part_cap = 0;
+  // per-kernel device time of the wavefront path (rt_context_profile): an
+  // event pool, the blocks of it the last frame recorded ({first event,
+  // first class, last class}) and the totals
+  bool prof_on = false;
+  std::vector<hipEvent_t> prof_pool;
+  size_t prof_used = 0;
+  struct ProfBlock {
+    size_t base;
+    int first, last;
+  };
+  std::vector<ProfBlock> prof_pending;
+  double prof_secs[kWfClasses] = {0};
+  int64_t prof_launches[kWfClasses] = {0};
 };
+
+// Events for kernel classes [first, last] of one launch sequence: ev[k] opens
+// class k (null when not profiling)
+static hipEvent_t* prof_block(rt_context* c, int first, int last) {
+  if (!c->prof_on) return nullptr;
+  const size_t need = kWfProfEvents;
+  while (c->prof_pool.size() < c->prof_used + need) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    c->prof_pool.push_back(e);
+  }
+  hipEvent_t* ev = c->prof_pool.data() + c->prof_used;
+  c->prof_pending.push_back({c->prof_used, first, last});
+  c->prof_used += need;
+  return ev;
+}
+
+// Adds the recorded blocks to the totals (waits for them)
+static int prof_collect(rt_context* c) {
+  if (c->prof_pending.empty()) return RT_OK;
+  const auto& lastb = c->prof_pending.back();
+  HIP_TRY(hipEventSynchronize(c->prof_pool[lastb.base + lastb.last + 1]));
+  for (const auto& b : c->prof_pending)
+    for (int k = b.first; k <= b.last; ++k) {
+      float ms = 0;
+      HIP_TRY(hipEventElapsedTime(&ms, c->prof_pool[b.base + k], c->prof_pool[b.base + k + 1]));
+      c->prof_secs[k] += ms * 1e-3;
+      c->prof_launches[k] += 1;
+    }
+  c->prof_pending.clear();
+  c->prof_used = 0;
+  return RT_OK;
+}
+
+// Does a render of (w, h, world) use the context's partition?
+static bool use_partition(const rt_context* c, int w, int h, int world) {
+  return c->part && world > 1 && c->part->w == w && c->part->h == h && c->part->world == world;
+}
+// Tiles of `rank`: the partition's list or the strided set (createRenderTasks's
+// tiles t % world == rank)
+static int local_tiles(const rt_context* c, int w, int h, int rank, int world) {
+  if (use_partition(c, w, h, world)) return c->part->offsets[rank + 1] - c->part->offsets[rank];
+  return rt_tiles_for_rank(w, h, rank, world);
+}
+static void host_tiles(const rt_context* c, int w, int h, int rank, int world, std::vector<int32_t>* out) {
+  if (use_partition(c, w, h, world)) {
+    const PartitionData& d = *c->part;
+    out->assign(d.lists.begin() + d.offsets[rank], d.lists.begin() + d.offsets[rank + 1]);
+  } else {
+    strided_tiles(w, h, rank, world, out);
+  }
+}
+static const int32_t* dev_tiles(const rt_context* c, int w, int h, int rank, int world) {
+  return use_partition(c, w, h, world) ? c->d_part + c->part->offsets[rank] : nullptr;
+}
+
+namespace rtgo {
+bool context_has_bvh(const rt_context* c) { return c && !c->flat.bvh.empty(); }
+}  // namespace rtgo
 
 extern "C" {
 
@@ -202,7 +280,7 @@ int rt_context_create(int32_t device, rt_context** out) {
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
-  if (e == hipSuccess) e = hipMalloc((void**)&c->d_counts, 16 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->d_counts, kCountSlots * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_totals, 4 * sizeof(int32_t), hipHostMallocDefault);
 
   if (e != hipSuccess) {
@@ -227,6 +305,7 @@ void rt_context_destroy(rt_context* c) {
   if (c->d_meas) (void)hipFree(c->d_meas);
   if (c->d_split) (void)hipFree(c->d_split);
   if (c->d_sched) (void)hipFree(c->d_sched);
+  if (c->d_part) (void)hipFree(c->d_part);
   if (c->h_totals) (void)hipHostFree(c->h_totals);
   if (c->wf_mem) (void)hipFree(c->wf_mem);
   if (c->wf_rad) (void)hipFree(c->wf_rad);
@@ -234,6 +313,7 @@ void rt_context_destroy(rt_context* c) {
   if (c->wf_host) (void)hipHostFree(c->wf_host);
   for (hipEvent_t& e : c->wf_ev)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -358,150 +438,234 @@ static int grow(void* ptr, size_t* cap, size_t n) {
   return RT_OK;
 }
 
+// The launch parameters of a render of (w, h, st) by `rank` of `world`
+// (outputs, counters and schedule are filled in by the caller).
+static void base_params(const rt_context* c, int w, int h, const rt_settings* st, int rank, int world, int layout,
+                        KParams* out) {
+  const FlatScene& f = c->flat;
+  KParams& p = *out;
+  memset(&p, 0, sizeof p);
+  p.spheres = c->d_spheres;
+  p.tris = c->d_tris;
+  p.boxes = c->d_boxes;
+  p.mats = c->d_mats;
+  p.lights = c->d_lights;
+  p.bvh = c->d_bvh;
+  p.jump = c->d_jump;
+  p.sky = st->sky != RT_SKY_NONE ? c->d_sky + (st->sky - 1) : nullptr;
+  p.dbg = c->dbg;
+  memcpy(p.cam, f.cam_pos, sizeof p.cam);
+  p.aspect = f.aspect;
+  p.seed_key = rt_rng_seed_key(st->seed);
+  p.ns = (int32_t)f.spheres.size();
+  p.nt = (int32_t)f.tris.size();
+  p.nl = (int32_t)f.lights.size();
+  p.nb = (int32_t)f.boxes.size();
+  p.use_bvh = f.bvh.empty() ? 0 : 1;
+  p.W = w;
+  p.H = h;
+  p.spp = st->samples;
+  p.max_depth = st->max_depth;
+  p.recursive = st->recursive_reflections != 0;
+  p.soft = st->soft_shadows != 0;
+  p.rank = rank;
+  p.world = world;
+  p.tiles_x = (w + 31) / 32;
+  p.ntiles = rt_num_tiles(w, h);
+  p.layout = layout;
+  // LDS staging of the scene prefix + BVH stack placement
+  p.stage_src = c->d_scene;
+  p.stage_bytes = c->tun.stage ? c->stage_bytes : 0;
+  p.stack_off = (p.stage_bytes + 15) & ~15;
+  p.stack_depth = std::max(1, f.bvh_depth);
+}
+
+// The scheduler's inputs for `tiles` (host masks and costs uploaded into
+// `in`, the scratch layout at `scratch`), as SchedParams.
+static SchedParams sched_params(rt_context* c, const KParams& p, const rt_settings* st, const std::vector<int32_t>& tiles,
+                                const int32_t* d_tiles, bool masks, bool frustum, double block_work, int bigP,
+                                void* scratch, unsigned long long* d_masks, float* d_cost) {
+  const FlatScene& f = c->flat;
+  const rt_tuning& tn = c->tun;
+  SchedParams sp;
+  memset(&sp, 0, sizeof sp);
+  sched_layout(scratch, (int)tiles.size(), &sp);
+  sp.spheres = c->d_spheres;
+  sp.tris = c->d_tris;
+  memcpy(sp.cam, f.cam_pos, sizeof sp.cam);
+  sp.vw = 2.0 * f.aspect;
+  sp.W = p.W;
+  sp.H = p.H;
+  sp.rank = p.rank;
+  sp.world = p.world;
+  sp.tiles_x = (p.W + 31) / 32;
+  sp.ntiles = rt_num_tiles(p.W, p.H);
+  sp.local = (int)tiles.size();
+  sp.spp = st->samples;
+  sp.big_pixels = bigP;
+  sp.frustum = frustum;
+  sp.split_samples = tn.split_samples > 0 ? std::min(64, tn.split_samples) : 64;
+  sp.split_depth = tn.split_depth > 0 ? tn.split_depth : 16;
+  sp.block_work = block_work;
+  sp.tile_masks = masks ? d_masks : nullptr;
+  sp.tile_cost = d_cost;
+  sp.tile_list = d_tiles;
+  return sp;
+}
+
+// The one-sample pilot render of sp's tiles (blocks of 64 pixels, packed
+// output into `buf`, npx * 24 bytes): each pixel's longest path and its
+// bounces into sp.work_max / work_sum.
+static int run_pilot(const rt_context* c, const KParams& p, SchedParams* sp, char* buf, hipStream_t s) {
+  const size_t npx = (size_t)sp->local * 1024;
+  float* plin = (float*)buf;
+  uint8_t* prgba = (uint8_t*)buf + npx * 12;
+  unsigned int* plen = (unsigned int*)((uint8_t*)buf + npx * 16);
+  KParams q = p;
+  q.spp = 1;
+  q.blocks = sp->pilot_blocks;
+  q.num_blocks = sp->local * 16;
+  q.num_wgs = q.num_blocks;
+  q.layout = RT_LAYOUT_PACKED_TILES;
+  q.out_linear = plin;
+  q.out_rgba = prgba;
+  q.counts = nullptr;
+  q.dbg = nullptr;
+  q.work_max = plen;
+  q.work_sum = plen + npx;
+  q.soft = 0;  // path lengths only (see above)
+  if (c->tun.pilot_depth > 0) q.max_depth = std::min(q.max_depth, c->tun.pilot_depth);
+  q.tile_masks = sp->tile_masks;
+  q.split_rad = nullptr;
+  q.split_hits = nullptr;
+  q.split_cnt = nullptr;
+  q.acc = nullptr;
+  q.acc_mode = 0;
+  q.sample_base = 0;
+  q.spp_total = 1;
+  HIP_TRY(hipMemsetAsync(plen, 0, 2 * npx * sizeof(unsigned int), s));
+  const int e = launch_render(q, false, s);
+  if (e != hipSuccess) {
+    set_error(std::string("pilot launch failed: ") + hipGetErrorString((hipError_t)e));
+    return RT_E_DEVICE;
+  }
+  sp->work_max = plen;
+  sp->work_sum = plen + npx;
+  sp->work_n = 1;
+  return RT_OK;
+}
+
+// path bounces per block: 8 full-wave bounce steps; 16x that with a BVH,
+// whose bounces are long divergent traversals that need full waves more
+// than short blocks (C4: 2.10 s at 512, 1.77 s at 8192)
+// (triangle scenes: 256 -- a bounce there tests 12 triangles per cube, so
+// fewer bounces make a block: silver C3 0.56 -> 0.46 ms; sphere scenes:
+// 384 since solo paths (r02, headline 0.785 -> 0.745 ms; 320: 0.755,
+// 448: 0.79, 512 was the r01 optimum)
+static double default_block_work(const rt_context* c) {
+  const FlatScene& f = c->flat;
+  double block_work = !f.bvh.empty() ? 8192.0 : (f.tris.empty() ? 384.0 : 256.0);
+  if (c->tun.block_work > 0) block_work = std::max(1.0, c->tun.block_work);
+  return block_work;
+}
+
+// primary-ray candidate masks apply (small linear-scan scenes)
+static bool masks_apply(const FlatScene& f) { return f.bvh.empty() && f.spheres.size() <= 64 && f.tris.size() <= 64; }
+
 static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hipStream_t s) {
   const FlatScene& f = c->flat;
   const int w = p->W, h = p->H, rank = p->rank, world = p->world;
   const rt_tuning& tn = c->tun;
   int bigP = big_block_pixels(st->samples, tn);
-  // path bounces per block: 8 full-wave bounce steps; 16x that with a BVH,
-  // whose bounces are long divergent traversals that need full waves more
-  // than short blocks (C4: 2.10 s at 512, 1.77 s at 8192)
-  // (triangle scenes: 256 -- a bounce there tests 12 triangles per cube, so
-  // fewer bounces make a block: silver C3 0.56 -> 0.46 ms; sphere scenes:
-  // 384 since solo paths (r02, headline 0.785 -> 0.745 ms; 320: 0.755,
-  // 448: 0.79, 512 was the r01 optimum)
-  double block_work = !f.bvh.empty() ? 8192.0 : (f.tris.empty() ? 384.0 : 256.0);
-  if (tn.block_work > 0) block_work = std::max(1.0, tn.block_work);
+  const double block_work = default_block_work(c);
   const bool pilot = tn.pilot != 0;
   // a sky makes every camera sample count (a miss returns the sky, not +0):
   // no primary-ray culling, no black tiles
   const bool sky = st->sky != RT_SKY_NONE;
   const bool frustum = tn.frustum != 0 && !sky;
-  const int64_t key[13] = {(int64_t)c->scene_gen, w, h, rank, world, st->samples, st->max_depth,
+  const bool part = use_partition(c, w, h, world);
+  const int64_t key[14] = {(int64_t)c->scene_gen, w, h, rank, world, st->samples, st->max_depth,
                            st->recursive_reflections, st->soft_shadows, bigP, (int64_t)(block_work * 16),
                            (pilot ? 1 + tn.pilot_depth : 0) | (int64_t)tn.split_samples << 16,
-                           (frustum ? 1 : 0) | (sky ? 2 : 0) | (tn.measure ? 4 : 0) | (int64_t)tn.split_depth << 8};
-  const bool masks = f.bvh.empty() && f.spheres.size() <= 64 && f.tris.size() <= 64;
+                           (frustum ? 1 : 0) | (sky ? 2 : 0) | (tn.measure ? 4 : 0) | (int64_t)tn.split_depth << 8,
+                           part ? (int64_t)c->part->id : 0};
+  const bool masks = masks_apply(f);
   const bool new_key = memcmp(key, c->order_key, sizeof key) != 0;
   // a measured re-cut: the previous frame of this key measured every pixel
   const bool remeasured = !new_key && c->meas_state == 2;
   if (new_key || remeasured) {
     int rc = quiesce(c);  // the last render may still read the blocks, masks and split rows
     if (rc) return rc;
-    const int local = rt_tiles_for_rank(w, h, rank, world);
-    // per-tile inputs (host): primary-ray candidate masks, projected-primitive counts
-    if (masks) tile_primary_masks(f, w, h, rank, world, &c->masks_host);
-    else c->masks_host.clear();
-    std::vector<float> cost;
-    tile_cost(f, w, h, rank, world, &cost);
-    const size_t scratch = sched_scratch_bytes(local);
-    const size_t inputs = c->masks_host.size() * sizeof(unsigned long long) + cost.size() * sizeof(float);
-    rc = grow(&c->d_sched, &c->sched_cap, scratch + inputs + 256);
-    if (rc) return rc;
-    SchedParams sp;
-    memset(&sp, 0, sizeof sp);
-    sched_layout(c->d_sched, local, &sp);
-    char* in = (char*)c->d_sched + ((scratch + 255) & ~size_t(255));
-    c->d_masks = masks ? (unsigned long long*)in : nullptr;
-    float* d_cost = (float*)(in + c->masks_host.size() * sizeof(unsigned long long));
-    if (!c->masks_host.empty())
-      HIP_TRY(hipMemcpyAsync(c->d_masks, c->masks_host.data(), c->masks_host.size() * sizeof(unsigned long long),
-                             hipMemcpyHostToDevice, s));
-    if (!cost.empty()) HIP_TRY(hipMemcpyAsync(d_cost, cost.data(), cost.size() * sizeof(float), hipMemcpyHostToDevice, s));
-    sp.spheres = c->d_spheres;
-    sp.tris = c->d_tris;
-    memcpy(sp.cam, f.cam_pos, sizeof sp.cam);
-    sp.vw = 2.0 * f.aspect;
-    sp.W = w;
-    sp.H = h;
-    sp.rank = rank;
-    sp.world = world;
-    sp.tiles_x = (w + 31) / 32;
-    sp.ntiles = rt_num_tiles(w, h);
-    sp.local = local;
-    sp.spp = st->samples;
-    sp.big_pixels = bigP;
-    sp.frustum = frustum;
-    sp.split_samples = tn.split_samples > 0 ? std::min(64, tn.split_samples) : 64;
-    sp.block_work = block_work;
-    sp.tile_masks = c->d_masks;
-    sp.tile_cost = d_cost;
-    int e = sched_launch_pixels(sp, s);
-    if (e != hipSuccess) {
-      set_error(std::string("schedule launch failed: ") + hipGetErrorString((hipError_t)e));
-      return RT_E_DEVICE;
-    }
-    sp.split_depth = tn.split_depth > 0 ? tn.split_depth : 16;
-    if (remeasured) {  // every sample's path of the last frame (the measuring render)
-      sp.work_max = (const unsigned int*)c->d_meas;
-      sp.work_sum = sp.work_max + (size_t)local * 1024;
-      sp.work_n = st->samples;
-    } else if (pilot && local > 0 && st->samples > 0 && st->max_depth > 0) {
-      // one sample per pixel, blocks of 64 pixels, packed output into scratch
-      const size_t npx = (size_t)local * 1024;
-      rc = grow(&c->d_pilot, &c->pilot_cap, npx * 24 + 256);
+    std::vector<int32_t> tiles;
+    host_tiles(c, w, h, rank, world, &tiles);
+    const int local = (int)tiles.size();
+    c->num_blocks = 0;
+    c->nsplit = 0;
+    c->masks_host.clear();
+    c->d_masks = nullptr;
+    if (local > 0) {
+      // per-tile inputs (host): primary-ray candidate masks, projected-primitive counts
+      if (masks) tile_primary_masks(f, w, h, tiles, &c->masks_host);
+      std::vector<float> cost;
+      tile_cost(f, w, h, tiles, &cost);
+      const size_t scratch = sched_scratch_bytes(local);
+      const size_t inputs = c->masks_host.size() * sizeof(unsigned long long) + cost.size() * sizeof(float);
+      rc = grow(&c->d_sched, &c->sched_cap, scratch + inputs + 256);
       if (rc) return rc;
-      float* plin = (float*)c->d_pilot;
-      uint8_t* prgba = (uint8_t*)c->d_pilot + npx * 12;
-      unsigned int* plen = (unsigned int*)((uint8_t*)c->d_pilot + npx * 16);
-      KParams q = *p;
-      q.spp = 1;
-      q.blocks = sp.pilot_blocks;
-      q.num_blocks = local * 16;
-      q.num_wgs = q.num_blocks;
-      q.layout = RT_LAYOUT_PACKED_TILES;
-      q.out_linear = plin;
-      q.out_rgba = prgba;
-      q.counts = nullptr;
-      q.dbg = nullptr;
-      q.work_max = plen;
-      q.work_sum = plen + npx;
-      q.soft = 0;  // path lengths only (see above)
-      if (tn.pilot_depth > 0) q.max_depth = std::min(q.max_depth, tn.pilot_depth);
-      q.tile_masks = c->d_masks;
-      q.split_rad = nullptr;
-      q.split_hits = nullptr;
-      q.split_cnt = nullptr;
-      q.acc = nullptr;
-      q.acc_mode = 0;
-      q.sample_base = 0;
-      q.spp_total = 1;
-      HIP_TRY(hipMemsetAsync(plen, 0, 2 * npx * sizeof(unsigned int), s));
-      e = launch_render(q, false, s);
+      char* in = (char*)c->d_sched + ((scratch + 255) & ~size_t(255));
+      c->d_masks = masks ? (unsigned long long*)in : nullptr;
+      float* d_cost = (float*)(in + c->masks_host.size() * sizeof(unsigned long long));
+      if (!c->masks_host.empty())
+        HIP_TRY(hipMemcpyAsync(c->d_masks, c->masks_host.data(), c->masks_host.size() * sizeof(unsigned long long),
+                               hipMemcpyHostToDevice, s));
+      if (!cost.empty())
+        HIP_TRY(hipMemcpyAsync(d_cost, cost.data(), cost.size() * sizeof(float), hipMemcpyHostToDevice, s));
+      SchedParams sp = sched_params(c, *p, st, tiles, dev_tiles(c, w, h, rank, world), masks, frustum, block_work,
+                                    bigP, c->d_sched, c->d_masks, d_cost);
+      int e = sched_launch_pixels(sp, s);
       if (e != hipSuccess) {
-        set_error(std::string("pilot launch failed: ") + hipGetErrorString((hipError_t)e));
+        set_error(std::string("schedule launch failed: ") + hipGetErrorString((hipError_t)e));
         return RT_E_DEVICE;
       }
-      sp.work_max = plen;
-      sp.work_sum = plen + npx;
-      sp.work_n = 1;
+      if (remeasured) {  // every sample's path of the last frame (the measuring render)
+        sp.work_max = (const unsigned int*)c->d_meas;
+        sp.work_sum = sp.work_max + (size_t)local * 1024;
+        sp.work_n = st->samples;
+      } else if (pilot && st->samples > 0 && st->max_depth > 0) {
+        rc = grow(&c->d_pilot, &c->pilot_cap, (size_t)local * 1024 * 24 + 256);
+        if (rc) return rc;
+        rc = run_pilot(c, *p, &sp, c->d_pilot, s);
+        if (rc) return rc;
+      }
+      e = sched_launch_blocks(sp, false, s);
+      if (e != hipSuccess) {
+        set_error(std::string("schedule launch failed: ") + hipGetErrorString((hipError_t)e));
+        return RT_E_DEVICE;
+      }
+      HIP_TRY(hipMemcpyAsync(c->h_totals, sp.totals, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      const int nblocks = c->h_totals[0], nsplit = c->h_totals[1];
+      rc = grow(&c->d_blocks, &c->d_blocks_cap, (size_t)std::max(nblocks, 1) * kBlockInts * sizeof(int32_t));
+      if (rc) return rc;
+      sp.blocks = c->d_blocks;
+      e = sched_launch_blocks(sp, true, s);
+      if (e != hipSuccess) {
+        set_error(std::string("schedule launch failed: ") + hipGetErrorString((hipError_t)e));
+        return RT_E_DEVICE;
+      }
+      const size_t need = (size_t)nsplit * st->samples * 3 * sizeof(double) + split_flags_bytes(nsplit, st->samples);
+      rc = grow(&c->d_split, &c->split_cap, need + 256);
+      if (rc) return rc;
+      // split pixels' hit bits and sub-block counters start at zero; each
+      // launch's last sub-block of a pixel zeroes them again (rt_kernel.hip)
+      if (nsplit)
+        HIP_TRY(hipMemsetAsync((char*)c->d_split + (size_t)nsplit * st->samples * 3 * sizeof(double), 0,
+                               split_flags_bytes(nsplit, st->samples), s));
+      c->num_blocks = nblocks;
+      c->nsplit = nsplit;
     }
-    e = sched_launch_blocks(sp, false, s);
-    if (e != hipSuccess) {
-      set_error(std::string("schedule launch failed: ") + hipGetErrorString((hipError_t)e));
-      return RT_E_DEVICE;
-    }
-    HIP_TRY(hipMemcpyAsync(c->h_totals, sp.totals, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    const int nblocks = c->h_totals[0], nsplit = c->h_totals[1];
-    rc = grow(&c->d_blocks, &c->d_blocks_cap, (size_t)std::max(nblocks, 1) * kBlockInts * sizeof(int32_t));
-    if (rc) return rc;
-    sp.blocks = c->d_blocks;
-    e = sched_launch_blocks(sp, true, s);
-    if (e != hipSuccess) {
-      set_error(std::string("schedule launch failed: ") + hipGetErrorString((hipError_t)e));
-      return RT_E_DEVICE;
-    }
-    const size_t need = (size_t)nsplit * st->samples * 3 * sizeof(double) + split_flags_bytes(nsplit, st->samples);
-    rc = grow(&c->d_split, &c->split_cap, need + 256);
-    if (rc) return rc;
-    // split pixels' hit bits and sub-block counters start at zero; each
-    // launch's last sub-block of a pixel zeroes them again (rt_kernel.hip)
-    if (nsplit)
-      HIP_TRY(hipMemsetAsync((char*)c->d_split + (size_t)nsplit * st->samples * 3 * sizeof(double), 0,
-                             split_flags_bytes(nsplit, st->samples), s));
-    c->num_blocks = nblocks;
-    c->nsplit = nsplit;
+    // (a rank with no tiles -- more ranks than the frame has tiles -- renders
+    // nothing: no scheduler launch, no read-back of counts it never wrote)
     memcpy(c->order_key, key, sizeof key);
     // a new key's first frame measures (state 1), the next re-cuts (2 -> 3)
     c->meas_state = remeasured ? 3 : (tn.measure && local > 0 ? 1 : 0);
@@ -546,8 +710,12 @@ static int wf_shard_cap(int nl, const rt_tuning& tn, uint64_t samples) {
 
 static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings* st, hipStream_t s, bool count) {
   const FlatScene& f = c->flat;
+  if (c->prof_on) {  // the last frame's kernel times (its events are reused)
+    int rc = prof_collect(c);
+    if (rc) return rc;
+  }
   const int nl = (int)f.lights.size();
-  const int local = rt_tiles_for_rank(kp.W, kp.H, kp.rank, kp.world);
+  const int local = local_tiles(c, kp.W, kp.H, kp.rank, kp.world);
   const uint64_t local_px = (uint64_t)local * 1024;
   const uint64_t spp = (uint64_t)std::max(st->samples, 1);
   uint64_t max_chunk = kWfMaxChunkSamples;
@@ -612,6 +780,7 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   p.tiles_x = kp.tiles_x;
   p.ntiles = kp.ntiles;
   p.layout = kp.layout;
+  p.tile_list = dev_tiles(c, kp.W, kp.H, kp.rank, kp.world);
   // a lane holds at most one pending child per internal node above its leaf:
   // depth - 1 entries (leaves at level bvh_depth, the root at level 1)
   p.stack_depth = std::max(1, f.bvh_depth - 1);
@@ -681,7 +850,7 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
       // host reads the loop state one bounce behind the GPU
       p.live_bound = (int32_t)cap;
       p.dry = 0;
-      int e = wf_launch_bounce(p, true, count, s);
+      int e = wf_launch_bounce(p, true, count, s, prof_block(c, kWfRegen, kWfRegen));
       if (e) return fail(e, "launch");
       std::swap(p.cur, p.next);
       const long long max_iter = (long long)total + std::max(kp.max_depth, 0) + 8;
@@ -690,7 +859,7 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
           set_error("wavefront loop did not terminate");
           return RT_E_DEVICE;
         }
-        e = wf_launch_bounce(p, false, count, s);
+        e = wf_launch_bounce(p, false, count, s, prof_block(c, kWfExtend, kWfRegen));
         if (e) return fail(e, "launch");
         std::swap(p.cur, p.next);
         const int r = (int)(it % kWfRing);
@@ -709,8 +878,11 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
         }
       }
     }
+    hipEvent_t* rev = prof_block(c, kWfResolve, kWfResolve);
+    if (rev) HIP_TRY(hipEventRecord(rev[kWfResolve], s));
     int e = wf_launch_resolve(p, (int)npx, s);
     if (e) return fail(e, "resolve launch");
+    if (rev) HIP_TRY(hipEventRecord(rev[kWfResolve + 1], s));
   }
   return RT_OK;
 }
@@ -733,46 +905,11 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
     return RT_E_INVALID;
   }
   HIP_TRY(hipSetDevice(c->device));
-  const FlatScene& f = c->flat;
   KParams p;
-  memset(&p, 0, sizeof p);
-  p.spheres = c->d_spheres;
-  p.tris = c->d_tris;
-  p.boxes = c->d_boxes;
-  p.mats = c->d_mats;
-  p.lights = c->d_lights;
-  p.bvh = c->d_bvh;
-  p.jump = c->d_jump;
-  p.sky = st->sky != RT_SKY_NONE ? c->d_sky + (st->sky - 1) : nullptr;
+  base_params(c, w, h, st, rank, world, layout, &p);
   p.out_linear = d_linear;
   p.out_rgba = d_rgba;
   p.counts = counts ? c->d_counts : nullptr;
-  p.dbg = c->dbg;
-  memcpy(p.cam, f.cam_pos, sizeof p.cam);
-  p.aspect = f.aspect;
-  p.seed_key = rt_rng_seed_key(st->seed);
-  p.ns = (int32_t)f.spheres.size();
-  p.nt = (int32_t)f.tris.size();
-  p.nl = (int32_t)f.lights.size();
-  p.nb = (int32_t)f.boxes.size();
-  p.use_bvh = f.bvh.empty() ? 0 : 1;
-  p.W = w;
-  p.H = h;
-  p.spp = st->samples;
-  p.max_depth = st->max_depth;
-  p.recursive = st->recursive_reflections != 0;
-  p.soft = st->soft_shadows != 0;
-  p.rank = rank;
-  p.world = world;
-  p.tiles_x = (w + 31) / 32;
-  p.ntiles = rt_num_tiles(w, h);
-  p.layout = layout;
-  {  // LDS staging of the scene prefix + BVH stack placement
-    p.stage_src = c->d_scene;
-    p.stage_bytes = c->tun.stage ? c->stage_bytes : 0;
-    p.stack_off = (p.stage_bytes + 15) & ~15;
-    p.stack_depth = std::max(1, f.bvh_depth);
-  }
   // the caller's stream, as given (NULL = the legacy default stream); a
   // render enqueued on another stream than this context's last one waits for
   // that one first (they share the split rows and the wavefront state)
@@ -787,11 +924,11 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   const int npass = wf ? 1 : std::max(1, (spp + kMaxBlockSamples - 1) / kMaxBlockSamples);
   p.spp_total = spp;
   if (npass > 1) {
-    rc = grow(&c->d_acc, &c->acc_cap, (size_t)rt_tiles_for_rank(w, h, rank, world) * 1024 * 3 * sizeof(double));
+    rc = grow(&c->d_acc, &c->acc_cap, (size_t)local_tiles(c, w, h, rank, world) * 1024 * 3 * sizeof(double));
     if (rc) return rc;
     p.acc = (double*)c->d_acc;
   }
-  unsigned long long total[16] = {0};
+  unsigned long long total[kCountSlots] = {0};
   bool measuring = false;
   for (int pass = 0; pass < npass; ++pass) {
     rt_settings ps = *st;
@@ -809,15 +946,15 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
     // image; a separate instantiation records the lengths): the next frame's
     // blocks are cut from them (prepare_schedule)
     if (!wf && npass == 1 && c->meas_state == 1 && !counts && st->sky == RT_SKY_NONE && p.num_blocks > 0) {
-      const size_t npx = (size_t)rt_tiles_for_rank(w, h, rank, world) * 1024;
+      const size_t npx = (size_t)local_tiles(c, w, h, rank, world) * 1024;
       rc = grow(&c->d_meas, &c->meas_cap, npx * 8);
       if (rc) return rc;
       p.work_max = (unsigned int*)c->d_meas;
       p.work_sum = p.work_max + npx;
       measuring = true;
     }
-    if (counts) HIP_TRY(hipMemsetAsync(c->d_counts, 0, 16 * sizeof(unsigned long long), s));
-    if (measuring) HIP_TRY(hipMemsetAsync(c->d_meas, 0, (size_t)rt_tiles_for_rank(w, h, rank, world) * 1024 * 8, s));
+    if (counts) HIP_TRY(hipMemsetAsync(c->d_counts, 0, kCountSlots * sizeof(unsigned long long), s));
+    if (measuring) HIP_TRY(hipMemsetAsync(c->d_meas, 0, (size_t)local_tiles(c, w, h, rank, world) * 1024 * 8, s));
     if (pass == 0) HIP_TRY(hipEventRecord(c->ev0, s));
     if (wf) {
       rc = render_wavefront(c, p, st, s, counts != nullptr);
@@ -830,10 +967,10 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
       }
     }
     if (counts) {
-      unsigned long long h_c[16];
+      unsigned long long h_c[kCountSlots];
       HIP_TRY(hipMemcpyAsync(h_c, c->d_counts, sizeof h_c, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
-      for (int i = 0; i < 16; ++i) total[i] += h_c[i];
+      for (int i = 0; i < kCountSlots; ++i) total[i] += h_c[i];
     }
   }
   HIP_TRY(hipEventRecord(c->ev1, s));
@@ -851,6 +988,153 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
     counts->shade_events = h_c[6];
     counts->light_evals = h_c[7];
     counts->rng_draws = h_c[8];
+    for (int i = 0; i < kCounters; ++i) {
+      counts->culled[i] = h_c[kCounters + i];
+      counts->soft_occlusion[i] = h_c[2 * kCounters + i];
+    }
+  }
+  return RT_OK;
+}
+
+// ------------------------------------------------------------ partitions
+int rt_context_set_partition(rt_context* c, const rt_partition* p) {
+  if (!c) {
+    set_error("context is NULL");
+    return RT_E_INVALID;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = quiesce(c);  // the last render may still read the tile lists
+  if (rc) return rc;
+  if (!p) {
+    c->part.reset();
+    return RT_OK;
+  }
+  auto d = std::make_shared<const PartitionData>(partition_data(p));
+  rc = grow(&c->d_part, &c->d_part_cap, std::max<size_t>(d->lists.size(), 1) * sizeof(int32_t));
+  if (rc) return rc;
+  if (!d->lists.empty())
+    HIP_TRY(hipMemcpy(c->d_part, d->lists.data(), d->lists.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  c->part = std::move(d);
+  return RT_OK;
+}
+
+// Balanced partition (include/rt_api.h): a one-sample pilot of the whole
+// frame (the schedule's pilot, prepare_schedule, over all tiles as one rank),
+// each tile's estimated work (spp x the sum of its pixels' estimates,
+// sched_tile_work), then longest-processing-time-first: tiles by decreasing
+// work (ties: lower tile first) to the least loaded rank (ties: lower rank).
+int rt_partition_balanced(rt_context* c, int32_t w, int32_t h, const rt_settings* st, int32_t world,
+                          rt_partition** out) {
+  if (!c || !c->have_scene || !out) {
+    set_error("rt_partition_balanced: context without a scene, or out is NULL");
+    return RT_E_INVALID;
+  }
+  *out = nullptr;
+  int rc = validate_settings(st, w, h);
+  if (rc) return rc;
+  if (world < 1 || world > 65536) {
+    set_error("rt_partition_balanced: world must be in [1, 65536]");
+    return RT_E_INVALID;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  const FlatScene& f = c->flat;
+  const rt_tuning& tn = c->tun;
+  hipStream_t s = c->stream;
+  const int ntiles = rt_num_tiles(w, h);
+  std::vector<int32_t> tiles;
+  strided_tiles(w, h, 0, 1, &tiles);
+  KParams p;
+  base_params(c, w, h, st, 0, 1, RT_LAYOUT_PACKED_TILES, &p);
+  const bool masks = masks_apply(f);
+  const bool frustum = tn.frustum != 0 && st->sky == RT_SKY_NONE;
+  std::vector<unsigned long long> mh;
+  if (masks) tile_primary_masks(f, w, h, tiles, &mh);
+  std::vector<float> cost;
+  tile_cost(f, w, h, tiles, &cost);
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t npx = (size_t)ntiles * 1024;
+  const size_t o_in = al(sched_scratch_bytes(ntiles));
+  const size_t o_cost = o_in + al(mh.size() * sizeof(unsigned long long));
+  const size_t o_pilot = o_cost + al(cost.size() * sizeof(float));
+  const size_t o_tw = o_pilot + al(npx * 24);
+  const size_t total = o_tw + al((size_t)ntiles * sizeof(float));
+  char* buf = nullptr;
+  HIP_TRY(hipMalloc((void**)&buf, total));
+  auto fail = [&](int code) {
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(buf);
+    return code;
+  };
+  std::vector<float> work(ntiles, 0.0f);
+  {
+    unsigned long long* d_masks = masks ? (unsigned long long*)(buf + o_in) : nullptr;
+    float* d_cost = (float*)(buf + o_cost);
+    float* d_tw = (float*)(buf + o_tw);
+    if (!mh.empty() &&
+        hipMemcpyAsync(d_masks, mh.data(), mh.size() * sizeof(unsigned long long), hipMemcpyHostToDevice, s))
+      return fail(RT_E_DEVICE);
+    if (!cost.empty() && hipMemcpyAsync(d_cost, cost.data(), cost.size() * sizeof(float), hipMemcpyHostToDevice, s))
+      return fail(RT_E_DEVICE);
+    SchedParams sp = sched_params(c, p, st, tiles, nullptr, masks, frustum, default_block_work(c),
+                                  big_block_pixels(st->samples, tn), buf, d_masks, d_cost);
+    int e = sched_launch_pixels(sp, s);
+    if (e != hipSuccess) {
+      set_error(std::string("partition pilot launch failed: ") + hipGetErrorString((hipError_t)e));
+      return fail(RT_E_DEVICE);
+    }
+    if (tn.pilot != 0 && st->samples > 0 && st->max_depth > 0) {
+      rc = run_pilot(c, p, &sp, buf + o_pilot, s);
+      if (rc) return fail(rc);
+    }
+    e = sched_launch_tile_work(sp, d_tw, s);
+    if (e != hipSuccess) {
+      set_error(std::string("partition estimate launch failed: ") + hipGetErrorString((hipError_t)e));
+      return fail(RT_E_DEVICE);
+    }
+    if (hipMemcpyAsync(work.data(), d_tw, (size_t)ntiles * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      set_error("partition estimate read-back failed");
+      return fail(RT_E_DEVICE);
+    }
+  }
+  (void)fail(RT_OK);
+  PartitionData d;
+  d.w = w;
+  d.h = h;
+  d.world = world;
+  lpt_partition(work, &d);
+  finish_partition(&d);
+  *out = make_partition(std::move(d));
+  return RT_OK;
+}
+
+int rt_context_profile(rt_context* c, int32_t on) {
+  if (!c) {
+    set_error("context is NULL");
+    return RT_E_INVALID;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = prof_collect(c);
+  if (rc) return rc;
+  c->prof_on = on != 0;
+  for (int k = 0; k < kWfClasses; ++k) {
+    c->prof_secs[k] = 0;
+    c->prof_launches[k] = 0;
+  }
+  return RT_OK;
+}
+
+int rt_context_kernel_seconds(rt_context* c, double* seconds, int64_t* launches) {
+  if (!c || !seconds) {
+    set_error("context or seconds is NULL");
+    return RT_E_INVALID;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = prof_collect(c);
+  if (rc) return rc;
+  for (int k = 0; k < kWfClasses; ++k) {
+    seconds[k] = c->prof_secs[k];
+    if (launches) launches[k] = c->prof_launches[k];
   }
   return RT_OK;
 }

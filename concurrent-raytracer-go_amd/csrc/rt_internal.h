@@ -40,16 +40,20 @@ void flatten_scene(const rt_scene& s, FlatScene* out);
 // Binned-SAH BVH over out->spheres (reorders spheres). Requires no triangles.
 // bins / leaf: SAH bins per axis and spheres per leaf at most (0: defaults).
 void build_sphere_bvh(FlatScene* fs, int bins, int leaf);
-// Per local tile of (rank, world): primitives whose projected bounds overlap
-// it (the work estimate of a schedule without a pilot render).
-void tile_cost(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
+// The global tiles a rank renders, in local-tile order (local tile lt is
+// tiles[lt]): t % world == rank (strided, createRenderTasks order dealt
+// round-robin) or a partition's list (rt_partition, rt_multi.cpp).
+void strided_tiles(int32_t W, int32_t H, int32_t rank, int32_t world, std::vector<int32_t>* tiles);
+// Per local tile: primitives whose projected bounds overlap it (the work
+// estimate of a schedule without a pilot render).
+void tile_cost(const FlatScene& fs, int32_t W, int32_t H, const std::vector<int32_t>& tiles,
                std::vector<float>* local_cost);
 constexpr int32_t kBlockBlack = 1;  // block flag (8th int): black tile, nothing to trace
 constexpr int kBlockInts = 16;      // ints per work block record (KParams::blocks)
 // Primary-ray candidate masks per local tile (2 x u64: spheres, triangles;
 // scenes with <= 64 of each): bit i set unless primitive i's bounding sphere
 // provably misses the cone of the tile's camera rays.
-void tile_primary_masks(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
+void tile_primary_masks(const FlatScene& fs, int32_t W, int32_t H, const std::vector<int32_t>& tiles,
                         std::vector<unsigned long long>* masks);
 
 // The GPU work scheduler (rt_schedule.hip).
@@ -64,6 +68,7 @@ struct SchedParams {
   double block_work;
   const unsigned long long* tile_masks;  // per local tile (2 u64) or null (no primary culling)
   const float* tile_cost;      // per local tile: projected primitives (estimate without a pilot)
+  const int32_t* tile_list;    // per local tile: its global tile (a partition), or null: rank + lt * world
   const unsigned int* work_max;  // measured per local pixel: the longest path (bounces + 1) ...
   const unsigned int* work_sum;  // ... and the sum over the measured samples, or null (no measurement)
   int32_t work_n;              // samples measured per pixel (1..16: a pilot; spp: a whole frame)
@@ -96,6 +101,12 @@ constexpr int kJump = 64 + 1;
 // pixels per block (at most 64), so spp <= 1024.
 constexpr int kMaxBlockSamples = 1024;
 constexpr int kDbgStride = 48;  // RT_WG_TIMING: 64-bit words per workgroup in the debug buffer
+// Counters of the counting variants: the nine of rt_counts, then the same
+// nine for the work the counting variant walks only to report the
+// reference's counts (camera samples of culled pixels, rt_counts.culled),
+// then the soft-shadow traversal kernel's share (rt_counts.soft_occlusion).
+constexpr int kCounters = 9;
+constexpr int kCountSlots = 3 * kCounters;
 // Deepest BVH the kernels accept (per-lane LDS stack entries; bvh.cpp keeps
 // the linear scan for deeper trees).  The stacks are allocated per launch for
 // the scene's actual depth (10k spheres: 15 levels).
@@ -111,7 +122,7 @@ struct KParams {
   const uint64_t* jump;        // PCG jump table: (A_3h, C_3h) for h = 0..kJump-1 (rt_rng.h)
   float* out_linear;
   uint8_t* out_rgba;
-  unsigned long long* counts;  // 9 counters (rt_counts order) or null
+  unsigned long long* counts;  // kCounters counters (rt_counts order, then the culled ones) or null
   unsigned long long* dbg;     // per-WG timing records (RT_WG_TIMING builds only) or null
   const int32_t* blocks;       // per block, kBlockInts ints: {local tile, first pixel, pixel count, first sample,
                                //   samples, split slot (-1: none), sub-blocks of the split pixel, flags,
@@ -154,6 +165,12 @@ int launch_render(const KParams& p, bool count, void* stream);
 size_t render_shmem(const KParams& p);
 int launch_unpack(int32_t W, int32_t H, int32_t world, const void* gathered, size_t share_bytes, size_t rgba_off,
                   float* ol, uint8_t* orgba, void* stream);
+// The same for a partition: slot[t] = {owner rank, local tile} of global tile t.
+int launch_unpack_map(int32_t W, int32_t H, const int32_t* slot, const void* gathered, size_t share_bytes,
+                      size_t rgba_off, float* ol, uint8_t* orgba, void* stream);
+// Per global tile of a frame, the sum of its pixels' estimated work (rt_schedule.hip
+// sched_est of a whole-frame pilot): the input of a balanced partition.
+int sched_launch_tile_work(const SchedParams& p, float* tile_work, void* stream);
 
 // The geometry an occlusion / closest-hit query needs (device pointers).
 struct Geo {
@@ -199,6 +216,7 @@ struct WfParams {
   const DSky* sky;           // miss radiance or null (black)
   int32_t nl, max_depth, recursive, soft, spp;
   int32_t W, H, rank, world, tiles_x, ntiles, layout;
+  const int32_t* tile_list;  // per local tile: its global tile (a partition), or null: rank + lt * world
   int32_t stack_depth;       // BVH stack entries per lane (the tree's depth - 1)
   int32_t lds_nodes;         // leading quantized nodes (breadth-first: the top levels) staged in LDS
   int32_t bvh_nodes;         // quantized nodes in all
@@ -223,11 +241,40 @@ struct WfParams {
   float* out_linear;
   uint8_t* out_rgba;
 };
-int wf_launch_bounce(const WfParams& p, bool first, bool count, void* stream);
+// Kernel classes of one bounce (rt_context_profile): prof, when not null,
+// holds kWfProfEvents hipEvent_t recorded at their boundaries (event k opens
+// class k, event k + 1 closes it; a skipped kernel takes no time).
+enum { kWfExtend = 0, kWfShade1, kWfHard, kWfSoftgen, kWfSoft, kWfShade, kWfRegen, kWfResolve, kWfClasses };
+constexpr int kWfProfEvents = kWfClasses + 1;  // (one block serves any class range)
+int wf_launch_bounce(const WfParams& p, bool first, bool count, void* stream, const void* prof);
 // Quantized nodes the traversal kernels can stage in LDS next to their stacks
 // (all of them when they fit; else an odd count, so no child pair is split).
 int wf_lds_nodes(int stack_depth, int nodes, int block, int wgs_per_cu);
 int wf_launch_resolve(const WfParams& p, int npix, void* stream);
+
+// ---------------------------------------------------------------- partitions
+// A tile -> rank assignment (rt_partition, include/rt_api.h): every rank's
+// tiles ascending, each tile with its owner and its index in the owner's list
+// (its local tile: the slot range [local * 1024, local * 1024 + 1024) of the
+// owner's packed share).
+struct PartitionData {
+  int32_t w = 0, h = 0, world = 1;
+  std::vector<int32_t> owner;    // per global tile
+  std::vector<int32_t> local;    // per global tile
+  std::vector<int32_t> offsets;  // world + 1: rank r's tiles are lists[offsets[r], offsets[r + 1])
+  std::vector<int32_t> lists;
+  std::vector<double> work;      // per rank: the estimated work of its tiles (balanced partitions), else empty
+  int32_t max_local = 0;
+  uint64_t id = 0;               // unique per partition object (part of a context's schedule key)
+};
+// Fills local / offsets / lists / max_local / id from w, h, world, owner.
+void finish_partition(PartitionData* d);
+// owner and work of a balanced partition of tiles with estimated `work` over
+// d->world ranks (longest processing time first), then finish_partition.
+void lpt_partition(const std::vector<float>& work, PartitionData* d);
+rt_partition* make_partition(PartitionData&& d);
+bool context_has_bvh(const rt_context* c);
+const PartitionData& partition_data(const rt_partition* p);
 
 // ---------------------------------------------------------------- output
 double go_pow_tonemap(double x);  // Pow(x, 1/2.2) with Go's special cases

@@ -411,7 +411,7 @@ __device__ __forceinline__ BlockLoc block_loc(KArg k, int b) {
   r.slot = f.y;
   r.nsub = f.z;
   r.black = (f.w & kBlockBlack) != 0;
-  r.tile = k->rank + r.lt * k->world;
+  r.tile = l.z;  // the block's global tile (sched_blocks: strided or a partition's list)
   r.tx = r.tile % k->tiles_x;
   r.ty = r.tile / k->tiles_x;
   return r;
@@ -714,9 +714,9 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   }
   __syncthreads();
 
-  Counters c;
+  Counters c, culled;
   if constexpr (kCount) {
-    for (int i = 0; i < 9; ++i) c.v[i] = 0;
+    for (int i = 0; i < kCounters; ++i) c.v[i] = culled.v[i] = 0;
   }
 #ifdef RT_WG_TIMING
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
@@ -781,18 +781,33 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       const int p = kCount ? pj : (int)lpix[pj], s = s0 + sl, id = p * ns + sl;
       const int tp = p0 + p;
       const int x = x0 + (tp & 31), y = y0 + (tp >> 5);
-      if (tp >= 1024 || !live || x >= W || y >= H) continue;
-      cnt<kCount>(c, C_CAM);
-      rt_rng rng;
-      d3 o, d;
-      camera_ray_c<kCount>(ck, x, y, sbase + s, rng, o, d, c);
-      if (!trace) continue;
-      cnt<kCount>(c, C_BOUNCE);
-      // hit or miss is all this phase needs: an any-hit query over
-      // [0.001, +inf) decides exactly what hitWorld's closest hit would
-      const bool hit = sky || (h.masks ? any_hit_masked<kCount>(h.g, o, d, __builtin_inf(), prim, c)
-                                       : any_hit<kCount>(h.g, o, d, __builtin_inf(), stack, c));
-      if (hit) atomicOr(&hbits[id >> 5], 1u << (id & 31));
+      // (kCount) this sample's counts; a sample the product never traces (a
+      // black block, or a pixel without primary candidates) also goes to
+      // `culled`, so the executed work is the difference (rt_counts.culled)
+      Counters cs;
+      if constexpr (kCount)
+        for (int i = 0; i < kCounters; ++i) cs.v[i] = 0;
+      [&] {
+        if (tp >= 1024 || !live || x >= W || y >= H) return;
+        cnt<kCount>(cs, C_CAM);
+        rt_rng rng;
+        d3 o, d;
+        camera_ray_c<kCount>(ck, x, y, sbase + s, rng, o, d, cs);
+        if (!trace) return;
+        cnt<kCount>(cs, C_BOUNCE);
+        // hit or miss is all this phase needs: an any-hit query over
+        // [0.001, +inf) decides exactly what hitWorld's closest hit would
+        const bool hit = sky || (h.masks ? any_hit_masked<kCount>(h.g, o, d, __builtin_inf(), prim, cs)
+                                         : any_hit<kCount>(h.g, o, d, __builtin_inf(), stack, cs));
+        if (hit) atomicOr(&hbits[id >> 5], 1u << (id & 31));
+      }();
+      if constexpr (kCount) {
+        const bool traced = !loc.black && ((pxlive >> p) & 1ull);
+        for (int i = 0; i < kCounters; ++i) {
+          c.v[i] += cs.v[i];
+          if (!traced) culled.v[i] += cs.v[i];
+        }
+      }
     }
   }
   __syncthreads();
@@ -1281,9 +1296,9 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     }
   }
   if constexpr (kCount) {
-    for (int i = 0; i < 9; ++i) {
+    for (int i = 0; i < 2 * kCounters; ++i) {
       // wave reduction, then one atomic per counter
-      unsigned long long v = c.v[i];
+      unsigned long long v = i < kCounters ? c.v[i] : culled.v[i - kCounters];
       for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
       if (lane3 == 0) atomicAdd(&k->counts[i], v);
     }
@@ -1339,6 +1354,27 @@ __global__ __launch_bounds__(256) void unpack_kernel(int W, int H, int world, in
     *reinterpret_cast<uint32_t*>(orgba + o * 4) = *reinterpret_cast<const uint32_t*>(share + rgba_off + pi * 4);
 }
 
+// The same scatter for a partition: slot[t] = {owner rank, local tile}.
+__global__ __launch_bounds__(256) void unpack_map_kernel(int W, int H, int tiles_x, const int2* __restrict__ slot,
+                                                         const uint8_t* __restrict__ g, size_t share_bytes,
+                                                         size_t rgba_off, float* __restrict__ ol,
+                                                         uint8_t* __restrict__ orgba) {
+  const long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= (long long)W * H) return;
+  const int y = (int)(o / W), x = (int)(o - (long long)y * W);
+  const int2 rl = slot[(y >> 5) * tiles_x + (x >> 5)];
+  const size_t pi = (size_t)rl.y * 1024 + (size_t)((y & 31) * 32 + (x & 31));
+  const uint8_t* share = g + (size_t)rl.x * share_bytes;
+  if (ol) {
+    const float* pl = reinterpret_cast<const float*>(share) + pi * 3;
+    ol[o * 3 + 0] = pl[0];
+    ol[o * 3 + 1] = pl[1];
+    ol[o * 3 + 2] = pl[2];
+  }
+  if (orgba)
+    *reinterpret_cast<uint32_t*>(orgba + o * 4) = *reinterpret_cast<const uint32_t*>(share + rgba_off + pi * 4);
+}
+
 size_t render_shmem(const KParams& p) {
   return (size_t)p.stack_off + (p.use_bvh ? sizeof(int) * p.stack_depth * 64 : 0);
 }
@@ -1352,6 +1388,23 @@ int launch_render(const KParams& p, bool count, void* stream) {
   // (the opted-in sky has instantiations of its own: its code would cost the
   // others registers; the pilot and the counting variant ignore it -- path
   // lengths and counts do not depend on what a miss returns)
+  if (count && p.sky) {
+    // counts with an opted-in sky: the image comes from the sky variant, the
+    // counts from a second, output-less launch of the counting variant (it
+    // leaves the split rows zeroed like any launch and neither reads nor
+    // writes the sample-pass sums)
+    KParams q = p;
+    q.counts = nullptr;
+    const int e = launch_render(q, false, stream);
+    if (e != hipSuccess) return e;
+    q = p;
+    q.sky = nullptr;
+    q.out_linear = nullptr;
+    q.out_rgba = nullptr;
+    q.acc = nullptr;
+    q.acc_mode = 0;
+    return launch_render(q, true, stream);
+  }
   if (p.work_max) {  // a measuring render (pilot or first frame): its own instantiation (and kernel name)
     if (stage)
       hipLaunchKernelGGL((render_kernel<false, true, true, false>), g, b, shmem, st, p);
@@ -1380,6 +1433,16 @@ int launch_unpack(int32_t W, int32_t H, int32_t world, const void* gathered, siz
   const unsigned blocks = (unsigned)((total + 255) / 256);
   hipLaunchKernelGGL(unpack_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, W, H, world, (W + 31) / 32,
                      (const uint8_t*)gathered, share_bytes, rgba_off, ol, orgba);
+  return (int)hipGetLastError();
+}
+
+int launch_unpack_map(int32_t W, int32_t H, const int32_t* slot, const void* gathered, size_t share_bytes,
+                      size_t rgba_off, float* ol, uint8_t* orgba, void* stream) {
+  const long long total = (long long)W * H;
+  if (total <= 0) return hipSuccess;
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  hipLaunchKernelGGL(unpack_map_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, W, H, (W + 31) / 32,
+                     reinterpret_cast<const int2*>(slot), (const uint8_t*)gathered, share_bytes, rgba_off, ol, orgba);
   return (int)hipGetLastError();
 }
 

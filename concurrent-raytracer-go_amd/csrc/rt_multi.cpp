@@ -16,9 +16,13 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <mutex>
 #include <string>
+#include <system_error>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "rt_internal.h"
@@ -79,19 +83,38 @@ struct DevBuf {
   }
 };
 
-// The scene's content as bytes: two calls with equal bytes render the same
-// image, so the second one re-uploads nothing.
+// The scene's content as bytes, field by field (padding is left out: caller
+// padding that differs must not force a re-upload): two calls with equal
+// bytes render the same image, so the second one re-uploads nothing.
 void scene_bytes(const rt_scene& s, std::vector<uint8_t>* out) {
   out->clear();
   auto put = [&](const void* p, size_t n) {
     const uint8_t* b = (const uint8_t*)p;
     out->insert(out->end(), b, b + n);
   };
-  put(&s.camera, sizeof s.camera);
+  const rt_camera& c = s.camera;
+  put(c.position, sizeof c.position);
+  put(c.look_at, sizeof c.look_at);
+  put(c.up, sizeof c.up);
+  put(&c.fov, sizeof c.fov);
+  put(&c.aspect_ratio, sizeof c.aspect_ratio);
   put(&s.num_objects, sizeof s.num_objects);
   put(&s.num_lights, sizeof s.num_lights);
-  if (s.num_objects > 0) put(s.objects, sizeof(rt_object) * (size_t)s.num_objects);
-  if (s.num_lights > 0) put(s.lights, sizeof(rt_light) * (size_t)s.num_lights);
+  for (int i = 0; i < s.num_objects; ++i) {
+    const rt_object& o = s.objects[i];
+    put(&o.type, sizeof o.type);
+    put(o.position, sizeof o.position);
+    put(o.size, sizeof o.size);
+    put(&o.radius, sizeof o.radius);
+    const rt_material& m = o.material;
+    put(&m.kind, sizeof m.kind);
+    put(m.color, sizeof m.color);
+    put(&m.roughness, sizeof m.roughness);
+    put(&m.metallic, sizeof m.metallic);
+    put(&m.specular, sizeof m.specular);
+    put(&m.refraction_index, sizeof m.refraction_index);
+  }
+  if (s.num_lights > 0) put(s.lights, sizeof(rt_light) * (size_t)s.num_lights);  // (no padding)
 }
 
 double now_s() {
@@ -99,6 +122,24 @@ double now_s() {
 }
 
 }  // namespace
+
+struct rt_partition {
+  PartitionData d;
+  std::mutex mu;
+  std::vector<std::pair<int, int32_t*>> slots;  // per device: {owner, local tile} per global tile (unpack)
+};
+
+namespace rtgo {
+
+rt_partition* make_partition(PartitionData&& d) {
+  rt_partition* p = new rt_partition();
+  p->d = std::move(d);
+  return p;
+}
+
+const PartitionData& partition_data(const rt_partition* p) { return p->d; }
+
+}  // namespace rtgo
 
 struct rt_renderer {
   std::vector<Rank> ranks;
@@ -109,7 +150,12 @@ struct rt_renderer {
   DevBuf img_lin, img_rgba;        // root: the W*H image
   std::vector<uint8_t> scene_key;  // content of the scene the contexts hold
   bool have_scene = false;
+  uint64_t scene_gen = 0;          // bumped per upload
   rt_tuning tun;
+  // the partition of the last multi-rank frame and its key (scene, frame, settings)
+  rt_partition* part = nullptr;
+  std::vector<int64_t> part_key;
+  std::vector<double> rank_secs;   // device seconds of each rank's last render
 };
 
 struct rt_comm {
@@ -146,6 +192,47 @@ int group_gather(rt_renderer* r, size_t share_bytes) {
                       r->comms[0], root_s));
   }
   NCCL_TRY(ncclGroupEnd());
+  return RT_OK;
+}
+
+// The tile partition of a multi-rank frame (rt_tuning.partition): balanced
+// for linear-scan scenes by default, whose work sits in a few tiles (the
+// headline scene: 23 of 475 tiles), strided for BVH scenes (thousands of
+// busy tiles).  A balanced partition is planned on the first rank's device
+// once per (scene, frame, settings) and set on every rank's context.
+int renderer_partition(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t h, const rt_settings* st) {
+  const int n = (int)r->ranks.size();
+  int mode = r->tun.partition;
+  if (mode == RT_PARTITION_AUTO)
+    mode = context_has_bvh(r->ranks[0].ctx) ? RT_PARTITION_STRIDED : RT_PARTITION_BALANCED;
+  if (mode != RT_PARTITION_BALANCED) {
+    if (r->part) {
+      for (Rank& q : r->ranks) {
+        int rc = rt_context_set_partition(q.ctx, nullptr);
+        if (rc) return rc;
+      }
+      rt_partition_destroy(r->part);
+      r->part = nullptr;
+      r->part_key.clear();
+    }
+    return RT_OK;
+  }
+  const std::vector<int64_t> key = {(int64_t)r->scene_gen, w, h, n, st->samples, st->max_depth,
+                                    st->recursive_reflections, st->soft_shadows, st->sky};
+  if (r->part && key == r->part_key) return RT_OK;
+  rt_partition* p = nullptr;
+  int rc = rt_partition_balanced(r->ranks[0].ctx, w, h, st, n, &p);
+  if (rc) return rc;
+  for (Rank& q : r->ranks) {
+    rc = rt_context_set_partition(q.ctx, p);
+    if (rc) {
+      rt_partition_destroy(p);
+      return rc;
+    }
+  }
+  rt_partition_destroy(r->part);
+  r->part = p;
+  r->part_key = key;
   return RT_OK;
 }
 
@@ -234,6 +321,7 @@ void rt_renderer_destroy(rt_renderer* r) {
     }
   }
   for (ncclComm_t c : r->comms) (void)ncclCommDestroy(c);
+  rt_partition_destroy(r->part);
   const int root = r->ranks.empty() ? 0 : r->ranks[0].device;
   r->gathered.release(root);
   r->img_lin.release(root);
@@ -284,6 +372,7 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
     }
     r->scene_key.swap(key);
     r->have_scene = true;
+    r->scene_gen += 1;
   }
   const size_t npix = (size_t)w * h;
   rc = r->img_lin.grow(root, npix * 3 * sizeof(float));
@@ -295,7 +384,10 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
                                  (uint8_t*)r->img_rgba.p, root_s, nullptr);
     if (rc) return rc;
   } else {
-    const size_t share = rt_packed_bytes(w, h, n), rgba_off = rt_packed_rgba_offset(w, h, n);
+    rc = renderer_partition(r, scene, w, h, st);
+    if (rc) return rc;
+    const size_t share = r->part ? rt_partition_packed_bytes(r->part) : rt_packed_bytes(w, h, n);
+    const size_t rgba_off = r->part ? rt_partition_rgba_offset(r->part) : rt_packed_rgba_offset(w, h, n);
     rc = r->gathered.grow(root, share * (size_t)n);
     if (rc) return rc;
     std::vector<uint8_t*> bufs(n);
@@ -328,7 +420,11 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
       if (rcs[k]) errs[k] = rt_last_error();  // (the error text is per thread)
     };
     std::vector<std::thread> pool;
-    for (int k = 1; k < n; ++k) pool.emplace_back(render_rank, k);
+    try {
+      for (int k = 1; k < n; ++k) pool.emplace_back(render_rank, k);
+    } catch (const std::system_error& ex) {  // no thread: the remaining ranks run on this one
+      for (int k = (int)pool.size() + 1; k < n; ++k) render_rank(k);
+    }
     render_rank(0);
     for (std::thread& t : pool) t.join();
     for (int k = 0; k < n; ++k)
@@ -347,7 +443,9 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
       HIP_TRY(hipEventRecord(q.done, q.stream));
       HIP_TRY(hipStreamWaitEvent(root_s, q.done, 0));
     }
-    rc = rt_unpack_tiles_async(w, h, n, r->gathered.p, (float*)r->img_lin.p, (uint8_t*)r->img_rgba.p, root_s);
+    rc = r->part ? rt_unpack_partition_async(r->part, r->gathered.p, (float*)r->img_lin.p, (uint8_t*)r->img_rgba.p,
+                                             root_s)
+                 : rt_unpack_tiles_async(w, h, n, r->gathered.p, (float*)r->img_lin.p, (uint8_t*)r->img_rgba.p, root_s);
     if (rc) return rc;
   }
   HIP_TRY(hipSetDevice(root));
@@ -355,12 +453,15 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
     HIP_TRY(hipMemcpyAsync(out_linear, r->img_lin.p, npix * 3 * sizeof(float), hipMemcpyDeviceToHost, root_s));
   if (out_rgba) HIP_TRY(hipMemcpyAsync(out_rgba, r->img_rgba.p, npix * 4, hipMemcpyDeviceToHost, root_s));
   double ks = 0;
-  for (Rank& q : r->ranks) {
+  r->rank_secs.assign(n, 0.0);
+  for (int k = 0; k < n; ++k) {
+    Rank& q = r->ranks[k];
     HIP_TRY(hipSetDevice(q.device));
     HIP_TRY(hipStreamSynchronize(q.stream));
     double s = 0;
     rc = rt_context_last_kernel_seconds(q.ctx, &s);
     if (rc) return rc;
+    r->rank_secs[k] = s;
     ks = std::max(ks, s);
   }
   const double secs = now_s() - t0;
@@ -392,6 +493,120 @@ int rt_render(const rt_scene* scene, int32_t w, int32_t h, const rt_settings* st
     stats->pixels_per_second = (double)w * h / stats->render_seconds;
   }
   return rc;
+}
+
+
+// ------------------------------------------------------------ partitions
+
+int rt_partition_create(int32_t w, int32_t h, int32_t world, const int32_t* owner, rt_partition** out) {
+  if (!out || w <= 0 || h <= 0 || world < 1 || world > 65536) {
+    set_error("rt_partition_create: invalid arguments");
+    return RT_E_INVALID;
+  }
+  *out = nullptr;
+  PartitionData d;
+  d.w = w;
+  d.h = h;
+  d.world = world;
+  const int ntiles = rt_num_tiles(w, h);
+  d.owner.resize(ntiles);
+  for (int t = 0; t < ntiles; ++t) {
+    const int o = owner ? owner[t] : t % world;
+    if (o < 0 || o >= world) {
+      set_error("rt_partition_create: owner of tile " + std::to_string(t) + " out of range");
+      return RT_E_INVALID;
+    }
+    d.owner[t] = o;
+  }
+  finish_partition(&d);
+  *out = make_partition(std::move(d));
+  return RT_OK;
+}
+
+void rt_partition_destroy(rt_partition* p) {
+  if (!p) return;
+  for (auto& ds : p->slots) {
+    (void)hipSetDevice(ds.first);
+    (void)hipFree(ds.second);
+  }
+  delete p;
+}
+
+int32_t rt_partition_world(const rt_partition* p) { return p ? p->d.world : 0; }
+
+int32_t rt_partition_owner(const rt_partition* p, int32_t t) {
+  return (p && t >= 0 && t < (int32_t)p->d.owner.size()) ? p->d.owner[t] : -1;
+}
+
+int32_t rt_partition_local_tiles(const rt_partition* p, int32_t rank) {
+  if (!p || rank < 0 || rank >= p->d.world) return 0;
+  return p->d.offsets[rank + 1] - p->d.offsets[rank];
+}
+
+int32_t rt_partition_tile(const rt_partition* p, int32_t rank, int32_t local) {
+  if (!p || local < 0 || local >= rt_partition_local_tiles(p, rank)) return -1;
+  return p->d.lists[p->d.offsets[rank] + local];
+}
+
+int32_t rt_partition_max_local(const rt_partition* p) { return p ? p->d.max_local : 0; }
+size_t rt_partition_packed_bytes(const rt_partition* p) { return p ? (size_t)p->d.max_local * 1024 * 16 : 0; }
+size_t rt_partition_rgba_offset(const rt_partition* p) { return p ? (size_t)p->d.max_local * 1024 * 12 : 0; }
+
+double rt_partition_work(const rt_partition* p, int32_t rank) {
+  if (!p || rank < 0 || rank >= (int32_t)p->d.work.size()) return 0.0;
+  return p->d.work[rank];
+}
+
+int rt_unpack_partition_async(const rt_partition* pc, const void* d_gathered, float* d_linear, uint8_t* d_rgba,
+                              void* stream) {
+  if (!pc || !d_gathered) {
+    set_error("rt_unpack_partition_async: invalid arguments");
+    return RT_E_INVALID;
+  }
+  rt_partition* p = const_cast<rt_partition*>(pc);  // (the per-device slot maps are a cache)
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  int32_t* slot = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(p->mu);
+    for (auto& ds : p->slots)
+      if (ds.first == dev) slot = ds.second;
+    if (!slot) {
+      const int ntiles = (int)p->d.owner.size();
+      std::vector<int32_t> h(2 * (size_t)std::max(ntiles, 1), 0);
+      for (int t = 0; t < ntiles; ++t) {
+        h[2 * t] = p->d.owner[t];
+        h[2 * t + 1] = p->d.local[t];
+      }
+      HIP_TRY(hipMalloc((void**)&slot, h.size() * sizeof(int32_t)));
+      if (hipMemcpy(slot, h.data(), h.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(slot);
+        set_error("rt_unpack_partition_async: slot map upload failed");
+        return RT_E_DEVICE;
+      }
+      p->slots.emplace_back(dev, slot);
+    }
+  }
+  int e = launch_unpack_map(p->d.w, p->d.h, slot, d_gathered, rt_partition_packed_bytes(p),
+                            rt_partition_rgba_offset(p), d_linear, d_rgba, stream);
+  if (e != hipSuccess) {
+    set_error(std::string("unpack launch failed: ") + hipGetErrorString((hipError_t)e));
+    return RT_E_DEVICE;
+  }
+  return RT_OK;
+}
+
+int rt_renderer_rank_seconds(const rt_renderer* r, double* out) {
+  if (!r || !out) {
+    set_error("renderer or out is NULL");
+    return RT_E_INVALID;
+  }
+  if (r->rank_secs.size() != r->ranks.size()) {
+    set_error("the renderer has not rendered a frame yet");
+    return RT_E_INVALID;
+  }
+  for (size_t k = 0; k < r->rank_secs.size(); ++k) out[k] = r->rank_secs[k];
+  return RT_OK;
 }
 
 // ------------------------------------------------------------ multi-process
@@ -437,14 +652,12 @@ void rt_comm_destroy(rt_comm* c) {
   delete c;
 }
 
-int rt_comm_gather_tiles_async(rt_comm* c, int32_t w, int32_t h, const void* d_share, void* d_gathered,
-                               void* stream) {
-  if (!c || w <= 0 || h <= 0 || !d_share || (c->rank == 0 && !d_gathered)) {
-    set_error("rt_comm_gather_tiles_async: invalid arguments");
+int rt_comm_gather_bytes_async(rt_comm* c, size_t share, const void* d_share, void* d_gathered, void* stream) {
+  if (!c || !d_share || (c->rank == 0 && !d_gathered)) {
+    set_error("rt_comm_gather_bytes_async: invalid arguments");
     return RT_E_INVALID;
   }
-  if (c->world == 1) return RT_OK;
-  const size_t share = rt_packed_bytes(w, h, c->world);
+  if (c->world == 1 || share == 0) return RT_OK;
   hipStream_t s = (hipStream_t)stream;
   HIP_TRY(hipSetDevice(c->device));
   NCCL_TRY(ncclGroupStart());
@@ -456,6 +669,15 @@ int rt_comm_gather_tiles_async(rt_comm* c, int32_t w, int32_t h, const void* d_s
   }
   NCCL_TRY(ncclGroupEnd());
   return RT_OK;
+}
+
+int rt_comm_gather_tiles_async(rt_comm* c, int32_t w, int32_t h, const void* d_share, void* d_gathered,
+                               void* stream) {
+  if (!c || w <= 0 || h <= 0) {
+    set_error("rt_comm_gather_tiles_async: invalid arguments");
+    return RT_E_INVALID;
+  }
+  return rt_comm_gather_bytes_async(c, rt_packed_bytes(w, h, c->world), d_share, d_gathered, stream);
 }
 
 }  // extern "C"

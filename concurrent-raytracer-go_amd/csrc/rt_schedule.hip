@@ -99,7 +99,7 @@ __device__ __forceinline__ void put_u64(int32_t* r, unsigned long long v) {
 // K1: one wave per 64 pixels of a local tile.
 __global__ __launch_bounds__(64) void sched_pixels(const SchedParams p) {
   const int lt = blockIdx.x >> 4, w = blockIdx.x & 15, lane = threadIdx.x;
-  const int q = w * 64 + lane, t = p.rank + lt * p.world;
+  const int q = w * 64 + lane, t = p.tile_list ? p.tile_list[lt] : p.rank + lt * p.world;
   unsigned long long ms = 0, mt = 0;
   if (p.tile_masks) {
     const unsigned long long ts = p.tile_masks[2 * lt], tt = p.tile_masks[2 * lt + 1];
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(64) void sched_pixels(const SchedParams p) {
     put_u64(r + 8, ms);
     put_u64(r + 10, mt);
     put_u64(r + 12, live);
-    r[14] = 0;
+    r[14] = t;
     r[15] = 0;
   }
 }
@@ -192,7 +192,8 @@ __device__ void put_record(const SchedParams& p, int pos, int lt, int p0, int np
   r[0] = make_int4(lt, p0, np, s0);
   r[1] = make_int4(ns, slot, nsub, flags);
   r[2] = make_int4((int)(uint32_t)ms, (int)(uint32_t)(ms >> 32), (int)(uint32_t)mt, (int)(uint32_t)(mt >> 32));
-  r[3] = make_int4((int)(uint32_t)live, (int)(uint32_t)(live >> 32), 0, 0);
+  const int tile = p.tile_list ? p.tile_list[lt] : p.rank + lt * p.world;
+  r[3] = make_int4((int)(uint32_t)live, (int)(uint32_t)(live >> 32), tile, 0);
 }
 
 // K3 (pass 1, kWrite = false) / K5 (pass 2, kWrite = true): one wave per
@@ -375,7 +376,34 @@ __global__ __launch_bounds__(kBuckets) void sched_scan(const SchedParams p) {
   }
 }
 
+// Per local tile (the whole frame in a planning pilot: lt = t), the
+// estimated work of its image pixels, spp * sum(est) (the weight sched_blocks
+// gives the tile's blocks).  One wave per tile, a fixed reduction order: the
+// same inputs give the same bits on every device, so every rank that plans a
+// partition from the same pilot derives the same one.
+__global__ __launch_bounds__(64) void sched_tile_work(const SchedParams p, float* out) {
+  const int lt = blockIdx.x, lane = threadIdx.x;
+  const int t = p.tile_list ? p.tile_list[lt] : p.rank + lt * p.world;
+  const int x0 = (t % p.tiles_x) * 32, y0 = (t / p.tiles_x) * 32;
+  double a = 0;
+  for (int k = 0; k < 16; ++k) {
+    const int q = k * 64 + lane, x = x0 + (q & 31), y = y0 + (q >> 5);
+    if (x < p.W && y < p.H) a += (double)fabsf(p.est[(size_t)lt * 1024 + q]);
+  }
+  for (int off = 32; off; off >>= 1) a += __shfl_xor(a, off);
+  if (lane == 0) out[lt] = (float)(a * (double)max(p.spp, 1));
+}
+
 }  // namespace
+
+int sched_launch_tile_work(const SchedParams& p, float* tile_work, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (p.local <= 0) return hipSuccess;
+  const unsigned n = (unsigned)(((size_t)p.local * 1024 + 255) / 256);
+  hipLaunchKernelGGL(sched_est, dim3(n), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(sched_tile_work, dim3(p.local), dim3(64), 0, s, p, tile_work);
+  return (int)hipGetLastError();
+}
 
 size_t sched_scratch_bytes(int local) {
   // pixmask (2 u64 / pixel) | est (f32 / pixel) | pilot blocks (16 / tile) | hist | cursor | totals

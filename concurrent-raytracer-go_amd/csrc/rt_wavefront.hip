@@ -41,7 +41,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
 #include <mutex>
+#include <tuple>
 
 #include "../../include/rt_rng.h"
 #include "rt_device.h"
@@ -164,13 +166,21 @@ __device__ __forceinline__ size_t dense_at(const Dense& d, int j, size_t cap) {
   return (size_t)s * cap + (size_t)(j - off);
 }
 
+// (soft: the soft-shadow traversal kernel also adds its counts to the
+// rt_counts.soft_occlusion slots, for its own roofline; there the shadow-ray
+// slot counts the rays it traced, kept in c.v[kSoftJobs] -- softgen counts
+// them for the totals)
+constexpr int kSoftJobs = C_SHADOW;
 template <bool kCount>
-__device__ __forceinline__ void flush_counts(const WfParams& p, Counters& c) {
+__device__ __forceinline__ void flush_counts(const WfParams& p, Counters& c, bool soft = false) {
   if constexpr (kCount) {
-    for (int i = 0; i < 9; ++i) {
+    for (int i = 0; i < kCounters; ++i) {
       unsigned long long v = c.v[i];
       for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-      if ((threadIdx.x & 63) == 0 && v) atomicAdd(&p.counts[i], v);
+      if ((threadIdx.x & 63) == 0 && v) {
+        if (!(soft && i == kSoftJobs)) atomicAdd(&p.counts[i], v);
+        if (soft) atomicAdd(&p.counts[2 * kCounters + i], v);
+      }
     }
   }
 }
@@ -601,6 +611,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
         else
           e = make_uint4(p.hardq[at], 0, 0, 0);
         key = e.x;
+        if constexpr (kCount && kSoft) ++c.v[kSoftJobs];  // (flushed to the soft-occlusion slots only)
         const uint32_t slot = key / (uint32_t)p.nl, li = key - slot * (uint32_t)p.nl;
         o = mk(p.px[slot], p.py[slot], p.pz[slot]);
         d3 ldir;
@@ -653,7 +664,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
       if (blocked || cur == -1) busy = false;
     }
   }
-  flush_counts<kCount>(p, c);
+  flush_counts<kCount>(p, c, kSoft);
 }
 
 // ---------------------------------------------------------------- softgen
@@ -880,7 +891,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_regen(const WfParams p) {
       const uint32_t lp = p.lp0 + q;
       const int smp = (int)(sid - q * (uint32_t)p.spp);
       const int lt = (int)(lp >> 10), tp = (int)(lp & 1023);
-      const int tile = p.rank + lt * p.world;
+      const int tile = p.tile_list ? p.tile_list[lt] : p.rank + lt * p.world;
       const int x = (tile % p.tiles_x) * 32 + (tp & 31), y = (tile / p.tiles_x) * 32 + (tp >> 5);
       const size_t slot = (size_t)s * p.shard_cap + local;
       if (tile >= p.ntiles || x >= p.W || y >= p.H) {
@@ -931,7 +942,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_resolve(const WfParams p, int npi
   if (q >= npix) return;
   const uint32_t lp = p.lp0 + (uint32_t)q;
   const int lt = (int)(lp >> 10), tp = (int)(lp & 1023);
-  const int tile = p.rank + lt * p.world;
+  const int tile = p.tile_list ? p.tile_list[lt] : p.rank + lt * p.world;
   const int x = (tile % p.tiles_x) * 32 + (tp & 31), y = (tile / p.tiles_x) * 32 + (tp >> 5);
   if (tile >= p.ntiles || x >= p.W || y >= p.H) return;
   const double* r = p.rad + (size_t)q * p.spp * 3;
@@ -959,8 +970,11 @@ static int resident_grid(K kernel, int block, size_t shmem) {
   int dev = 0, cus = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 256;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 256;
+  // (the attribute is a permission: set to the whole LDS once, it never has
+  // to change, so renderers of other scene shapes on the same device cannot
+  // lower it under a launch of this one)
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)shmem);
+                            kLdsBytes);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, shmem) != hipSuccess || per < 1) per = 1;
   return cus * per;
 }
@@ -978,12 +992,19 @@ int wf_lds_nodes(int stack_depth, int nodes, int block, int wgs_per_cu) {
   return (int)(room % 2 ? room : room - 1);
 }
 
+// (prof: events recorded at the kernel boundaries of a profiled context,
+// rt_context_profile; ev[k] opens kernel class k, ev[k + 1] closes it)
+static inline void mark(const hipEvent_t* ev, int k, hipStream_t st) {
+  if (ev) (void)hipEventRecord(ev[k], st);
+}
+
 template <bool kCount>
-static int enqueue_regen_book(const WfParams& p, hipStream_t st) {
+static int enqueue_regen_book(const WfParams& p, hipStream_t st, const hipEvent_t* ev) {
   const int slots = kWfShards * p.shard_cap;
   // (once every sample has started, regen has nothing to do)
   if (!p.dry) hipLaunchKernelGGL((wf_regen<kCount>), dim3((slots + kWfBlock - 1) / kWfBlock), dim3(kWfBlock), 0, st, p);
   hipLaunchKernelGGL(wf_book, dim3(1), dim3(64), 0, st, p);
+  mark(ev, kWfRegen + 1, st);
   return (int)hipGetLastError();
 }
 
@@ -992,29 +1013,29 @@ template <bool kCount, bool kFull>
 static void enqueue_trav(const WfParams& p, hipStream_t st, int which) {
   const dim3 bt(p.trav_block);
   const size_t sh = trav_shmem(p);
-  // resident grids (and the LDS attribute) per device: an rt_renderer drives
-  // its devices from one thread each (rt_multi.cpp)
+  // resident grids per (device, LDS bytes, workgroup size): an rt_renderer
+  // drives its devices from one thread each (rt_multi.cpp), and contexts of
+  // different scenes may share a device
   struct Grids {
-    int ext = 0, occ_h = 0, occ_s = 0, block = 0;
-    size_t sh = 0;
+    int ext = 0, occ_h = 0, occ_s = 0;
   };
-  constexpr int kDevs = 64;
   static std::mutex mu;
-  static Grids cache[kDevs];
+  static std::map<std::tuple<int, size_t, int>, Grids> cache;
   int dev = 0;
   (void)hipGetDevice(&dev);
   Grids g;
   {
     std::lock_guard<std::mutex> lock(mu);
-    Grids& c = cache[dev % kDevs];
-    if (c.sh != sh || c.block != p.trav_block || !c.ext) {
+    const auto key = std::make_tuple(dev, sh, p.trav_block);
+    auto it = cache.find(key);
+    if (it == cache.end()) {
+      Grids c;
       c.ext = resident_grid(wf_extend<kCount, kFull>, p.trav_block, sh);
       c.occ_h = resident_grid(wf_occlude<kCount, false, kFull>, p.trav_block, sh);
       c.occ_s = resident_grid(wf_occlude<kCount, true, kFull>, p.trav_block, sh);
-      c.sh = sh;
-      c.block = p.trav_block;
+      it = cache.emplace(key, c).first;
     }
-    g = c;
+    g = it->second;
   }
   if (which == 0) hipLaunchKernelGGL((wf_extend<kCount, kFull>), dim3(g.ext), bt, sh, st, p);
   if (which == 1) hipLaunchKernelGGL((wf_occlude<kCount, false, kFull>), dim3(g.occ_h), bt, sh, st, p);
@@ -1022,7 +1043,7 @@ static void enqueue_trav(const WfParams& p, hipStream_t st, int which) {
 }
 
 template <bool kCount>
-static int enqueue_bounce(const WfParams& p, hipStream_t st) {
+static int enqueue_bounce(const WfParams& p, hipStream_t st, const hipEvent_t* ev) {
   const dim3 b(kWfBlock);
   // dense kernels: one thread per live path, at most one per slot; while the
   // last paths drain, the host's bound keeps tens of thousands of empty
@@ -1036,24 +1057,31 @@ static int enqueue_bounce(const WfParams& p, hipStream_t st) {
     else
       enqueue_trav<kCount, false>(p, st, which);
   };
+  mark(ev, kWfExtend, st);
   trav(0);
+  mark(ev, kWfShade1, st);
   hipLaunchKernelGGL((wf_shade1<kCount>), gd, b, 0, st, p);
-  if (p.nl > 0) {
-    trav(1);
-    if (p.soft) {
-      hipLaunchKernelGGL((wf_softgen<kCount>), gd, b, 0, st, p);
-      trav(2);
-    }
-  }
+  mark(ev, kWfHard, st);
+  if (p.nl > 0) trav(1);
+  mark(ev, kWfSoftgen, st);
+  if (p.nl > 0 && p.soft) hipLaunchKernelGGL((wf_softgen<kCount>), gd, b, 0, st, p);
+  mark(ev, kWfSoft, st);
+  if (p.nl > 0 && p.soft) trav(2);
+  mark(ev, kWfShade, st);
   hipLaunchKernelGGL((wf_shade<kCount>), gd, b, 0, st, p);
-  return enqueue_regen_book<kCount>(p, st);
+  mark(ev, kWfRegen, st);
+  return enqueue_regen_book<kCount>(p, st, ev);
 }
 
 // first == true: the arrays are empty; only regen + book (the first samples)
-int wf_launch_bounce(const WfParams& p, bool first, bool count, void* stream) {
+int wf_launch_bounce(const WfParams& p, bool first, bool count, void* stream, const void* prof) {
   hipStream_t st = (hipStream_t)stream;
-  if (first) return count ? enqueue_regen_book<true>(p, st) : enqueue_regen_book<false>(p, st);
-  return count ? enqueue_bounce<true>(p, st) : enqueue_bounce<false>(p, st);
+  const hipEvent_t* ev = (const hipEvent_t*)prof;
+  if (first) {
+    mark(ev, kWfRegen, st);
+    return count ? enqueue_regen_book<true>(p, st, ev) : enqueue_regen_book<false>(p, st, ev);
+  }
+  return count ? enqueue_bounce<true>(p, st, ev) : enqueue_bounce<false>(p, st, ev);
 }
 
 int wf_launch_resolve(const WfParams& p, int npix, void* stream) {

@@ -10,6 +10,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <atomic>
 #include <numeric>
 #include <vector>
 
@@ -17,7 +18,13 @@
 
 namespace rtgo {
 
-void tile_cost(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
+void strided_tiles(int32_t W, int32_t H, int32_t rank, int32_t world, std::vector<int32_t>* tiles) {
+  tiles->clear();
+  const int ntiles = rt_num_tiles(W, H);
+  for (int t = rank; t < ntiles; t += world) tiles->push_back(t);
+}
+
+void tile_cost(const FlatScene& fs, int32_t W, int32_t H, const std::vector<int32_t>& tiles,
                std::vector<float>* local_cost) {
   const int tiles_x = (W + 31) / 32, tiles_y = (H + 31) / 32, ntiles = tiles_x * tiles_y;
   std::vector<float> cost(ntiles, 0.0f);
@@ -51,7 +58,7 @@ void tile_cost(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t 
   for (const DTri& t : fs.tris) add_sphere(t.bc, t.br);
 
   local_cost->clear();
-  for (int t = rank; t < ntiles; t += world) local_cost->push_back(cost[t]);
+  for (int32_t t : tiles) local_cost->push_back(cost[t]);
 }
 
 // Does the cone (apex, unit axis, cos/sin of its half-angle) meet the sphere
@@ -110,13 +117,13 @@ static void cone_masks(const FlatScene& fs, const double axis[3], double cmin, d
 
 static unsigned long long low_bits(int n) { return n >= 64 ? ~0ull : (1ull << n) - 1ull; }
 
-void tile_primary_masks(const FlatScene& fs, int32_t W, int32_t H, int32_t rank, int32_t world,
+void tile_primary_masks(const FlatScene& fs, int32_t W, int32_t H, const std::vector<int32_t>& tiles,
                         std::vector<unsigned long long>* masks) {
   masks->clear();
-  const int tiles_x = (W + 31) / 32, tiles_y = (H + 31) / 32, ntiles = tiles_x * tiles_y;
+  const int tiles_x = (W + 31) / 32;
   const int ns = (int)fs.spheres.size(), nt = (int)fs.tris.size();
   const double vw = 2.0 * fs.aspect;
-  for (int t = rank; t < ntiles; t += world) {
+  for (int32_t t : tiles) {
     const int tx = t % tiles_x, ty = t / tiles_x;
     double axis[3], cmin, smax;
     rect_cone(vw, W, H, tx * 32, std::min(tx * 32 + 32, (int)W), ty * 32, std::min(ty * 32 + 32, (int)H), axis, &cmin,
@@ -126,6 +133,50 @@ void tile_primary_masks(const FlatScene& fs, int32_t W, int32_t H, int32_t rank,
     masks->push_back(ms);
     masks->push_back(mt);
   }
+}
+
+// ------------------------------------------------------------ partitions
+void finish_partition(PartitionData* d) {
+  static std::atomic<uint64_t> next_id{1};
+  const int ntiles = (int)d->owner.size();
+  d->offsets.assign(d->world + 1, 0);
+  for (int t = 0; t < ntiles; ++t) d->offsets[d->owner[t] + 1] += 1;
+  d->max_local = 0;
+  for (int r = 0; r < d->world; ++r) {
+    d->max_local = std::max(d->max_local, d->offsets[r + 1]);
+    d->offsets[r + 1] += d->offsets[r];
+  }
+  d->lists.assign(ntiles, 0);
+  d->local.assign(ntiles, 0);
+  std::vector<int32_t> fill(d->offsets.begin(), d->offsets.end() - 1);
+  for (int t = 0; t < ntiles; ++t) {  // ascending within each rank
+    const int r = d->owner[t];
+    d->local[t] = fill[r] - d->offsets[r];
+    d->lists[fill[r]++] = t;
+  }
+  d->id = next_id.fetch_add(1);
+}
+
+// Longest processing time first: tiles by decreasing estimated work (ties:
+// the lower tile first) to the least loaded rank (ties: the lower rank).
+// Each tile weighs its estimate + 1: tiles with no estimated work still cost
+// a launch slot, and spread evenly instead of piling onto one rank.
+void lpt_partition(const std::vector<float>& work, PartitionData* d) {
+  const int ntiles = (int)work.size(), world = d->world;
+  d->owner.assign(ntiles, 0);
+  std::vector<int32_t> order(ntiles);
+  std::iota(order.begin(), order.end(), 0);
+  auto wt = [&](int t) { return (double)work[t] + 1.0; };
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return wt(a) > wt(b); });
+  d->work.assign(world, 0.0);
+  for (int t : order) {
+    int r = 0;
+    for (int k = 1; k < world; ++k)
+      if (d->work[k] < d->work[r]) r = k;
+    d->owner[t] = r;
+    d->work[r] += wt(t);
+  }
+  finish_partition(d);
 }
 
 }  // namespace rtgo

@@ -40,8 +40,11 @@ MATERIAL_KINDS = {
 }
 RT_LAYOUT_IMAGE, RT_LAYOUT_PACKED_TILES = 0, 1
 RT_PATH_AUTO, RT_PATH_MEGAKERNEL = 0, 1
+RT_PARTITION_AUTO, RT_PARTITION_STRIDED, RT_PARTITION_BALANCED = 0, 1, 2
 SKIES = {"none": 0, "default": 1, "white": 2, "sunset": 3, "night": 4}  # RT_SKY_*
 RT_COMM_ID_BYTES = 128
+# wavefront kernel classes (RT_WF_*, rt_context_kernel_seconds)
+WF_KERNELS = ["extend", "shade1", "occlude_hard", "softgen", "occlude_soft", "shade", "regen", "resolve"]
 
 
 class RenderError(RuntimeError):
@@ -139,6 +142,8 @@ class Tuning(ctypes.Structure):
         ("split_samples", ctypes.c_int32),
         ("measure", ctypes.c_int32),
         ("split_depth", ctypes.c_int32),
+        ("partition", ctypes.c_int32),
+        ("_pad", ctypes.c_int32),
     ]
 
 
@@ -167,10 +172,24 @@ COUNT_FIELDS = [
 
 
 class Counts(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_uint64) for n in COUNT_FIELDS]
+    _fields_ = [(n, ctypes.c_uint64) for n in COUNT_FIELDS] + [("culled", ctypes.c_uint64 * 9),
+                                                               ("soft_occlusion", ctypes.c_uint64 * 9)]
 
     def as_dict(self):
+        """The nine counts (the reference's: every camera sample walked)."""
         return {n: int(getattr(self, n)) for n in COUNT_FIELDS}
+
+    def culled_dict(self):
+        """The part of each count the product never executes (culled pixels' camera samples)."""
+        return {n: int(self.culled[i]) for i, n in enumerate(COUNT_FIELDS)}
+
+    def soft_occlusion_dict(self):
+        """The wavefront soft-shadow traversal kernel's share of the counts."""
+        return {n: int(self.soft_occlusion[i]) for i, n in enumerate(COUNT_FIELDS)}
+
+    def executed_dict(self):
+        """Executed work: count - culled."""
+        return {n: int(getattr(self, n)) - int(self.culled[i]) for i, n in enumerate(COUNT_FIELDS)}
 
 
 # the symbols include/rt_api.h declares (checked by tests/test_abi.py)
@@ -211,6 +230,23 @@ EXPORTED_SYMBOLS = [
     "rt_tonemap_rgba",
     "rt_write_png",
     "rt_write_ppm",
+    "rt_partition_create",
+    "rt_partition_balanced",
+    "rt_partition_destroy",
+    "rt_partition_world",
+    "rt_partition_owner",
+    "rt_partition_local_tiles",
+    "rt_partition_tile",
+    "rt_partition_max_local",
+    "rt_partition_packed_bytes",
+    "rt_partition_rgba_offset",
+    "rt_partition_work",
+    "rt_context_set_partition",
+    "rt_unpack_partition_async",
+    "rt_comm_gather_bytes_async",
+    "rt_renderer_rank_seconds",
+    "rt_context_profile",
+    "rt_context_kernel_seconds",
 ]
 
 _lib = None
@@ -283,6 +319,24 @@ def lib():
         "rt_tonemap_rgba": (None, [vp, i32, vp]),
         "rt_write_png": (ctypes.c_int, [ctypes.c_char_p, vp, i32, i32]),
         "rt_write_ppm": (ctypes.c_int, [ctypes.c_char_p, vp, i32, i32]),
+        "rt_partition_create": (ctypes.c_int, [i32, i32, i32, ctypes.POINTER(i32), ctypes.POINTER(vp)]),
+        "rt_partition_balanced": (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(Settings), i32, ctypes.POINTER(vp)]),
+        "rt_partition_destroy": (None, [vp]),
+        "rt_partition_world": (i32, [vp]),
+        "rt_partition_owner": (i32, [vp, i32]),
+        "rt_partition_local_tiles": (i32, [vp, i32]),
+        "rt_partition_tile": (i32, [vp, i32, i32]),
+        "rt_partition_max_local": (i32, [vp]),
+        "rt_partition_packed_bytes": (sz, [vp]),
+        "rt_partition_rgba_offset": (sz, [vp]),
+        "rt_partition_work": (ctypes.c_double, [vp, i32]),
+        "rt_context_set_partition": (ctypes.c_int, [vp, vp]),
+        "rt_unpack_partition_async": (ctypes.c_int, [vp, vp, vp, vp, vp]),
+        "rt_comm_gather_bytes_async": (ctypes.c_int, [vp, sz, vp, vp, vp]),
+        "rt_renderer_rank_seconds": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
+        "rt_context_profile": (ctypes.c_int, [vp, i32]),
+        "rt_context_kernel_seconds": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
+                                                     ctypes.POINTER(ctypes.c_int64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -539,6 +593,13 @@ class ParallelRenderer:
         }
         return rgba
 
+    def rank_seconds(self) -> list:
+        """Device seconds of each rank's render launches in the last render (load balance)."""
+        n = max(1, len(self.devices) if self.devices else self.settings.num_devices)
+        out = (ctypes.c_double * n)()
+        _check(lib().rt_renderer_rank_seconds(self._renderer(), out))
+        return list(out)
+
     def save_image(self, img: np.ndarray, filename: str):
         """SaveImage (renderer.go:438-451); '.ppm' writes a P3 PPM."""
         img = np.ascontiguousarray(img, dtype=np.uint8)
@@ -580,7 +641,9 @@ class Context:
         )
 
     def count(self, width, height, settings: Settings, d_linear: int, d_rgba: int, stream: int = 0,
-              rank: int = 0, world: int = 1, layout: int = RT_LAYOUT_IMAGE) -> dict:
+              rank: int = 0, world: int = 1, layout: int = RT_LAYOUT_IMAGE, full: bool = False):
+        """The counting variant: the reference's nine counts (dict); full=True
+        returns the Counts struct (with the culled part, Counts.culled_dict)."""
         c = Counts()
         _check(
             lib().rt_context_render_async(
@@ -588,10 +651,32 @@ class Context:
                 ctypes.c_void_p(d_linear), ctypes.c_void_p(d_rgba), ctypes.c_void_p(stream), ctypes.byref(c),
             )
         )
-        return c.as_dict()
+        return c if full else c.as_dict()
+
+    def set_partition(self, partition):
+        """Render the tiles of `partition` (a Partition, or None: strided)."""
+        self._partition = partition  # (copied by the library; kept for symmetry)
+        _check(lib().rt_context_set_partition(self._h, partition._h if partition is not None else None))
+
+    def balanced_partition(self, width, height, settings: Settings, world: int) -> "Partition":
+        """rt_partition_balanced: a pilot-estimated, work-balanced tile partition."""
+        h = ctypes.c_void_p()
+        _check(lib().rt_partition_balanced(self._h, width, height, ctypes.byref(settings), world, ctypes.byref(h)))
+        return Partition(_handle=h)
 
     def set_debug_buffer(self, d_buf: int):
         _check(lib().rt_context_set_debug_buffer(self._h, ctypes.c_void_p(d_buf)))
+
+    def profile(self, on: bool = True):
+        """Per-kernel HIP-event timing of the wavefront path (resets the totals)."""
+        _check(lib().rt_context_profile(self._h, 1 if on else 0))
+
+    def kernel_seconds(self) -> dict:
+        """{kernel class: (total seconds, launches)} since profile(True)."""
+        s = (ctypes.c_double * len(WF_KERNELS))()
+        n = (ctypes.c_int64 * len(WF_KERNELS))()
+        _check(lib().rt_context_kernel_seconds(self._h, s, n))
+        return {k: (s[i], int(n[i])) for i, k in enumerate(WF_KERNELS)}
 
     def last_kernel_seconds(self) -> float:
         s = ctypes.c_double()
@@ -651,6 +736,67 @@ def unpack_tiles_async(width, height, world, d_gathered, d_linear, d_rgba, strea
     )
 
 
+class Partition:
+    """rt_partition: which rank renders each 32x32 tile (include/rt_api.h)."""
+
+    def __init__(self, width=0, height=0, world=1, owner=None, _handle=None):
+        if _handle is not None:
+            self._h = _handle
+            return
+        self._h = ctypes.c_void_p()
+        arr = None
+        if owner is not None:
+            owner = list(owner)
+            arr = (ctypes.c_int32 * len(owner))(*owner)
+        _check(lib().rt_partition_create(width, height, world, arr, ctypes.byref(self._h)))
+
+    @property
+    def world(self) -> int:
+        return lib().rt_partition_world(self._h)
+
+    def owner(self, tile: int) -> int:
+        return lib().rt_partition_owner(self._h, tile)
+
+    def owners(self, width: int, height: int) -> np.ndarray:
+        return np.array([self.owner(t) for t in range(num_tiles(width, height))], np.int32)
+
+    def local_tiles(self, rank: int) -> int:
+        return lib().rt_partition_local_tiles(self._h, rank)
+
+    def tiles(self, rank: int) -> list:
+        return [lib().rt_partition_tile(self._h, rank, k) for k in range(self.local_tiles(rank))]
+
+    @property
+    def max_local(self) -> int:
+        return lib().rt_partition_max_local(self._h)
+
+    @property
+    def packed_bytes(self) -> int:
+        return lib().rt_partition_packed_bytes(self._h)
+
+    @property
+    def rgba_offset(self) -> int:
+        return lib().rt_partition_rgba_offset(self._h)
+
+    def work(self, rank: int) -> float:
+        return lib().rt_partition_work(self._h, rank)
+
+    def unpack_async(self, d_gathered, d_linear, d_rgba, stream=0):
+        _check(lib().rt_unpack_partition_async(self._h, ctypes.c_void_p(d_gathered), ctypes.c_void_p(d_linear),
+                                               ctypes.c_void_p(d_rgba), ctypes.c_void_p(stream)))
+
+    def close(self):
+        if self._h and _lib is not None:
+            _lib.rt_partition_destroy(self._h)
+        self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Comm:
     """rt_comm: the RCCL communicator of one process per GPU (rank 0 makes
     the id with ``unique_id()``; the caller broadcasts it)."""
@@ -665,6 +811,10 @@ class Comm:
         buf = (ctypes.c_uint8 * RT_COMM_ID_BYTES)(*uid)
         self._h = ctypes.c_void_p()
         _check(lib().rt_comm_create(buf, world, rank, device, ctypes.byref(self._h)))
+
+    def gather_bytes_async(self, share_bytes, d_share, d_gathered, stream=0):
+        _check(lib().rt_comm_gather_bytes_async(self._h, share_bytes, ctypes.c_void_p(d_share),
+                                                ctypes.c_void_p(d_gathered), ctypes.c_void_p(stream)))
 
     def gather_tiles_async(self, width, height, d_share, d_gathered, stream=0):
         _check(lib().rt_comm_gather_tiles_async(self._h, width, height, ctypes.c_void_p(d_share),

@@ -28,15 +28,26 @@ import numpy as np
 from . import max_local_tiles, num_tiles, packed_bytes, packed_rgba_offset
 
 
-def packed_index(width: int, height: int, rank: int, world: int) -> np.ndarray:
+def rank_tiles(width: int, height: int, rank: int, world: int, owner=None) -> list:
+    """The tiles of `rank` in local-tile order: t % world == rank, or, with a
+    partition's owner array (owner[t] = rank of tile t), its tiles ascending."""
+    if owner is None:
+        return list(range(rank, num_tiles(width, height), world))
+    return [t for t in range(num_tiles(width, height)) if owner[t] == rank]
+
+
+def packed_index(width: int, height: int, rank: int, world: int, owner=None) -> np.ndarray:
     """Image pixel index (y*W + x) of every packed slot of `rank`, -1 where
     the slot is padding (a missing tile or a clipped edge pixel)."""
-    ml = max_local_tiles(width, height, world)
+    if owner is None:
+        ml = max_local_tiles(width, height, world)
+    else:
+        ml = max(len(rank_tiles(width, height, r, world, owner)) for r in range(world))
     idx = np.full(ml * 1024, -1, np.int64)
     tiles_x = (width + 31) // 32
     p = np.arange(1024)
     px, py = p % 32, p // 32
-    for lt, t in enumerate(range(rank, num_tiles(width, height), world)):
+    for lt, t in enumerate(rank_tiles(width, height, rank, world, owner)):
         x = (t % tiles_x) * 32 + px
         y = (t // tiles_x) * 32 + py
         ok = (x < width) & (y < height)
@@ -59,15 +70,19 @@ def pack_share_host(lin: np.ndarray, rgba: np.ndarray, rank: int, world: int) ->
     return out
 
 
-def unpack_shares_host(gathered: np.ndarray, width: int, height: int, world: int):
+def unpack_shares_host(gathered: np.ndarray, width: int, height: int, world: int, owner=None):
     """(world * packed_bytes,) uint8 gathered shares -> ((H, W, 3) f32, (H, W, 4) u8)."""
-    share = packed_bytes(width, height, world)
-    off = packed_rgba_offset(width, height, world)
+    if owner is None:
+        share = packed_bytes(width, height, world)
+        off = packed_rgba_offset(width, height, world)
+    else:
+        ml = max(len(rank_tiles(width, height, r, world, owner)) for r in range(world))
+        share, off = ml * 1024 * 16, ml * 1024 * 12
     lin = np.zeros((height * width, 3), np.float32)
     rgba = np.zeros((height * width, 4), np.uint8)
     for r in range(world):
         part = gathered[r * share:(r + 1) * share]
-        idx = packed_index(width, height, r, world)
+        idx = packed_index(width, height, r, world, owner)
         ok = idx >= 0
         lin[idx[ok]] = part[:off].view(np.float32).reshape(-1, 3)[ok]
         rgba[idx[ok]] = part[off:].reshape(-1, 4)[ok]

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* status codes */
 #define RT_OK 0
@@ -163,6 +163,18 @@ typedef struct {
   uint64_t shade_events;     /* surface hits shaded (direct lighting + scatter) */
   uint64_t light_evals;      /* per-light direct-lighting evaluations */
   uint64_t rng_draws;        /* uniform draws */
+  /* The part of the nine counts above that the product never executes: the
+   * counting variant walks every camera sample so that its counts are the
+   * reference's (tracePixel traces them all, renderer.go:150-163), but the
+   * product skips the samples of pixels whose camera rays provably miss
+   * everything (primary-ray culling).  Executed work =
+   * count - culled, in the same order (camera_rays .. rng_draws). */
+  uint64_t culled[9];
+  /* The wavefront path's soft-shadow traversal kernel alone (wf_occlude<soft>,
+   * calculateSmartShadow's 16 jittered rays, renderer.go:311-327): its share
+   * of the counts, for that kernel's own roofline (shadow_rays: the rays it
+   * traced).  Zero on the megakernel. */
+  uint64_t soft_occlusion[9];
 } rt_counts;
 
 void rt_settings_default(rt_settings* s);
@@ -268,7 +280,13 @@ typedef struct {
   int32_t measure;        /* 1: the first frame of a schedule measures every pixel's path lengths and the
                              next frame re-cuts the blocks from them; 0: pilot schedule only (default) */
   int32_t split_depth;    /* measured schedules split a pixel with a path of more bounces than this; 0: 16 */
+  int32_t partition;      /* rt_renderer with N > 1 ranks: RT_PARTITION_*; 0: auto (balanced for linear-scan
+                             scenes, strided for BVH scenes, whose frames have thousands of busy tiles) */
+  int32_t _pad;
 } rt_tuning;
+#define RT_PARTITION_AUTO 0
+#define RT_PARTITION_STRIDED 1
+#define RT_PARTITION_BALANCED 2
 void rt_tuning_default(rt_tuning* t);
 /* Applies to later rt_context_set_scene (BVH shape) and render calls. */
 int rt_context_set_tuning(rt_context* ctx, const rt_tuning* t);
@@ -324,12 +342,77 @@ void rt_comm_destroy(rt_comm* comm);
 int rt_comm_gather_tiles_async(rt_comm* comm, int32_t width, int32_t height, const void* d_share, void* d_gathered,
                                void* hip_stream);
 
+/* ------------------------------------------------ tile partitions (N ranks) */
+
+/* createRenderTasks hands 32x32 tiles to the goroutines through one channel
+ * (renderer.go:398-436), so a slow tile never holds the others up.  Ranks on
+ * separate GPUs share no queue: each renders a fixed set of tiles.  The
+ * default set is strided (t % world == rank).  A frame whose work sits in a
+ * few tiles (the headline scene: 23 of its 475 tiles hold all the shading)
+ * is better dealt by estimated work: rt_partition_balanced renders a
+ * one-sample pilot of the whole frame on ctx's device (the schedule's pilot,
+ * DESIGN.md §4.1), sums each tile's estimated path work and deals the tiles
+ * heaviest first to the least loaded rank.  The pilot is deterministic, so
+ * every rank that plans the same frame derives the same partition.  Every
+ * pixel stays on one rank and the random stream is keyed by global pixel and
+ * sample: the image is the same for every partition.
+ * A rank's packed share holds its tiles in ascending order (local tile lt =
+ * the lt-th of its tiles); every share is sized for the largest. */
+typedef struct rt_partition rt_partition;
+/* owner[t] = rank of tile t (rt_num_tiles entries, each in [0, world)); NULL: strided. */
+int rt_partition_create(int32_t width, int32_t height, int32_t world, const int32_t* owner, rt_partition** out);
+/* ctx must hold the scene (rt_context_set_scene); synchronous. */
+int rt_partition_balanced(rt_context* ctx, int32_t width, int32_t height, const rt_settings* settings, int32_t world,
+                          rt_partition** out);
+void rt_partition_destroy(rt_partition* p);
+int32_t rt_partition_world(const rt_partition* p);
+int32_t rt_partition_owner(const rt_partition* p, int32_t tile);      /* -1: no such tile */
+int32_t rt_partition_local_tiles(const rt_partition* p, int32_t rank); /* tiles of `rank` */
+int32_t rt_partition_tile(const rt_partition* p, int32_t rank, int32_t local); /* its local-th tile, -1: none */
+int32_t rt_partition_max_local(const rt_partition* p);
+size_t rt_partition_packed_bytes(const rt_partition* p);  /* one share: max_local * 1024 * 16 */
+size_t rt_partition_rgba_offset(const rt_partition* p);   /* max_local * 1024 * 12 */
+/* Estimated work of rank's tiles (pilot path bounces x samples; balanced partitions, else 0). */
+double rt_partition_work(const rt_partition* p, int32_t rank);
+/* Later renders of ctx with the partition's (W, H, world) render rank's tiles
+ * of it (packed: in its order); NULL (or other sizes): strided.  The
+ * partition is copied: it may be destroyed afterwards. */
+int rt_context_set_partition(rt_context* ctx, const rt_partition* p);
+/* rt_unpack_tiles_async for a partition's shares ([world][rt_partition_packed_bytes]). */
+int rt_unpack_partition_async(const rt_partition* p, const void* d_gathered, float* d_linear, uint8_t* d_rgba,
+                              void* hip_stream);
+/* rt_comm_gather_tiles_async with shares of share_bytes (a partition's packed bytes). */
+int rt_comm_gather_bytes_async(rt_comm* comm, size_t share_bytes, const void* d_share, void* d_gathered,
+                               void* hip_stream);
+/* Per rank of the renderer's last render: device seconds of its render launches
+ * (out[num_devices]) -- the load balance of a multi-GPU frame. */
+int rt_renderer_rank_seconds(const rt_renderer* r, double* out);
+
 /* Debug hook: a device buffer of 48 u64 per workgroup that
  * RT_WG_TIMING builds of the kernel fill: s_memrealtime at start / loop end
  * / end, then s_memtime clocks spent in closest hit, lighting and soft
  * shadows, coop/sequential soft-shadow counts and loop iterations
  * (scripts/wg_timing.py).  Product builds ignore it. */
 int rt_context_set_debug_buffer(rt_context* ctx, void* d_buf);
+
+/* Per-kernel device time of the wavefront path (BVH scenes):
+ * with profiling on, HIP events are recorded at every kernel boundary of the
+ * bounce loop on the render's stream; rt_context_kernel_seconds waits for
+ * them and returns each kernel class's total seconds and launches since
+ * profiling was switched on, in the order of RT_WF_*.  (The megakernel path
+ * records nothing here: rt_context_last_kernel_seconds is its one launch.) */
+#define RT_WF_EXTEND 0       /* closest hit of the live paths (hitWorld, renderer.go:333-346) */
+#define RT_WF_SHADE1 1       /* hit records + hard shadow rays queued */
+#define RT_WF_OCCLUDE_HARD 2 /* any-hit of the hard shadow rays (renderer.go:305) */
+#define RT_WF_SOFTGEN 3      /* the 16 jittered points per clear light (renderer.go:311-318) */
+#define RT_WF_OCCLUDE_SOFT 4 /* any-hit of the soft shadow rays (renderer.go:320) */
+#define RT_WF_SHADE 5        /* direct lighting + scatter (renderer.go:181-297) */
+#define RT_WF_REGEN 6        /* new camera samples + loop bookkeeping */
+#define RT_WF_RESOLVE 7      /* per-pixel in-order sums, tone map, write */
+#define RT_WF_KERNELS 8
+int rt_context_profile(rt_context* ctx, int32_t on);  /* on / off; resets the totals */
+int rt_context_kernel_seconds(rt_context* ctx, double* seconds /* RT_WF_KERNELS */,
+                              int64_t* launches /* RT_WF_KERNELS or NULL */);
 
 /* Device time (seconds) of the last render launch enqueued on this context
  * (HIP events recorded around it on its stream); waits for it. */

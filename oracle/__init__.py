@@ -19,6 +19,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
 
 _lib = None
+# Worker threads of a render without an explicit count: None = the affinity
+# count (Go's runtime.NumCPU()).  The test suite caps it (tests/conftest.py)
+# to stay inside a GPU box's CPU share; bench.py passes its count explicitly.
+DEFAULT_THREADS = None
 
 
 def _rtgo():
@@ -93,12 +97,15 @@ def render(scene, width, height, settings, rank=0, world=1, nthreads=None, max_t
     oracle_render_ex) -- the same image, not the reference's algorithm; its
     counts are not the reference's either."""
     rt = _rtgo()
+    if nthreads is None and DEFAULT_THREADS:
+        nthreads = DEFAULT_THREADS
     if nthreads is None:
-        # the CPUs this process may run on, at most 16 (a GPU box's share)
+        # the CPUs this process may run on: Go's runtime.NumCPU(), the worker
+        # count cmd/raytracer passes to NewParallelRenderer (main.go:46)
         try:
-            nthreads = min(16, len(os.sched_getaffinity(0)))
+            nthreads = len(os.sched_getaffinity(0))
         except AttributeError:
-            nthreads = min(16, os.cpu_count() or 1)
+            nthreads = os.cpu_count() or 1
     lin = np.full((height, width, 3), np.nan, np.float64)
     rgba = np.zeros((height, width, 4), np.uint8)
     c = rt.Counts()

@@ -44,12 +44,27 @@ static void exercise_scene(const rt_scene* s, const char* name) {
   flatten_scene(*s, &f);
   std::vector<unsigned long long> masks;
   std::vector<float> cost;
+  std::vector<int32_t> tiles;
   for (int world : {1, 3, 8}) {
     for (int rank = 0; rank < world; rank += 2) {
-      if (f.spheres.size() <= 64 && f.tris.size() <= 64) tile_primary_masks(f, 800, 600, rank, world, &masks);
-      tile_cost(f, 800, 600, rank, world, &cost);
-      tile_cost(f, 33, 17, rank, world, &cost);
+      strided_tiles(800, 600, rank, world, &tiles);
+      if (f.spheres.size() <= 64 && f.tris.size() <= 64) tile_primary_masks(f, 800, 600, tiles, &masks);
+      tile_cost(f, 800, 600, tiles, &cost);
+      strided_tiles(33, 17, rank, world, &tiles);
+      tile_cost(f, 33, 17, tiles, &cost);
     }
+    // a balanced partition of the frame from the projected-primitive costs
+    strided_tiles(800, 600, 0, 1, &tiles);
+    tile_cost(f, 800, 600, tiles, &cost);
+    PartitionData pd;
+    pd.w = 800;
+    pd.h = 600;
+    pd.world = world;
+    lpt_partition(cost, &pd);
+    CHECK((int)pd.lists.size() == rt_num_tiles(800, 600) && pd.offsets[world] == (int)pd.lists.size());
+    for (int r = 0; r < world; ++r)
+      for (int k = pd.offsets[r]; k < pd.offsets[r + 1]; ++k)
+        CHECK(pd.owner[pd.lists[k]] == r && pd.local[pd.lists[k]] == k - pd.offsets[r]);
   }
   if (f.tris.empty() && !f.spheres.empty()) {
     for (int leaf : {0, 1, 7})

@@ -22,6 +22,15 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
+    # oracle renders in the tests use at most 16 threads (a GPU box's CPU
+    # share); the oracle's own default is the affinity count (runtime.NumCPU())
+    import oracle
+
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    oracle.DEFAULT_THREADS = min(16, aff)
 
 
 @pytest.fixture(scope="session")
