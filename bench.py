@@ -15,16 +15,19 @@ workload: --config c2 (default, the headline): BASELINE configs[1],
           1920x1080x64), c5 (10k spheres 3840x2160x256: the 8-GPU config).
 step    : one render of a whole frame with the scene and output buffers
           resident in HBM; every step renders a DIFFERENT image (seed + i).
-          Frames are rendered with F frames in flight (--frames-in-flight;
-          default 2 for c2/c3 at one GPU, 8 per rank at N > 1): step i runs
-          on frame slot i % F (own context, stream and buffers), so a frame's
-          low-occupancy tail (its last 50-bounce paths)
-          overlaps the next frames.  The same frames are also timed one at a
-          time (the reference's synchronous Render): "one_frame_in_flight".
-          For N > 1 a step also includes the frame's one RCCL gather of the
-          ranks' packed shares to rank 0 (librtgo's ncclSend/ncclRecv group
-          over xGMI, on one gather stream per rank, in step order) and the
-          unpack kernel there.  The work schedule of a (scene, frame,
+          B consecutive steps (frames that differ only in their seed) form one
+          launch (rt_context_render_frames_async; --frames-per-launch, default
+          8 for c2/c3 at one GPU, 16 per rank at N > 1), and F launches are in
+          flight (--frames-in-flight; default 2 at one GPU, 3 at N > 1): launch
+          j runs on slot j % F (own context, stream and buffers), so a frame's
+          low-occupancy tail (its last 50-bounce paths) is
+          paid once per launch and overlaps the next launch's start.  The same
+          frames are also timed one at a time (the reference's synchronous
+          Render): "one_frame_in_flight".
+          For N > 1 a launch also includes its one RCCL gather of the ranks'
+          packed shares to rank 0 (librtgo's ncclSend/ncclRecv group over
+          xGMI, on one gather stream per rank, in step order) and the unpack
+          kernel there.  The work schedule of a (scene, frame,
           settings) key is built by the first frame and reused (seeds
           excluded from the key).
 scaling : STRONG by default: every N renders the config's frame (800x600x100
@@ -123,7 +126,14 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (default: the affinity count)")
     ap.add_argument("--frames-in-flight", type=int, default=0,
-                    help="frames rendered concurrently per rank (own context, stream and buffers each)")
+                    help="launches in flight per rank (own context, stream and buffers each)")
+    ap.add_argument("--frames-per-launch", type=int, default=0,
+                    help="frames of one launch (rt_context_render_frames_async, at most 16)")
+    ap.add_argument("--host-gather", action="store_true",
+                    help="TEST MODE (not a bench line): gather the shares over gloo host copies instead of RCCL, "
+                         "so N ranks can share one GPU (RCCL refuses two ranks on one device); --check compares "
+                         "rank 0's last image with a 1-rank render")
+    ap.add_argument("--check", action="store_true", help="compare the last frame with a 1-rank render (N > 1)")
     return ap.parse_args()
 
 
@@ -136,67 +146,107 @@ def load_scene(rtgo, spec):
 
 
 class Slot:
-    """One frame slot of this rank: its context (schedule), render stream and
-    buffers.  world 1: the W*H image.  world > 1: this rank's packed share of
-    the partition; rank 0 renders its share in place into its gather buffer
-    and unpacks the image there."""
+    """One launch slot of this rank: its context (schedule), render stream and
+    buffers for up to B frames per launch (rt_context_render_frames_async).
+    world 1: B W*H images.  world > 1: this rank's packed shares of the
+    partition, its B frames contiguous ([B][share]); rank 0 renders them in
+    place into its gather buffer [world][B][share] and unpacks the B images
+    there in one launch."""
 
-    def __init__(self, rtgo, torch, scene, w, h, rank, world, device, part):
-        self.rtgo, self.w, self.h, self.rank, self.world, self.part = rtgo, w, h, rank, world, part
+    def __init__(self, rtgo, torch, scene, w, h, rank, world, device, part, B):
+        self.rtgo, self.w, self.h, self.rank, self.world, self.part, self.B = rtgo, w, h, rank, world, part, B
         self.ctx = rtgo.Context(device)
         self.ctx.set_scene(scene)
         self.stream = torch.cuda.Stream(device)
         self.rendered = torch.cuda.Event()
-        self.gathered = None  # event: the share has been sent (and unpacked on rank 0)
+        self.gathered = None  # event: the shares have been sent (and unpacked on rank 0)
+        self.n = 0            # frames of the last launch
         dev = torch.device("cuda", device)
         if world == 1:
             self.layout = rtgo.RT_LAYOUT_IMAGE
-            self.lin = torch.zeros(w * h * 3, dtype=torch.float32, device=dev)
-            self.rgba = torch.zeros(w * h * 4, dtype=torch.uint8, device=dev)
-            self.p_lin, self.p_rgba = self.lin.data_ptr(), self.rgba.data_ptr()
+            self.lin = torch.zeros((B, w * h * 3), dtype=torch.float32, device=dev)
+            self.rgba = torch.zeros((B, w * h * 4), dtype=torch.uint8, device=dev)
+            self.p_lin = [self.lin[f].data_ptr() for f in range(B)]
+            self.p_rgba = [self.rgba[f].data_ptr() for f in range(B)]
             return
         self.ctx.set_partition(part)
         self.layout = rtgo.RT_LAYOUT_PACKED_TILES
         nb = part.packed_bytes
         self.share_bytes = nb
         if rank == 0:
-            self.gbuf = torch.zeros(world * nb, dtype=torch.uint8, device=dev)
-            self.share = self.gbuf[:nb]
-            self.img_lin = torch.zeros(w * h * 3, dtype=torch.float32, device=dev)
-            self.img_rgba = torch.zeros(w * h * 4, dtype=torch.uint8, device=dev)
+            self.gbuf = torch.zeros(world * B * nb, dtype=torch.uint8, device=dev)
+            self.share = self.gbuf[:B * nb]
+            self.img_lin = torch.zeros((B, w * h * 3), dtype=torch.float32, device=dev)
+            self.img_rgba = torch.zeros((B, w * h * 4), dtype=torch.uint8, device=dev)
         else:
             self.gbuf = None
-            self.share = torch.zeros(nb, dtype=torch.uint8, device=dev)
-        self.p_lin = self.share.data_ptr()
-        self.p_rgba = self.share.data_ptr() + part.rgba_offset
+            self.share = torch.zeros(B * nb, dtype=torch.uint8, device=dev)
+        base = self.share.data_ptr()
+        self.p_lin = [base + f * nb for f in range(B)]
+        self.p_rgba = [p + part.rgba_offset for p in self.p_lin]
 
-    def render(self, st):
-        if self.gathered is not None:  # the share buffer is free again once its last gather is done
+    def render(self, sts):
+        """One launch of the frames sts (<= B; they differ only in seed)."""
+        if self.gathered is not None:  # the buffers are free again once their last gather is done
             self.stream.wait_event(self.gathered)
-        self.ctx.render_async(self.w, self.h, st, self.p_lin, self.p_rgba, self.stream.cuda_stream, self.rank,
-                              self.world, self.layout)
+        n = self.n = len(sts)
+        self.ctx.render_frames_async(self.w, self.h, sts[0], [st.seed for st in sts], self.p_lin[:n],
+                                     self.p_rgba[:n], self.stream.cuda_stream, self.rank, self.world, self.layout)
 
     def gather(self, torch, comm, gstream):
-        """The frame's one collective (on the rank's gather stream, in step
-        order), then the unpack kernel on rank 0."""
+        """The launch's one collective (on the rank's gather stream, in step
+        order: each rank sends its n frames' shares, contiguous), then one
+        unpack kernel for the n images on rank 0."""
         if self.world == 1:
             return
         self.rendered.record(self.stream)
         gstream.wait_event(self.rendered)
         g = self.gbuf.data_ptr() if self.gbuf is not None else 0
-        comm.gather_bytes_async(self.share_bytes, self.share.data_ptr(), g, gstream.cuda_stream)
+        nbytes = self.n * self.share_bytes
+        if isinstance(comm, HostGather):
+            comm.gather(torch, self, gstream, nbytes)
+        else:
+            comm.gather_bytes_async(nbytes, self.share.data_ptr(), g, gstream.cuda_stream)
         if self.rank == 0:
-            self.part.unpack_async(g, self.img_lin.data_ptr(), self.img_rgba.data_ptr(), gstream.cuda_stream)
+            self.part.unpack_frames_async(self.n, g, self.img_lin.data_ptr(), self.img_rgba.data_ptr(),
+                                          gstream.cuda_stream)
         if self.gathered is None:
             self.gathered = torch.cuda.Event()
         self.gathered.record(gstream)
 
+    def image(self, f):
+        """(linear, rgba) device tensors of frame f of the last launch (rank 0)."""
+        if self.world == 1:
+            return self.lin[f], self.rgba[f]
+        return self.img_lin[f], self.img_rgba[f]
+
     def counts(self, st):
-        return self.ctx.count(self.w, self.h, st, self.p_lin, self.p_rgba, self.stream.cuda_stream, self.rank,
+        return self.ctx.count(self.w, self.h, st, self.p_lin[0], self.p_rgba[0], self.stream.cuda_stream, self.rank,
                               self.world, self.layout, full=True)
 
     def close(self):
         self.ctx.close()
+
+
+class HostGather:
+    """--host-gather (test mode): the same gather through torch.distributed
+    gloo and host copies, synchronous; lets N ranks share one GPU."""
+
+    def __init__(self, dist, rank, world):
+        self.dist, self.rank, self.world = dist, rank, world
+
+    def gather(self, torch, slot, gstream, nbytes):
+        with torch.cuda.stream(gstream):
+            host = slot.share[:nbytes].cpu()
+        parts = [torch.empty_like(host) for _ in range(self.world)] if self.rank == 0 else None
+        self.dist.gather(host, parts, dst=0)
+        if self.rank == 0:
+            with torch.cuda.stream(gstream):
+                for r in range(1, self.world):
+                    slot.gbuf[r * nbytes:(r + 1) * nbytes].copy_(parts[r].to(slot.gbuf.device))
+
+    def close(self):
+        pass
 
 
 def barrier_sync(torch, dist, world):
@@ -214,44 +264,49 @@ def max_over_ranks(torch, dist, world, x):
     return float(t.item())
 
 
-def time_steps(slots, torch, dist, world, sts, warmup, comm, gstream):
+def launches(sts, B):
+    """The K steps as launches of up to B consecutive frames."""
+    return [sts[i:i + B] for i in range(0, len(sts), B)]
+
+
+def time_steps(slots, torch, dist, world, sts, warmup, comm, gstream, B):
     """W untimed steps, then K = len(sts) timed steps (step i renders with
     settings sts[i]: its own seed) between barrier + synchronize on both
-    sides; step i runs slots[i % F].  Returns (max-over-ranks seconds,
-    per-launch kernel ms from HIP events recorded on the stream each render
-    runs on)."""
+    sides; B consecutive steps form one launch, launch j runs on
+    slots[j % F].  Returns (max-over-ranks seconds, per-frame kernel ms of
+    each launch from HIP events recorded on the stream it runs on)."""
     F = len(slots)
-    for i in range(warmup):
-        sl = slots[i % F]
-        sl.render(sts[i % len(sts)])
+    for j, batch in enumerate(launches([sts[i % len(sts)] for i in range(warmup)], B)):
+        sl = slots[j % F]
+        sl.render(batch)
         sl.gather(torch, comm, gstream)
     barrier_sync(torch, dist, world)
     evs = []
     t0 = time.perf_counter()
-    for i, st in enumerate(sts):
-        sl = slots[i % F]
+    for j, batch in enumerate(launches(sts, B)):
+        sl = slots[j % F]
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         if sl.gathered is not None:
             sl.stream.wait_event(sl.gathered)
         e0.record(sl.stream)
-        sl.render(st)
+        sl.render(batch)
         e1.record(sl.stream)
-        evs.append((e0, e1))
+        evs.append((e0, e1, len(batch)))
         sl.gather(torch, comm, gstream)
     barrier_sync(torch, dist, world)
     elapsed = max_over_ranks(torch, dist, world, time.perf_counter() - t0)
-    return elapsed, [a.elapsed_time(b) for a, b in evs]
+    return elapsed, [a.elapsed_time(b) / n for a, b, n in evs]
 
 
 def first_frame_ms(rtgo, torch, scene, W, H, st, local):
     """One frame on a fresh context (N = 1): it also builds what the timed
     steps reuse (frustum masks, the one-sample pilot render, block building
     and upload).  Wall clock."""
-    sl = Slot(rtgo, torch, scene, W, H, 0, 1, local, None)
+    sl = Slot(rtgo, torch, scene, W, H, 0, 1, local, None, 1)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    sl.render(st)
+    sl.render([st])
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3
     sl.close()
@@ -468,6 +523,11 @@ def plan_partition(rtgo, torch, dist, scene, W, H, st, rank, world, local, strid
 
 def main():
     args = parse()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        # a rank keeps several launches and its gather stream in flight: more
+        # hardware queues than HIP's default 4 let them run side by side
+        # (scripts/rank_share_probe.py); set before HIP starts
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
     import torch
     import torch.distributed as dist
 
@@ -480,6 +540,8 @@ def main():
         print(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes (WORLD_SIZE={world})",
               file=sys.stderr)
         sys.exit(2)
+    if args.host_gather:  # test mode: N ranks may share the box's GPUs
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
         # host-side coordination only (barriers, the max over ranks, the RCCL
@@ -502,28 +564,39 @@ def main():
         st.samples, st.max_depth, st.seed = args.spp, args.depth, args.seed + i
         st.num_workers = world
         sts.append(st)
-    if args.frames_in_flight:
-        F = args.frames_in_flight
-    elif world > 1 and cfg not in WAVEFRONT:
-        F = 8  # a rank's share is ~1/N of the frame's work but its longest path is the frame's
+    # F launches in flight of B frames each: a frame's launch ends with the
+    # lone chains of its longest paths; B frames in one launch
+    # pay that tail once, F launches overlap one launch's tail with the next's
+    # start.  A rank's share at N > 1 holds ~1/N of the frame's work but the
+    # frame's longest paths, so it needs more frames per launch
+    # (scripts/rank_share_probe.py).  BVH frames: one at a time.
+    if cfg in WAVEFRONT:
+        F, B = 1, 1
+    elif world > 1:
+        F, B = 3, 16
     else:
-        F = fif_default
+        F, B = fif_default, 8
+    F = args.frames_in_flight or F
+    B = max(1, min(16, args.frames_per_launch or B))
     scene = load_scene(rtgo, spec)
 
     comm = gstream = part = None
     part_kind = None
     if world > 1:
-        uid = [rtgo.Comm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = rtgo.Comm(uid[0], world, rank, local)
+        if args.host_gather:
+            comm = HostGather(dist, rank, world)
+        else:
+            uid = [rtgo.Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = rtgo.Comm(uid[0], world, rank, local)
         gstream = torch.cuda.Stream(local)
         part, part_kind = plan_partition(rtgo, torch, dist, scene, W, H, sts[0], rank, world, local,
                                          args.strided or cfg in WAVEFRONT)
 
     slots = []
-    for _ in range(F):  # F frames in flight: own context (schedule), stream and buffers each
-        sl = Slot(rtgo, torch, scene, W, H, rank, world, local, part)
-        sl.render(sts[0])  # set-up: builds this context's schedule (like the scene upload)
+    for _ in range(F):  # F launches in flight: own context (schedule), stream and buffers each
+        sl = Slot(rtgo, torch, scene, W, H, rank, world, local, part, B)
+        sl.render(sts[:B])  # set-up: builds this context's schedule (like the scene upload)
         sl.gather(torch, comm, gstream)
         slots.append(sl)
     barrier_sync(torch, dist, world)
@@ -532,15 +605,30 @@ def main():
     prof_ctx = slots[0].ctx if cfg in WAVEFRONT else None
     if prof_ctx is not None:
         prof_ctx.profile(True)  # per-kernel HIP events in the timed frames (F = 1: every frame on slot 0)
-    elapsed, kms = time_steps(slots, torch, dist, world, sts, args.warmup, comm, gstream)
+    elapsed, kms = time_steps(slots, torch, dist, world, sts, args.warmup, comm, gstream, B)
     kernel_prof = None
     if prof_ctx is not None:
         kernel_prof = prof_ctx.kernel_seconds()
         prof_ctx.profile(False)
     # the same frames one at a time (the reference's synchronous Render)
-    elapsed1, kms1 = (time_steps(slots[:1], torch, dist, world, sts, args.warmup, comm, gstream) if F > 1
-                      else (elapsed, kms))
+    elapsed1, kms1 = (time_steps(slots[:1], torch, dist, world, sts, args.warmup, comm, gstream, 1)
+                      if F * B > 1 else (elapsed, kms))
     first_ms = first_frame_ms(rtgo, torch, scene, W, H, sts[0], local) if world == 1 else None
+    check = None
+    if args.check and world > 1:
+        # the last timed frame (rank 0; slot 0 rendered it last, one frame at
+        # a time) against a 1-rank render of the same settings
+        torch.cuda.synchronize()
+        if rank == 0:
+            lin, rgba = slots[0].image(0)
+            ref = Slot(rtgo, torch, scene, W, H, 0, 1, local, None, 1)
+            ref.render([sts[-1]])
+            torch.cuda.synchronize()
+            check = bool(torch.equal(lin, ref.lin[0]) and torch.equal(rgba, ref.rgba[0]))
+            ref.close()
+        ok = [None] * world
+        dist.all_gather_object(ok, check)
+        check = ok[0]
     e2e = None
     if world == 1 and not args.no_e2e and cfg in ("c2", "c2_committed", "c3"):
         e2e = render_e2e(rtgo, scene, W, H, args, local)
@@ -592,7 +680,8 @@ def main():
         cpu_bvh = cpu_baseline_bvh(args, rtgo, scene, W, H, sts[0]) if cfg in WAVEFRONT else None
 
     if rank == 0:
-        parallelism = "1 GPU" if world == 1 else "%d ranks: tiles %s, one RCCL gather per frame" % (world, part_kind)
+        parallelism = "1 GPU" if world == 1 else "%d ranks: tiles %s, one %s gather per frame" % (
+            world, part_kind, "HOST (gloo, test mode: not a bench line)" if args.host_gather else "RCCL")
         out = {
             "metric": "Mrays/sec at 800x600x100spp max_depth=50 (sphere_reflections_light)" if cfg == "c2"
             else "Mrays/sec (%s)" % cfg,
@@ -603,7 +692,9 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / steps * 1e3, 4),
             "first_frame_ms": round(first_ms, 4) if first_ms is not None else None,
-            "frames_in_flight": F,
+            "frames_in_flight": F * B,
+            "launches_in_flight": F,
+            "frames_per_launch": B,
             "one_frame_in_flight": {
                 "value": round(rays * steps / elapsed1 / 1e6, 3),
                 "ms_per_step": round(elapsed1 / steps * 1e3, 4),
@@ -621,7 +712,8 @@ def main():
                 "workload": workload + ", soft shadows, recursive reflections",
                 "width": W, "height": H, "spp": args.spp, "max_depth": args.depth,
                 "parallelism": parallelism,
-                "frames_in_flight": F,
+                "frames_in_flight": F * B,
+                "frames_per_launch": B,
             },
             "roofline": {
                 "bound": "valu",
@@ -658,6 +750,7 @@ def main():
                 "algorithmic_bytes_per_launch": hbm_bytes,
             },
             "rank_kernel_ms": [round(x, 4) for x in rank_kernel_ms],
+            "check_equals_one_rank": check,
             "rank_estimated_work": [round(part.work(r)) for r in range(world)] if world > 1 else None,
             "counts_rank0": counts.as_dict(),
             "counts_rank0_executed": ex,

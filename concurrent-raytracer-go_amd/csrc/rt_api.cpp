@@ -125,6 +125,7 @@ struct rt_context {
   size_t d_blocks_cap = 0;  // bytes
   int32_t num_blocks = 0;
   int32_t nsplit = 0;       // split pixels of the current schedule
+  int32_t split_frames = 0; // frames whose copies of the split rows are laid out in d_split
   char* d_split = nullptr;  // their per-sample radiance rows + sub-block counters
   size_t split_cap = 0;
   void* d_acc = nullptr;  // sample passes: running per-pixel sums (KParams.acc)
@@ -572,7 +573,7 @@ static double default_block_work(const rt_context* c) {
 // primary-ray candidate masks apply (small linear-scan scenes)
 static bool masks_apply(const FlatScene& f) { return f.bvh.empty() && f.spheres.size() <= 64 && f.tris.size() <= 64; }
 
-static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hipStream_t s) {
+static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hipStream_t s, int frames = 1) {
   const FlatScene& f = c->flat;
   const int w = p->W, h = p->H, rank = p->rank, world = p->world;
   const rt_tuning& tn = c->tun;
@@ -601,6 +602,7 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
     const int local = (int)tiles.size();
     c->num_blocks = 0;
     c->nsplit = 0;
+    c->split_frames = 0;  // (the split rows are laid out again below)
     c->masks_host.clear();
     c->d_masks = nullptr;
     if (local > 0) {
@@ -653,14 +655,6 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
         set_error(std::string("schedule launch failed: ") + hipGetErrorString((hipError_t)e));
         return RT_E_DEVICE;
       }
-      const size_t need = (size_t)nsplit * st->samples * 3 * sizeof(double) + split_flags_bytes(nsplit, st->samples);
-      rc = grow(&c->d_split, &c->split_cap, need + 256);
-      if (rc) return rc;
-      // split pixels' hit bits and sub-block counters start at zero; each
-      // launch's last sub-block of a pixel zeroes them again (rt_kernel.hip)
-      if (nsplit)
-        HIP_TRY(hipMemsetAsync((char*)c->d_split + (size_t)nsplit * st->samples * 3 * sizeof(double), 0,
-                               split_flags_bytes(nsplit, st->samples), s));
       c->num_blocks = nblocks;
       c->nsplit = nsplit;
     }
@@ -670,12 +664,29 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
     // a new key's first frame measures (state 1), the next re-cuts (2 -> 3)
     c->meas_state = remeasured ? 3 : (tn.measure && local > 0 ? 1 : 0);
   }
+  // split pixels: one copy of their radiance rows, hit bits and sub-block
+  // counters per frame a launch renders (`frames`), laid out as [copies of
+  // the rows][copies of the bits][copies of the counters].  Bits and counters
+  // start at zero; each launch's last sub-block of a pixel zeroes them again
+  // (rt_kernel.hip), so they are cleared only when the layout changes.
+  const size_t rows = (size_t)c->nsplit * st->samples * 3 * sizeof(double);
+  const size_t flags = split_flags_bytes(c->nsplit, st->samples);
+  if (c->nsplit && c->split_frames < frames) {
+    int rc = quiesce(c);  // earlier launches may still use the rows
+    if (rc) return rc;
+    rc = grow(&c->d_split, &c->split_cap, (rows + flags) * (size_t)frames + 256);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync((char*)c->d_split + rows * (size_t)frames, 0, flags * (size_t)frames, s));
+    c->split_frames = frames;
+  }
+  const size_t nf = (size_t)std::max(c->split_frames, 1);
   p->blocks = c->d_blocks;
   p->num_blocks = c->num_blocks;
+  p->nsplit = c->nsplit;
+  p->split_frames = c->split_frames;
   p->split_rad = c->nsplit ? (double*)c->d_split : nullptr;
-  p->split_hits = c->nsplit ? (uint32_t*)((char*)c->d_split + (size_t)c->nsplit * st->samples * 3 * sizeof(double))
-                            : nullptr;
-  p->split_cnt = c->nsplit ? (int32_t*)(p->split_hits + (size_t)c->nsplit * ((st->samples + 31) / 32)) : nullptr;
+  p->split_hits = c->nsplit ? (uint32_t*)((char*)c->d_split + rows * nf) : nullptr;
+  p->split_cnt = c->nsplit ? (int32_t*)(p->split_hits + (size_t)c->nsplit * ((st->samples + 31) / 32) * nf) : nullptr;
   p->tile_masks = (masks && frustum) ? c->d_masks : nullptr;
   return RT_OK;
 }
@@ -1136,6 +1147,68 @@ int rt_context_kernel_seconds(rt_context* c, double* seconds, int64_t* launches)
     seconds[k] = c->prof_secs[k];
     if (launches) launches[k] = c->prof_launches[k];
   }
+  return RT_OK;
+}
+
+// Several frames of one schedule in ONE launch (include/rt_api.h).
+int rt_context_render_frames_async(rt_context* c, int32_t w, int32_t h, const rt_settings* st, int32_t nframes,
+                                   const uint64_t* seeds, int32_t rank, int32_t world, int32_t layout,
+                                   float* const* d_linear, uint8_t* const* d_rgba, void* stream) {
+  if (!c || !c->have_scene) {
+    set_error("context has no scene");
+    return RT_E_INVALID;
+  }
+  if (nframes < 1 || nframes > RT_MAX_FRAMES || !seeds || !d_linear) {
+    set_error("rt_context_render_frames_async: nframes must be in [1, RT_MAX_FRAMES] with seeds and d_linear given");
+    return RT_E_INVALID;
+  }
+  int rc = validate_settings(st, w, h);
+  if (rc) return rc;
+  if (world < 1 || rank < 0 || rank >= world) {
+    set_error("invalid rank/world");
+    return RT_E_INVALID;
+  }
+  if (layout != RT_LAYOUT_IMAGE && layout != RT_LAYOUT_PACKED_TILES) {
+    set_error("invalid layout");
+    return RT_E_INVALID;
+  }
+  // one frame at a time where a launch cannot hold several: the wavefront
+  // path (host-driven bounce loop), sample passes, a measuring frame
+  const int npass = std::max(1, (st->samples + kMaxBlockSamples - 1) / kMaxBlockSamples);
+  if (nframes == 1 || use_wavefront(c) || npass > 1 || (c->tun.measure && c->meas_state != 3)) {
+    for (int f = 0; f < nframes; ++f) {
+      rt_settings sf = *st;
+      sf.seed = seeds[f];
+      rc = rt_context_render_async(c, w, h, &sf, rank, world, layout, d_linear[f], d_rgba ? d_rgba[f] : nullptr,
+                                   stream, nullptr);
+      if (rc) return rc;
+    }
+    return RT_OK;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  KParams p;
+  base_params(c, w, h, st, rank, world, layout, &p);
+  hipStream_t s = (hipStream_t)stream;
+  if (c->have_timing && s != c->last_stream) HIP_TRY(hipStreamWaitEvent(s, c->ev1, 0));
+  rc = prepare_schedule(c, &p, st, s, nframes);
+  if (rc) return rc;
+  p.spp_total = st->samples;
+  p.nframes = nframes;
+  for (int f = 0; f < nframes; ++f) {
+    p.frame_key[f] = rt_rng_seed_key(seeds[f]);
+    p.frame_lin[f] = d_linear[f];
+    p.frame_rgba[f] = d_rgba ? d_rgba[f] : nullptr;
+  }
+  p.num_wgs = p.num_blocks * nframes;
+  HIP_TRY(hipEventRecord(c->ev0, s));
+  const int e = launch_render(p, false, s);
+  if (e != hipSuccess) {
+    set_error(std::string("render launch failed: ") + hipGetErrorString((hipError_t)e));
+    return RT_E_DEVICE;
+  }
+  HIP_TRY(hipEventRecord(c->ev1, s));
+  c->last_stream = s;
+  c->have_timing = true;
   return RT_OK;
 }
 

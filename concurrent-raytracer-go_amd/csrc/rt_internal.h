@@ -100,6 +100,7 @@ constexpr int kJump = 64 + 1;
 // radiance slots live in LDS: 24 KB); the host picks P = floor(1024 / spp)
 // pixels per block (at most 64), so spp <= 1024.
 constexpr int kMaxBlockSamples = 1024;
+constexpr int kMaxFrames = RT_MAX_FRAMES;  // frames per launch at most (rt_context_render_frames_async)
 constexpr int kDbgStride = 48;  // RT_WG_TIMING: 64-bit words per workgroup in the debug buffer
 // Counters of the counting variants: the nine of rt_counts, then the same
 // nine for the work the counting variant walks only to report the
@@ -149,7 +150,7 @@ struct KParams {
   int32_t tiles_x, ntiles;
   int32_t num_blocks;        // this rank's blocks (one workgroup each)
   int32_t layout;     // RT_LAYOUT_*
-  int32_t num_wgs;         // = num_blocks
+  int32_t num_wgs;         // = num_blocks * nframes
   // sample passes (more samples per pixel than a block holds, DESIGN.md
   // §4.1): this launch renders samples [sample_base, sample_base + spp) of
   // spp_total; acc holds each local pixel's running sum (lt * 1024 + pixel,
@@ -158,6 +159,17 @@ struct KParams {
   // (not the last pass).  Single pass: acc_mode 0, spp_total = spp.
   double* acc;
   int32_t sample_base, spp_total, acc_mode;
+  // FRAMES of one launch (rt_context_render_frames_async): the same schedule
+  // rendered nframes times, each frame with its own seed and outputs.
+  // Workgroup g renders block g / nframes of frame g % nframes, so every
+  // frame's heaviest blocks start first and one launch's tail covers all
+  // its frames.  launch_render fills entry 0 from seed_key / out_linear /
+  // out_rgba when nframes <= 1.  Split pixels: a copy of the split rows and
+  // flags per frame, nsplit slots each (split_frames copies in memory).
+  int32_t nframes, nsplit, split_frames, _fpad;
+  uint64_t frame_key[kMaxFrames];
+  float* frame_lin[kMaxFrames];
+  uint8_t* frame_rgba[kMaxFrames];
 };
 
 // Enqueue the render kernel; returns hipError_t as int.
@@ -165,9 +177,10 @@ int launch_render(const KParams& p, bool count, void* stream);
 size_t render_shmem(const KParams& p);
 int launch_unpack(int32_t W, int32_t H, int32_t world, const void* gathered, size_t share_bytes, size_t rgba_off,
                   float* ol, uint8_t* orgba, void* stream);
-// The same for a partition: slot[t] = {owner rank, local tile} of global tile t.
-int launch_unpack_map(int32_t W, int32_t H, const int32_t* slot, const void* gathered, size_t share_bytes,
-                      size_t rgba_off, float* ol, uint8_t* orgba, void* stream);
+// The same for a partition: slot[t] = {owner rank, local tile} of global tile t;
+// nframes frames gathered as [world][nframes][share] into [nframes][W*H] images.
+int launch_unpack_map(int32_t W, int32_t H, int32_t nframes, const int32_t* slot, const void* gathered,
+                      size_t share_bytes, size_t rgba_off, float* ol, uint8_t* orgba, void* stream);
 // Per global tile of a frame, the sum of its pixels' estimated work (rt_schedule.hip
 // sched_est of a whole-frame pilot): the input of a balanced partition.
 int sched_launch_tile_work(const SchedParams& p, float* tile_work, void* stream);

@@ -379,6 +379,18 @@ __device__ __forceinline__ KArg fresh() {
   return k;
 }
 
+// The launch's frame and block of this workgroup (KParams.nframes)
+__device__ __forceinline__ int frame_of(KArg k) {
+  return k->nframes > 1 ? (int)(blockIdx.x % (unsigned)k->nframes) : 0;
+}
+__device__ __forceinline__ int block_of(KArg k) {
+  return k->nframes > 1 ? (int)(blockIdx.x / (unsigned)k->nframes) : (int)blockIdx.x;
+}
+// a split pixel's radiance row / hit-bit words / sub-block counter in this frame's copy
+__device__ __forceinline__ size_t split_index(KArg k, int slot) {
+  return (size_t)frame_of(k) * (size_t)k->nsplit + (size_t)slot;
+}
+
 // ------------------------------------------------------------ work blocks
 // A BLOCK is np consecutive row-major pixels of one 32x32 tile with all
 // their spp samples: NB = np*spp sample ids, pixel-major (id = p*spp + s).
@@ -463,7 +475,7 @@ __device__ __forceinline__ Hot hot() {
 // the launch-uniform inputs; phase 1 loads it once per block (SGPRs), the
 // shading loop rebuilds it from the kernarg segment where it needs it.
 __device__ __forceinline__ CamK cam_k(KArg k) {
-  return make_cam(k->seed_key, k->W, k->H, k->aspect, k->cam[0], k->cam[1], k->cam[2]);
+  return make_cam(k->frame_key[frame_of(k)], k->W, k->H, k->aspect, k->cam[0], k->cam[1], k->cam[2]);
 }
 template <bool kCount>
 __device__ __forceinline__ void camera_ray(KArg k, int x, int y, int s, rt_rng& rng, d3& o, d3& d, Counters& c) {
@@ -686,7 +698,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
 
   const int lane = threadIdx.x;
   int* stack = reinterpret_cast<int*>(dyn_lds + pk.stack_off) + lane;
-  const BlockLoc blk = block_loc(fresh(), blockIdx.x);
+  const BlockLoc blk = block_loc(fresh(), block_of(fresh()));
   // a black block (up to 64 pixels x spp samples) sets no hit bits
   const int nwords = blk.black ? 0 : (blk.np * blk.ns + 31) >> 5;
   if (lane < nwords) hbits[lane] = 0;
@@ -738,7 +750,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     // SGPRs); re-reading the kernarg segment inside the loop put scalar
     // load round trips on every iteration
     KArg k = fresh();
-    const BlockLoc loc = block_loc(k, blockIdx.x);
+    const BlockLoc loc = block_loc(k, block_of(k));
     const int NB = loc.np * loc.ns, ns = loc.ns;
     // primary-ray frustum culling (host-computed per pixel, schedule.cpp):
     // only primitives whose bounding sphere meets the cone of a pixel's
@@ -866,8 +878,8 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"((int)threadIdx.x));
     if (blk.slot >= 0) {
       KArg k = fresh();
-      double* row = k->split_rad + (size_t)blk.slot * k->spp * 3;
-      uint32_t* hw = k->split_hits + (size_t)blk.slot * ((k->spp + 31) >> 5);
+      double* row = k->split_rad + split_index(k, blk.slot) * k->spp * 3;
+      uint32_t* hw = k->split_hits + split_index(k, blk.slot) * ((k->spp + 31) >> 5);
       for (int e = a + lane; e < b; e += 64) {
         const int s = blk.s0 + entry_id(e);  // one pixel: id = sample - s0
         const int q = e & (kRound - 1);
@@ -946,7 +958,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       const int e = next + lanes_below(freem);
       if (!alive && e < limit) {
         KArg k = fresh();
-        const BlockLoc loc = block_loc(k, blockIdx.x);
+        const BlockLoc loc = block_loc(k, block_of(k));
         const int id = entry_id(e), ns = loc.ns;
         const int p = id / ns, s = k->sample_base + loc.s0 + id - p * ns;
         const int tp = loc.p0 + p;
@@ -1207,7 +1219,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       if (fin) {  // the path's radiance goes to its entry's ring slot
         if constexpr (kPilot) {  // a measuring render: the pixel's longest path and its bounces
           KArg k = fresh();
-          const BlockLoc loc = block_loc(k, blockIdx.x);
+          const BlockLoc loc = block_loc(k, block_of(k));
           const size_t px = (size_t)loc.lt * 1024 + loc.p0 + entry_id(entry) / loc.ns;
           atomicMax(k->work_max + px, (unsigned)depth + 1u);
           atomicAdd(k->work_sum + px, (unsigned)depth + 1u);
@@ -1238,13 +1250,13 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     // samples of the slot row in sample order (misses add +0) and writes it
     __threadfence();
     int old = 0;
-    if (lane3 == 0) old = atomicAdd(&k->split_cnt[blk.slot], 1);
+    if (lane3 == 0) old = atomicAdd(&k->split_cnt[split_index(k, blk.slot)], 1);
     old = __builtin_amdgcn_readfirstlane(old);
     resolve = old == blk.nsub - 1;
     if (resolve) {
       __threadfence();
-      const double* row = k->split_rad + (size_t)blk.slot * k->spp * 3;
-      uint32_t* hw = k->split_hits + (size_t)blk.slot * ((k->spp + 31) >> 5);
+      const double* row = k->split_rad + split_index(k, blk.slot) * k->spp * 3;
+      uint32_t* hw = k->split_hits + split_index(k, blk.slot) * ((k->spp + 31) >> 5);
       // chunks of kRound samples: all lanes load (in parallel) into the LDS
       // slots, misses as +0, then one lane per channel adds them in order
       double a = 0;  // (a later sample pass continues the running sum)
@@ -1267,12 +1279,12 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       // the slot's hit bits and counter are left zeroed for the next launch
       // (the host clears them only when it builds a schedule: no memset per frame)
       for (int i = lane3; i < ((k->spp + 31) >> 5); i += 64) hw[i] = 0u;
-      if (lane3 == 0) k->split_cnt[blk.slot] = 0;
+      if (lane3 == 0) k->split_cnt[split_index(k, blk.slot)] = 0;
       __syncthreads();
     }
   }
   if (resolve) {
-    const BlockLoc loc = block_loc(k, blockIdx.x);
+    const BlockLoc loc = block_loc(k, block_of(k));
     const int p = lane3;
     const int tp = loc.p0 + p;
     const int x = loc.tx * 32 + (tp & 31), y = loc.ty * 32 + (tp >> 5);
@@ -1285,13 +1297,16 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       const double n = (double)k->spp_total;
       const double mx = psum[p][0] / n, my = psum[p][1] / n, mz = psum[p][2] / n;  // DivScalar(float64(samples))
       const size_t oi = k->layout == RT_LAYOUT_IMAGE ? (size_t)y * k->W + x : (size_t)loc.lt * 1024 + (size_t)tp;
-      if (k->out_linear) {
-        k->out_linear[oi * 3 + 0] = (float)mx;
-        k->out_linear[oi * 3 + 1] = (float)my;
-        k->out_linear[oi * 3 + 2] = (float)mz;
+      const int fr = frame_of(k);
+      float* const ol = k->frame_lin[fr];
+      uint8_t* const orgba = k->frame_rgba[fr];
+      if (ol) {
+        ol[oi * 3 + 0] = (float)mx;
+        ol[oi * 3 + 1] = (float)my;
+        ol[oi * 3 + 2] = (float)mz;
       }
-      if (k->out_rgba) {
-        *reinterpret_cast<uint32_t*>(k->out_rgba + oi * 4) = tonemap_rgba8(mx, my, mz);
+      if (orgba) {
+        *reinterpret_cast<uint32_t*>(orgba + oi * 4) = tonemap_rgba8(mx, my, mz);
       }
     }
   }
@@ -1354,34 +1369,45 @@ __global__ __launch_bounds__(256) void unpack_kernel(int W, int H, int world, in
     *reinterpret_cast<uint32_t*>(orgba + o * 4) = *reinterpret_cast<const uint32_t*>(share + rgba_off + pi * 4);
 }
 
-// The same scatter for a partition: slot[t] = {owner rank, local tile}.
-__global__ __launch_bounds__(256) void unpack_map_kernel(int W, int H, int tiles_x, const int2* __restrict__ slot,
-                                                         const uint8_t* __restrict__ g, size_t share_bytes,
-                                                         size_t rgba_off, float* __restrict__ ol,
+// The same scatter for a partition: slot[t] = {owner rank, local tile}; frame
+// blockIdx.y of nframes, gathered as [world][nframes][share], written to
+// [nframes][W*H] images.
+__global__ __launch_bounds__(256) void unpack_map_kernel(int W, int H, int tiles_x, int nframes,
+                                                         const int2* __restrict__ slot, const uint8_t* __restrict__ g,
+                                                         size_t share_bytes, size_t rgba_off, float* __restrict__ ol,
                                                          uint8_t* __restrict__ orgba) {
   const long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= (long long)W * H) return;
+  const int f = blockIdx.y;
+  const long long oo = (long long)f * W * H + o;
   const int y = (int)(o / W), x = (int)(o - (long long)y * W);
   const int2 rl = slot[(y >> 5) * tiles_x + (x >> 5)];
   const size_t pi = (size_t)rl.y * 1024 + (size_t)((y & 31) * 32 + (x & 31));
-  const uint8_t* share = g + (size_t)rl.x * share_bytes;
+  const uint8_t* share = g + ((size_t)rl.x * nframes + f) * share_bytes;
   if (ol) {
     const float* pl = reinterpret_cast<const float*>(share) + pi * 3;
-    ol[o * 3 + 0] = pl[0];
-    ol[o * 3 + 1] = pl[1];
-    ol[o * 3 + 2] = pl[2];
+    ol[oo * 3 + 0] = pl[0];
+    ol[oo * 3 + 1] = pl[1];
+    ol[oo * 3 + 2] = pl[2];
   }
   if (orgba)
-    *reinterpret_cast<uint32_t*>(orgba + o * 4) = *reinterpret_cast<const uint32_t*>(share + rgba_off + pi * 4);
+    *reinterpret_cast<uint32_t*>(orgba + oo * 4) = *reinterpret_cast<const uint32_t*>(share + rgba_off + pi * 4);
 }
 
 size_t render_shmem(const KParams& p) {
   return (size_t)p.stack_off + (p.use_bvh ? sizeof(int) * p.stack_depth * 64 : 0);
 }
 
-int launch_render(const KParams& p, bool count, void* stream) {
+int launch_render(const KParams& pin, bool count, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (p.num_wgs <= 0) return hipSuccess;
+  if (pin.num_wgs <= 0) return hipSuccess;
+  KParams p = pin;
+  if (p.nframes <= 1) {  // one frame: entry 0 from the single-frame fields
+    p.nframes = 1;
+    p.frame_key[0] = p.seed_key;
+    p.frame_lin[0] = p.out_linear;
+    p.frame_rgba[0] = p.out_rgba;
+  }
   const size_t shmem = render_shmem(p);
   const bool stage = p.stage_bytes > 0;
   const dim3 g(p.num_wgs), b(64);
@@ -1436,13 +1462,14 @@ int launch_unpack(int32_t W, int32_t H, int32_t world, const void* gathered, siz
   return (int)hipGetLastError();
 }
 
-int launch_unpack_map(int32_t W, int32_t H, const int32_t* slot, const void* gathered, size_t share_bytes,
-                      size_t rgba_off, float* ol, uint8_t* orgba, void* stream) {
+int launch_unpack_map(int32_t W, int32_t H, int32_t nframes, const int32_t* slot, const void* gathered,
+                      size_t share_bytes, size_t rgba_off, float* ol, uint8_t* orgba, void* stream) {
   const long long total = (long long)W * H;
-  if (total <= 0) return hipSuccess;
+  if (total <= 0 || nframes <= 0) return hipSuccess;
   const unsigned blocks = (unsigned)((total + 255) / 256);
-  hipLaunchKernelGGL(unpack_map_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, W, H, (W + 31) / 32,
-                     reinterpret_cast<const int2*>(slot), (const uint8_t*)gathered, share_bytes, rgba_off, ol, orgba);
+  hipLaunchKernelGGL(unpack_map_kernel, dim3(blocks, nframes), dim3(256), 0, (hipStream_t)stream, W, H, (W + 31) / 32,
+                     nframes, reinterpret_cast<const int2*>(slot), (const uint8_t*)gathered, share_bytes, rgba_off, ol,
+                     orgba);
   return (int)hipGetLastError();
 }
 

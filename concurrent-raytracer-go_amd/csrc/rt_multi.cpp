@@ -557,10 +557,10 @@ double rt_partition_work(const rt_partition* p, int32_t rank) {
   return p->d.work[rank];
 }
 
-int rt_unpack_partition_async(const rt_partition* pc, const void* d_gathered, float* d_linear, uint8_t* d_rgba,
-                              void* stream) {
-  if (!pc || !d_gathered) {
-    set_error("rt_unpack_partition_async: invalid arguments");
+int rt_unpack_partition_frames_async(const rt_partition* pc, int32_t nframes, const void* d_gathered,
+                                     float* d_linear, uint8_t* d_rgba, void* stream) {
+  if (!pc || !d_gathered || nframes < 1) {
+    set_error("rt_unpack_partition_frames_async: invalid arguments");
     return RT_E_INVALID;
   }
   rt_partition* p = const_cast<rt_partition*>(pc);  // (the per-device slot maps are a cache)
@@ -581,19 +581,24 @@ int rt_unpack_partition_async(const rt_partition* pc, const void* d_gathered, fl
       HIP_TRY(hipMalloc((void**)&slot, h.size() * sizeof(int32_t)));
       if (hipMemcpy(slot, h.data(), h.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipFree(slot);
-        set_error("rt_unpack_partition_async: slot map upload failed");
+        set_error("rt_unpack_partition_frames_async: slot map upload failed");
         return RT_E_DEVICE;
       }
       p->slots.emplace_back(dev, slot);
     }
   }
-  int e = launch_unpack_map(p->d.w, p->d.h, slot, d_gathered, rt_partition_packed_bytes(p),
+  int e = launch_unpack_map(p->d.w, p->d.h, nframes, slot, d_gathered, rt_partition_packed_bytes(p),
                             rt_partition_rgba_offset(p), d_linear, d_rgba, stream);
   if (e != hipSuccess) {
     set_error(std::string("unpack launch failed: ") + hipGetErrorString((hipError_t)e));
     return RT_E_DEVICE;
   }
   return RT_OK;
+}
+
+int rt_unpack_partition_async(const rt_partition* p, const void* d_gathered, float* d_linear, uint8_t* d_rgba,
+                              void* stream) {
+  return rt_unpack_partition_frames_async(p, 1, d_gathered, d_linear, d_rgba, stream);
 }
 
 int rt_renderer_rank_seconds(const rt_renderer* r, double* out) {

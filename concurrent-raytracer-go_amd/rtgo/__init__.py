@@ -43,6 +43,7 @@ RT_PATH_AUTO, RT_PATH_MEGAKERNEL = 0, 1
 RT_PARTITION_AUTO, RT_PARTITION_STRIDED, RT_PARTITION_BALANCED = 0, 1, 2
 SKIES = {"none": 0, "default": 1, "white": 2, "sunset": 3, "night": 4}  # RT_SKY_*
 RT_COMM_ID_BYTES = 128
+RT_MAX_FRAMES = 16  # frames per launch (rt_context_render_frames_async)
 # wavefront kernel classes (RT_WF_*, rt_context_kernel_seconds)
 WF_KERNELS = ["extend", "shade1", "occlude_hard", "softgen", "occlude_soft", "shade", "regen", "resolve"]
 
@@ -247,6 +248,8 @@ EXPORTED_SYMBOLS = [
     "rt_renderer_rank_seconds",
     "rt_context_profile",
     "rt_context_kernel_seconds",
+    "rt_context_render_frames_async",
+    "rt_unpack_partition_frames_async",
 ]
 
 _lib = None
@@ -335,6 +338,12 @@ def lib():
         "rt_comm_gather_bytes_async": (ctypes.c_int, [vp, sz, vp, vp, vp]),
         "rt_renderer_rank_seconds": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
         "rt_context_profile": (ctypes.c_int, [vp, i32]),
+        "rt_context_render_frames_async": (
+            ctypes.c_int,
+            [vp, i32, i32, ctypes.POINTER(Settings), i32, ctypes.POINTER(ctypes.c_uint64), i32, i32, i32,
+             ctypes.POINTER(vp), ctypes.POINTER(vp), vp],
+        ),
+        "rt_unpack_partition_frames_async": (ctypes.c_int, [vp, i32, vp, vp, vp, vp]),
         "rt_context_kernel_seconds": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
                                                      ctypes.POINTER(ctypes.c_int64)]),
     }
@@ -653,6 +662,17 @@ class Context:
         )
         return c if full else c.as_dict()
 
+    def render_frames_async(self, width, height, settings: Settings, seeds, d_linear, d_rgba=None, stream: int = 0,
+                            rank: int = 0, world: int = 1, layout: int = RT_LAYOUT_IMAGE):
+        """rt_context_render_frames_async: len(seeds) frames of one schedule in one launch;
+        d_linear / d_rgba: per-frame device pointers (d_rgba None: no RGBA8)."""
+        n = len(seeds)
+        sd = (ctypes.c_uint64 * n)(*seeds)
+        lp = (ctypes.c_void_p * n)(*d_linear)
+        rp = (ctypes.c_void_p * n)(*d_rgba) if d_rgba is not None else None
+        _check(lib().rt_context_render_frames_async(self._h, width, height, ctypes.byref(settings), n, sd, rank, world,
+                                                     layout, lp, rp, ctypes.c_void_p(stream)))
+
     def set_partition(self, partition):
         """Render the tiles of `partition` (a Partition, or None: strided)."""
         self._partition = partition  # (copied by the library; kept for symmetry)
@@ -784,6 +804,12 @@ class Partition:
     def unpack_async(self, d_gathered, d_linear, d_rgba, stream=0):
         _check(lib().rt_unpack_partition_async(self._h, ctypes.c_void_p(d_gathered), ctypes.c_void_p(d_linear),
                                                ctypes.c_void_p(d_rgba), ctypes.c_void_p(stream)))
+
+    def unpack_frames_async(self, nframes, d_gathered, d_linear, d_rgba, stream=0):
+        """[world][nframes][packed bytes] -> [nframes][W*H] images."""
+        _check(lib().rt_unpack_partition_frames_async(self._h, nframes, ctypes.c_void_p(d_gathered),
+                                                      ctypes.c_void_p(d_linear), ctypes.c_void_p(d_rgba),
+                                                      ctypes.c_void_p(stream)))
 
     def close(self):
         if self._h and _lib is not None:

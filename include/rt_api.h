@@ -310,6 +310,20 @@ int rt_context_render_async(rt_context* ctx, int32_t width, int32_t height, cons
                             int32_t rank, int32_t world, int32_t layout, float* d_linear, uint8_t* d_rgba,
                             void* hip_stream, rt_counts* counts);
 
+/* Several frames of the same scene, size and settings that differ only in
+ * their seed (seeds[f]), rendered by ONE launch: the reference's Render
+ * called nframes times (renderer.go:67-126), each frame bit-identical to its
+ * own rt_context_render_async.  The frames share the work schedule; the
+ * launch's workgroups interleave them (every frame's heaviest blocks first),
+ * so the low-occupancy tail of long paths is paid once per launch instead of
+ * once per frame.  d_linear[f] / d_rgba[f] (d_rgba may
+ * be NULL, entries may be NULL) are laid out as in rt_context_render_async.
+ * BVH scenes, sample passes and measuring frames render frame by frame. */
+#define RT_MAX_FRAMES 16
+int rt_context_render_frames_async(rt_context* ctx, int32_t width, int32_t height, const rt_settings* settings,
+                                   int32_t nframes, const uint64_t* seeds, int32_t rank, int32_t world,
+                                   int32_t layout, float* const* d_linear, uint8_t* const* d_rgba, void* hip_stream);
+
 /* Packed share of one rank, as rt_comm_gather_tiles_async moves it:
  * [max_local_tiles * 1024 float3][max_local_tiles * 1024 RGBA8] = 16 B per
  * pixel of the largest share (rank 0's).  Render a share with layout
@@ -381,6 +395,10 @@ int rt_context_set_partition(rt_context* ctx, const rt_partition* p);
 /* rt_unpack_tiles_async for a partition's shares ([world][rt_partition_packed_bytes]). */
 int rt_unpack_partition_async(const rt_partition* p, const void* d_gathered, float* d_linear, uint8_t* d_rgba,
                               void* hip_stream);
+/* The same for nframes frames gathered as [world][nframes][packed bytes] (each
+ * rank's frames contiguous: one send per rank) into [nframes][W*H] images. */
+int rt_unpack_partition_frames_async(const rt_partition* p, int32_t nframes, const void* d_gathered, float* d_linear,
+                                     uint8_t* d_rgba, void* hip_stream);
 /* rt_comm_gather_tiles_async with shares of share_bytes (a partition's packed bytes). */
 int rt_comm_gather_bytes_async(rt_comm* comm, size_t share_bytes, const void* d_share, void* d_gathered,
                                void* hip_stream);

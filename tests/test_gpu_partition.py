@@ -203,3 +203,54 @@ def test_wavefront_kernel_profile():
     assert soft["camera_rays"] == 0 and soft["rng_draws"] == 0
     ctx.profile(False)
     ctx.close()
+
+
+@pytest.mark.parametrize("tuning", [{}, {"split_samples": 16, "block_work": 64.0}], ids=["default", "many_splits"])
+def test_frames_of_one_launch_equal_single_renders(tuning):
+    """rt_context_render_frames_async: 6 frames (seeds 11..16) of the headline
+    frame in one launch, each bit-identical to its own single render (split
+    pixels included: a copy of their rows per frame); then the packed shares
+    of 3 ranks of a balanced partition, 4 frames per launch, gathered as
+    [rank][frame][share] and unpacked in one launch."""
+    import torch
+
+    scene = load_case(rtgo, FACING)
+    w, h, spp = 800, 600, 100
+    tn = rtgo.default_tuning(**tuning)
+    st = make_settings(rtgo, {"samples": spp, "max_depth": 50}, seed=1)
+    seeds = list(range(11, 17))
+    ctx = rtgo.Context(0)
+    ctx.set_tuning(tn)
+    ctx.set_scene(scene)
+    lin = torch.zeros((len(seeds), w * h * 3), dtype=torch.float32, device="cuda")
+    rgba = torch.zeros((len(seeds), w * h * 4), dtype=torch.uint8, device="cuda")
+    ctx.render_frames_async(w, h, st, seeds, [lin[f].data_ptr() for f in range(len(seeds))],
+                            [rgba[f].data_ptr() for f in range(len(seeds))])
+    torch.cuda.synchronize()
+    for f, sd in enumerate(seeds):
+        ref_lin, ref_rgba, _, _ = render_dev(scene, w, h, make_settings(rtgo, {"samples": spp, "max_depth": 50},
+                                                                        seed=sd), tuning=tn)
+        assert lin[f].cpu().numpy().tobytes() == ref_lin.tobytes(), f
+        assert rgba[f].cpu().numpy().tobytes() == ref_rgba.tobytes(), f
+    # packed shares of a balanced partition, frames batched per rank
+    world, nf = 3, 4
+    part = ctx.balanced_partition(w, h, st, world)
+    ctx.close()
+    nb = part.packed_bytes
+    g = torch.zeros(world * nf * nb, dtype=torch.uint8, device="cuda")
+    for r in range(world):
+        c = rtgo.Context(0)
+        c.set_tuning(tn)
+        c.set_scene(scene)
+        c.set_partition(part)
+        base = g.data_ptr() + r * nf * nb
+        lp = [base + f * nb for f in range(nf)]
+        c.render_frames_async(w, h, st, seeds[:nf], lp, [p + part.rgba_offset for p in lp], 0, r, world,
+                              rtgo.RT_LAYOUT_PACKED_TILES)
+        torch.cuda.synchronize()
+        c.close()
+    img_lin = torch.zeros(nf * w * h * 3, dtype=torch.float32, device="cuda")
+    img_rgba = torch.zeros(nf * w * h * 4, dtype=torch.uint8, device="cuda")
+    part.unpack_frames_async(nf, g.data_ptr(), img_lin.data_ptr(), img_rgba.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(img_lin.view(nf, -1), lin[:nf]) and torch.equal(img_rgba.view(nf, -1), rgba[:nf])
