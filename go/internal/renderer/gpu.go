@@ -104,7 +104,8 @@ func (r *ParallelRenderer) RenderGPU(s *scene.Scene, width, height int) *image.R
 	cdata := C.CBytes(data)
 	defer C.free(cdata)
 	var sb *C.rt_scene_buf
-	if rc := C.rt_scene_parse_json((*C.char)(cdata), C.size_t(len(data)), 0, &sb); rc != C.RT_OK {
+	// verbose 1: the lines Render prints through GetHittables (scene.go:62-88)
+	if rc := C.rt_scene_parse_json((*C.char)(cdata), C.size_t(len(data)), 1, &sb); rc != C.RT_OK {
 		panic(rtError("rt_scene_parse_json", rc).Error())
 	}
 	defer C.rt_scene_free(sb)
@@ -119,12 +120,18 @@ func (r *ParallelRenderer) RenderGPU(s *scene.Scene, width, height int) *image.R
 	st.depth_of_field = cbool(r.depthOfField)
 	st.num_workers = C.int32_t(r.numWorkers)
 
+	img := image.NewRGBA(image.Rect(0, 0, width, height))
+	var stats C.rt_stats
+	if width <= 0 || height <= 0 {
+		// Render with no tiles (createRenderTasks makes none): an empty image
+		stats.objects = C.int32_t(C.rt_scene_view(sb).num_objects)
+		stats.lights = C.int32_t(C.rt_scene_view(sb).num_lights)
+		return r.finishGPU(s, img, width, height, start, stats)
+	}
 	h, err := r.gpuRenderer()
 	if err != nil {
 		panic(err.Error())
 	}
-	img := image.NewRGBA(image.Rect(0, 0, width, height))
-	var stats C.rt_stats
 	// img.Pix: W*H*4 bytes, row y = Go image row y, the layout rt_renderer_render
 	// writes; a Go pointer to pointer-free memory, not retained (cgo rules)
 	rc := C.rt_renderer_render(h, C.rt_scene_view(sb), C.int32_t(width), C.int32_t(height), &st, nil,
@@ -132,6 +139,13 @@ func (r *ParallelRenderer) RenderGPU(s *scene.Scene, width, height int) *image.R
 	if rc != C.RT_OK {
 		panic(rtError("rt_renderer_render", rc).Error())
 	}
+	return r.finishGPU(s, img, width, height, start, stats)
+}
+
+// finishGPU records Render's benchmark data and prints its closing lines
+// (renderer.go:101-123).
+func (r *ParallelRenderer) finishGPU(s *scene.Scene, img *image.RGBA, width, height int, start time.Time,
+	stats C.rt_stats) *image.RGBA {
 	renderTime := time.Since(start)
 	r.benchmarkData.SceneName = s.GetSceneName() // renderer.go:103-112
 	r.benchmarkData.Resolution = fmt.Sprintf("%dx%d", width, height)

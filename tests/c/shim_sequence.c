@@ -4,11 +4,14 @@
  * mirror's render.
  *
  *   usage: shim_sequence <scene as json.Marshal writes it> <W> <H> <samples> <out.rgba> [devices]
+ *   devices: the device of each rank, comma-separated (e.g. 0,0,0: three
+ *   ranks on device 0); default 0
  *   exit 0: rendered, raw RGBA (W*H*4) written; exit 2: bad usage / I/O;
  *   exit 3: a library call failed (message on stderr, e.g. no GPU).
  *
  * The calls, in gpu.go's order:
- *   rt_scene_parse_json (the json.Marshal bytes of *scene.Scene)
+ *   rt_scene_parse_json (the json.Marshal bytes of *scene.Scene; verbose: the
+ *     lines GetHittables prints, scene.go:62-88)
  *   rt_settings_default + the ParallelRenderer fields (settings.go:3-25)
  *   rt_renderer_create (first Render of this ParallelRenderer)
  *   rt_renderer_render into the caller's Pix buffer (image.RGBA, W*H*4)
@@ -25,7 +28,15 @@ int main(int argc, char** argv) {
     return 2;
   }
   const int w = atoi(argv[2]), h = atoi(argv[3]), spp = atoi(argv[4]);
-  const int ndev = argc > 6 ? atoi(argv[6]) : 1;
+  int devs[64], ndev = 0;
+  if (argc > 6) {
+    for (const char* p = argv[6]; *p && ndev < 64;) {
+      devs[ndev++] = atoi(p);
+      while (*p && *p != ',') ++p;
+      if (*p == ',') ++p;
+    }
+  }
+  if (ndev == 0) devs[ndev++] = 0;
   FILE* f = fopen(argv[1], "rb");
   if (!f) return 2;
   fseek(f, 0, SEEK_END);
@@ -36,7 +47,7 @@ int main(int argc, char** argv) {
   fclose(f);
 
   rt_scene_buf* sb = NULL;
-  int rc = rt_scene_parse_json(data, (size_t)n, 0, &sb);
+  int rc = rt_scene_parse_json(data, (size_t)n, 1, &sb);
   free(data);
   if (rc != RT_OK) {
     fprintf(stderr, "rt_scene_parse_json failed (%d): %s\n", rc, rt_last_error());
@@ -51,9 +62,10 @@ int main(int argc, char** argv) {
   st.soft_shadows = 1;
   st.depth_of_field = 0;
   st.num_workers = 8;
+  st.num_devices = ndev;
 
   rt_renderer* r = NULL;
-  rc = rt_renderer_create(NULL, ndev, &r);
+  rc = rt_renderer_create(devs, ndev, &r);
   if (rc != RT_OK) {
     fprintf(stderr, "rt_renderer_create failed (%d): %s\n", rc, rt_last_error());
     rt_scene_free(sb);

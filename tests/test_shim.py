@@ -79,7 +79,7 @@ def test_sequence_fails_loudly_without_a_gpu(harness, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("devices", [1])
+@pytest.mark.parametrize("devices", ["0", "0,0,0"], ids=["1_rank", "3_ranks_on_device_0"])
 def test_sequence_renders_like_the_mirror(harness, tmp_path, devices):
     w, h, spp = 64, 48, 3
     out = tmp_path / "o.rgba"
@@ -87,6 +87,7 @@ def test_sequence_renders_like_the_mirror(harness, tmp_path, devices):
                        text=True, timeout=300)
     assert p.returncode == 0, p.stderr
     assert "objects 11 lights 3" in p.stdout
+    assert "Created 11 hittables total" in p.stdout  # GetHittables' lines (scene.go:62-88)
     got = np.fromfile(out, np.uint8).reshape(h, w, 4)
     r = rtgo.ParallelRenderer()
     r.settings = make_settings(rtgo, {"samples": spp}, seed=1)
