@@ -1,14 +1,20 @@
 #!/usr/bin/env python3
-"""Reduce rocprofv3 PMC passes to HBM bytes per render launch.
+"""Reduce rocprofv3 PMC passes to HBM bytes per launch of a config's
+dominant kernel, merged into profiles/<round>_pmc_traffic.json under the
+workload label bench.py prints (its roofline.traffic).
 
-usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json
+usage: pmc_traffic.py CONFIG FETCH_DIR WRITE_DIR OUT.json FRAMES
 Each DIR holds one rocprofv3 --pmc pass (FETCH_SIZE, resp. WRITE_SIZE; they
-cannot share a pass on gfx950) in CSV form.  Corrections from
+cannot share a pass on gfx950) in CSV form over FRAMES frames of the config
+(scripts/pmc_workload.py).  Corrections from
 /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE is in KiB and
-reports half the bytes of wide (16 B/lane) streaming reads; WRITE_SIZE is
-exact for 16 B/lane stores.  This kernel's stores are 4 B/lane (RGBA8) and
-3 x 4 B/lane (float3), a width the guide has not calibrated, so both raw
-and corrected values are recorded.
+reports half the bytes of wide streaming reads on gfx950 (x2 here);
+WRITE_SIZE is exact for this code's store patterns (calibrated on
+unpack_kernel, profiles/r02_pmc_calibration.json).
+c2 / c3: the render kernel, the median over its launches.  c4 / c5: the
+soft-shadow traversal kernel (wf_occlude<soft>, the roofline's kernel for
+those configs), summed over a frame's launches (bench.py prices it per
+frame), and the whole frame's bytes beside it.
 """
 import csv
 import glob
@@ -17,47 +23,68 @@ import os
 import statistics
 import sys
 
-KERNEL = "render_kernel<false, true, false, false>"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "concurrent-raytracer-go_amd"), os.path.join(ROOT, "tests")]
+from bench import CONFIGS, KERNELS, WAVEFRONT  # noqa: E402
 
 
 def per_dispatch(d, counter):
+    """[(kernel name, value)] per dispatch, in dispatch order."""
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
     vals = {}
     for f in files:
         for row in csv.DictReader(open(f)):
-            if KERNEL not in row.get("Kernel_Name", "") or row.get("Counter_Name") != counter:
+            if row.get("Counter_Name") != counter:
                 continue
-            key = row.get("Dispatch_Id") or row.get("Correlation_Id")
-            vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
-    if not vals:
-        raise SystemExit(f"no {counter} rows for {KERNEL} in {files}")
-    return sorted(vals.values())
+            key = int(row.get("Dispatch_Id") or row.get("Correlation_Id"))
+            name, v = vals.get(key, (row.get("Kernel_Name", ""), 0.0))
+            vals[key] = (name, v + float(row["Counter_Value"]))
+    return [vals[k] for k in sorted(vals)]
 
 
 def main():
-    fdir, wdir, out = sys.argv[1:4]
-    fetch_kib = statistics.median(per_dispatch(fdir, "FETCH_SIZE"))
-    write_kib = statistics.median(per_dispatch(wdir, "WRITE_SIZE"))
-    fetch_b = fetch_kib * 1024 * 2  # gfx950: FETCH_SIZE counts half the bytes
-    write_b = write_kib * 1024
-    res = {
-        "workload": "sphere_reflections_light_facing 800x600 100spp depth 50",
-        "kernel": KERNEL,
-        "fetch_size_kib_raw": fetch_kib,
-        "write_size_kib_raw": write_kib,
-        "fetch_bytes_corrected": fetch_b,
-        "write_bytes": write_b,
-        "hbm_bytes_per_launch": fetch_b + write_b,
-        "algorithmic_bytes_per_launch": 800 * 600 * 16 + 4096,
-        "note": "median over the profiled launches; FETCH_SIZE x2 per MI355X_MICROARCH.md; WRITE_SIZE is exact for "
-                "this kernel's 12 + 4 B/lane store pattern (calibrated on unpack_kernel, "
-                "profiles/r02_pmc_calibration.json); the kernel has no scratch (r02); the bytes written beyond the framebuffer are the split pixels' per-sample radiance rows",
-    }
+    cfg, fdir, wdir, out, frames = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5])
+    spec, W, H, SPP, label = CONFIGS[cfg][:5]
+    workload = "%s %dx%d %dspp depth 50" % (label, W, H, SPP)
+    kern = KERNELS[cfg].replace("rtgo::", "")
+    fetch = per_dispatch(fdir, "FETCH_SIZE")
+    write = per_dispatch(wdir, "WRITE_SIZE")
+
+    def pick(rows):
+        return [v for n, v in rows if kern in n]
+
+    kf, kw = pick(fetch), pick(write)
+    if not kf or not kw:
+        raise SystemExit(f"no {kern} rows")
+    res = {"kernel": KERNELS[cfg], "frames_profiled": frames}
+    if cfg in WAVEFRONT:
+        fb = sum(kf) / frames * 1024 * 2
+        wb = sum(kw) / frames * 1024
+        res.update({
+            "unit": "per frame (the kernel's launches of one frame)",
+            "launches_per_frame": len(kf) / frames,
+            "fetch_bytes_corrected": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
+            "frame_fetch_bytes_all_kernels": sum(v for _, v in fetch) / frames * 1024 * 2,
+            "frame_write_bytes_all_kernels": sum(v for _, v in write) / frames * 1024,
+        })
+    else:
+        fb = statistics.median(kf) * 1024 * 2
+        wb = statistics.median(kw) * 1024
+        res.update({"unit": "per launch (median)", "fetch_bytes_corrected": fb, "write_bytes": wb,
+                    "hbm_bytes_per_launch": fb + wb, "algorithmic_bytes_per_launch": W * H * 16 + 4096})
+    res["note"] = ("FETCH_SIZE (KiB) x1024 x2 per MI355X_MICROARCH.md §HBM (gfx950 counts half the bytes of wide "
+                   "reads); WRITE_SIZE (KiB) x1024, exact for these stores (profiles/r02_pmc_calibration.json)")
+    try:
+        with open(out) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        d = {}
+    d[workload] = res
     with open(out, "w") as f:
-        json.dump(res, f, indent=1)
-    print(json.dumps(res))
+        json.dump(d, f, indent=1)
+    print(json.dumps({workload: res}))
 
 
 if __name__ == "__main__":
