@@ -205,6 +205,14 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 4; ++i) fprintf(f, "    \"%s\"%s\n", features[i], i < 3 ? "," : "");
     fprintf(f, "  ],\n");
     fprintf(f, "  \"kernel_time_seconds\": %.17g,\n", stats.kernel_seconds);
+    // the published benchmark JSON's setup_time / bvh_build_time
+    // (demo-assets/*_benchmark.json; not produced by the snapshot's Go code)
+    fprintf(f, "  \"setup_time\": %.17g,\n", stats.create_seconds + stats.scene_seconds);
+    fprintf(f, "  \"bvh_build_time\": %.17g,\n", stats.bvh_build_seconds);
+    fprintf(f, "  \"render_breakdown_seconds\": {\"create\": %.9g, \"scene\": %.9g, \"launch\": %.9g, "
+               "\"kernels_and_download\": %.9g, \"destroy\": %.9g},\n",
+            stats.create_seconds, stats.scene_seconds, stats.launch_seconds, stats.download_seconds,
+            stats.destroy_seconds);
     fprintf(f, "  \"pixels_per_second\": %.17g,\n", stats.pixels_per_second);
     fprintf(f, "  \"rays_per_second\": %.17g\n", stats.rays_per_second);
     fprintf(f, "}");

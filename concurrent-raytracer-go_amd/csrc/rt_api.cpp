@@ -140,7 +140,7 @@ struct rt_context {
   size_t meas_cap = 0;
   char* d_sched = nullptr;  // scheduler scratch (sched_layout) + the per-tile inputs
   size_t sched_cap = 0;
-  int32_t* h_totals = nullptr;  // pinned: block and split counts of the last schedule
+  int32_t h_totals[4] = {0, 0, 0, 0};  // block and split counts of the last schedule (12 bytes read back)
   std::vector<unsigned long long> masks_host;  // per local tile primary-ray masks
   unsigned long long* d_masks = nullptr;       // (inside d_sched)
   int32_t stage_bytes = 0;  // scene prefix staged into LDS per workgroup (0 = none)
@@ -157,6 +157,7 @@ struct rt_context {
   std::shared_ptr<const PartitionData> part;
   int32_t* d_part = nullptr;
   size_t d_part_cap = 0;
+  double bvh_seconds = 0;  // host time of the last BVH build (rt_stats.bvh_build_seconds)
   // per-kernel device time of the wavefront path (rt_context_profile): an
   // event pool, the blocks of it the last frame recorded ({first event,
   // first class, last class}) and the totals
@@ -229,6 +230,8 @@ static const int32_t* dev_tiles(const rt_context* c, int w, int h, int rank, int
 
 namespace rtgo {
 bool context_has_bvh(const rt_context* c) { return c && !c->flat.bvh.empty(); }
+double context_bvh_seconds(const rt_context* c) { return c ? c->bvh_seconds : 0.0; }
+void* context_stream(const rt_context* c) { return c ? (void*)c->stream : nullptr; }
 }  // namespace rtgo
 
 extern "C" {
@@ -281,8 +284,6 @@ int rt_context_create(int32_t device, rt_context** out) {
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
-  if (e == hipSuccess) e = hipMalloc((void**)&c->d_counts, kCountSlots * sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_totals, 4 * sizeof(int32_t), hipHostMallocDefault);
 
   if (e != hipSuccess) {
     set_error(std::string("context init failed: ") + hipGetErrorString(e));
@@ -296,21 +297,14 @@ int rt_context_create(int32_t device, rt_context** out) {
 void rt_context_destroy(rt_context* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  // the last render (on the caller's stream) and the context's own stream
+  // must be done before the buffers go back to the cache
+  if (c->have_timing) (void)hipEventSynchronize(c->ev1);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->d_scene) (void)hipFree(c->d_scene);
-  if (c->d_counts) (void)hipFree(c->d_counts);
-
-  if (c->d_blocks) (void)hipFree(c->d_blocks);
-  if (c->d_pilot) (void)hipFree(c->d_pilot);
-  if (c->d_acc) (void)hipFree(c->d_acc);
-  if (c->d_meas) (void)hipFree(c->d_meas);
-  if (c->d_split) (void)hipFree(c->d_split);
-  if (c->d_sched) (void)hipFree(c->d_sched);
-  if (c->d_part) (void)hipFree(c->d_part);
-  if (c->h_totals) (void)hipHostFree(c->h_totals);
-  if (c->wf_mem) (void)hipFree(c->wf_mem);
-  if (c->wf_rad) (void)hipFree(c->wf_rad);
-  if (c->wf_ctl) (void)hipFree(c->wf_ctl);
+  for (void* p : {(void*)c->d_scene, (void*)c->d_counts, (void*)c->d_blocks, (void*)c->d_pilot, c->d_acc,
+                  (void*)c->d_meas, (void*)c->d_split, (void*)c->d_sched, (void*)c->d_part, c->wf_mem, c->wf_rad,
+                  (void*)c->wf_ctl})
+    dev_free(p);
   if (c->wf_host) (void)hipHostFree(c->wf_host);
   for (hipEvent_t& e : c->wf_ev)
     if (e) (void)hipEventDestroy(e);
@@ -338,6 +332,7 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   if (rc) return rc;
   HIP_TRY(hipSetDevice(c->device));
   flatten_scene(*s, &c->flat);
+  c->bvh_seconds = 0;
   const bool want_bvh = force_bvh > 0 || (force_bvh == 0 && c->flat.spheres.size() > 64);
   if (want_bvh && !c->flat.tris.empty()) {
     if (force_bvh > 0) {
@@ -345,7 +340,9 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
       return RT_E_INVALID;
     }
   } else if (want_bvh) {
+    const auto t0 = std::chrono::steady_clock::now();
     build_sphere_bvh(&c->flat, c->tun.bvh_bins, c->tun.bvh_leaf);
+    c->bvh_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
   const FlatScene& f = c->flat;
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -362,11 +359,11 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   rc = quiesce(c);  // the last render may still read the scene
   if (rc) return rc;
   if (c->d_scene && c->d_scene_bytes < total) {
-    HIP_TRY(hipFree(c->d_scene));
+    dev_free(c->d_scene);
     c->d_scene = nullptr;
   }
   if (!c->d_scene) {
-    HIP_TRY(hipMalloc(&c->d_scene, total));
+    HIP_TRY((hipError_t)dev_alloc(&c->d_scene, total));
     c->d_scene_bytes = total;
   }
   char* base = (char*)c->d_scene;
@@ -431,10 +428,10 @@ static size_t split_flags_bytes(int nsplit, int spp) {
 static int grow(void* ptr, size_t* cap, size_t n) {
   void** p = (void**)ptr;
   if (n <= *cap) return RT_OK;
-  if (*p) HIP_TRY(hipFree(*p));
+  dev_free(*p);
   *p = nullptr;
   *cap = 0;
-  HIP_TRY(hipMalloc(p, n));
+  HIP_TRY((hipError_t)dev_alloc(p, n));
   *cap = n;
   return RT_OK;
 }
@@ -749,14 +746,14 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   if (need > c->wf_mem_bytes) {
     int rq = quiesce(c);
     if (rq) return rq;
-    if (c->wf_mem) HIP_TRY(hipFree(c->wf_mem));
+    dev_free(c->wf_mem);
     c->wf_mem = nullptr;
     c->wf_mem_bytes = 0;
-    HIP_TRY(hipMalloc(&c->wf_mem, need));
+    HIP_TRY((hipError_t)dev_alloc(&c->wf_mem, need));
     c->wf_mem_bytes = need;
   }
   if (!c->wf_ctl) {
-    HIP_TRY(hipMalloc((void**)&c->wf_ctl, sizeof(WfCtl)));
+    HIP_TRY((hipError_t)dev_alloc((void**)&c->wf_ctl, sizeof(WfCtl)));
     HIP_TRY(hipHostMalloc((void**)&c->wf_host, kWfRing * sizeof(WfCtl), hipHostMallocDefault));
     for (hipEvent_t& e : c->wf_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
@@ -764,10 +761,10 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   if (rad_need > c->wf_rad_bytes) {
     int rq = quiesce(c);
     if (rq) return rq;
-    if (c->wf_rad) HIP_TRY(hipFree(c->wf_rad));
+    dev_free(c->wf_rad);
     c->wf_rad = nullptr;
     c->wf_rad_bytes = 0;
-    HIP_TRY(hipMalloc(&c->wf_rad, rad_need));
+    HIP_TRY((hipError_t)dev_alloc(&c->wf_rad, rad_need));
     c->wf_rad_bytes = rad_need;
   }
   WfParams p;
@@ -920,6 +917,7 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   base_params(c, w, h, st, rank, world, layout, &p);
   p.out_linear = d_linear;
   p.out_rgba = d_rgba;
+  if (counts && !c->d_counts) HIP_TRY((hipError_t)dev_alloc((void**)&c->d_counts, kCountSlots * sizeof(unsigned long long)));
   p.counts = counts ? c->d_counts : nullptr;
   // the caller's stream, as given (NULL = the legacy default stream); a
   // render enqueued on another stream than this context's last one waits for
@@ -1070,10 +1068,10 @@ int rt_partition_balanced(rt_context* c, int32_t w, int32_t h, const rt_settings
   const size_t o_tw = o_pilot + al(npx * 24);
   const size_t total = o_tw + al((size_t)ntiles * sizeof(float));
   char* buf = nullptr;
-  HIP_TRY(hipMalloc((void**)&buf, total));
+  HIP_TRY((hipError_t)dev_alloc((void**)&buf, total));
   auto fail = [&](int code) {
     (void)hipStreamSynchronize(s);
-    (void)hipFree(buf);
+    dev_free(buf);
     return code;
   };
   std::vector<float> work(ntiles, 0.0f);

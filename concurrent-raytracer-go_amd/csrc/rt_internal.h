@@ -14,6 +14,12 @@ namespace rtgo {
 
 void set_error(const std::string& msg);
 
+// Device memory through a per-device cache of freed blocks (dev_pool.cpp):
+// hipMalloc / hipFree semantics (hipError_t as int), the block must no longer
+// be in use by any stream when it is freed.
+int dev_alloc(void** p, size_t n);
+void dev_free(void* p);
+
 // ---------------------------------------------------------------- scene
 struct FlatScene {
   std::vector<DSphere> spheres;
@@ -287,6 +293,8 @@ void finish_partition(PartitionData* d);
 void lpt_partition(const std::vector<float>& work, PartitionData* d);
 rt_partition* make_partition(PartitionData&& d);
 bool context_has_bvh(const rt_context* c);
+double context_bvh_seconds(const rt_context* c);
+void* context_stream(const rt_context* c);  // its own non-blocking stream (hipStream_t)
 const PartitionData& partition_data(const rt_partition* p);
 
 // ---------------------------------------------------------------- output

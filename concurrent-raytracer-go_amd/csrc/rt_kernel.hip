@@ -543,6 +543,81 @@ __device__ __forceinline__ bool solo_closest(const Geo& g, d3 o, d3 d, HitSel& h
   return found;
 }
 
+// ---- parallel direct lighting of a lone path (solo_lights)
+// The tries of a bounce's random stream, evaluated ahead: try k of the
+// stream whose state is x uses draws 3k, 3k+1, 3k+2 (RandomVec3InUnitSphere,
+// vector.go:132-139); lane h holds tries h and 64 + h.  The soft shadows of
+// calculateSmartShadow take their points from this stream in light order
+// (each light whose hard ray is clear: the next 16 accepted tries), so the
+// tries of every light are known once the hard rays are, and all lights'
+// soft rays can be traced at once.  The scatter draws follow them.
+struct SoloTries {
+  uint32_t a0, a1, a2, b0, b1, b2;  // the draws of tries h and 64 + h
+  unsigned long long ma, mb;        // accepted tries 0..63 / 64..127 (wave-uniform)
+};
+__device__ __forceinline__ SoloTries solo_tries(uint64_t x, uint64_t jA, uint64_t jC, uint64_t jA64, uint64_t jC64) {
+  SoloTries t;
+  uint64_t s = jA * x + jC;  // state before draw 3h
+  t.a0 = rt_pcg_out(s);
+  s = s * RT_PCG_MULT + RT_PCG_INC;
+  t.a1 = rt_pcg_out(s);
+  s = s * RT_PCG_MULT + RT_PCG_INC;
+  t.a2 = rt_pcg_out(s);
+  s = jA * (jA64 * x + jC64) + jC;  // state before draw 3(64 + h)
+  t.b0 = rt_pcg_out(s);
+  s = s * RT_PCG_MULT + RT_PCG_INC;
+  t.b1 = rt_pcg_out(s);
+  s = s * RT_PCG_MULT + RT_PCG_INC;
+  t.b2 = rt_pcg_out(s);
+  t.ma = __ballot(unit_ball_accept(t.a0, t.a1, t.a2));
+  t.mb = __ballot(unit_ball_accept(t.b0, t.b1, t.b2));
+  return t;
+}
+// The index after the 16th accepted try at or after `from` (< 128), or -1
+// when the 128 evaluated tries do not hold 16 more (wave-uniform).
+// position of the n-th set bit (n >= 1) of m, which has at least n
+__device__ __forceinline__ int nth_set_bit(unsigned long long m, int n) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const int c = __popcll(m & ((1ull << w) - 1ull));
+    if (n > c) {
+      n -= c;
+      m >>= w;
+      pos += w;
+    }
+  }
+  return pos;
+}
+__device__ __forceinline__ int solo_take16(const SoloTries& t, int from) {
+  // tries [from, 64) of ma, then [max(from, 64), 128) of mb
+  const unsigned long long a = from < 64 ? t.ma >> from : 0ull;
+  const int ca = __popcll(a);
+  if (ca >= 16) return from + nth_set_bit(a, 16) + 1;
+  const int fb = from > 64 ? from - 64 : 0;
+  const unsigned long long b = t.mb >> fb;
+  if (ca + __popcll(b) < 16) return -1;
+  return 64 + fb + nth_set_bit(b, 16 - ca) + 1;
+}
+
+// RT_WG_TIMING builds: s_memtime clocks of a lone path's bounce by section
+// (solo_clk[k], wave-uniform; scripts/latency_probe.py PROBE_SECTIONS):
+// 0 loop top + closest hit, 1 hit record, 2 stream tries + light vectors +
+// cones + hard rays, 3 soft rays, 4 lighting terms, 5 scatter, 6 bounces.
+#ifdef RT_WG_TIMING
+__shared__ unsigned long long solo_clk[8];
+#define SOLO_T(k)                                          \
+  do {                                                     \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    solo_clk[k] += now_ - solo_t0;                         \
+    solo_t0 = now_;                                        \
+  } while (0)
+#else
+#define SOLO_T(k) \
+  do {            \
+  } while (0)
+#endif
+
 // The path of lane `ow`, run to its end by the whole wave: its radiance.
 template <bool kSky>
 __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t rx, int depth, int* stack) {
@@ -554,13 +629,37 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
   rt_rng rng{rl64(rx, ow)};
   depth = (int)rl32((uint32_t)depth, ow);
   Counters c;
+#ifdef RT_WG_TIMING
+  unsigned long long solo_t0 = __builtin_amdgcn_s_memtime();
+#endif
+  // the parallel lighting form (solo_lights): sphere-only scenes with one or
+  // two lights, a (light, sphere) pair per lane
+  bool par;
+  // jump coefficients of try `lane` and of try 64 (solo_tries), held in
+  // VGPRs for the lone path's bounces (the state at any try k < 64 of the
+  // stream is then a readlane away: no memory access per bounce)
+  uint64_t jA, jC, jA64, jC64;
+  {
+    const Hot h0 = hot<true>();
+    par = h0.g.nt == 0 && h0.nl >= 1 && h0.nl <= 2 && h0.nl * h0.g.ns <= 64;
+    jA = h0.jump[2 * lane];
+    jC = h0.jump[2 * lane + 1];
+    jA64 = h0.jump[128];
+    jC64 = h0.jump[129];
+    asm volatile("" : "+v"(jA64), "+v"(jC64));
+  }
   for (;;) {
     const Hot h = hot<true>();
     const Geo& g = h.g;
     if (depth >= h.max_depth) return L;  // traceRay depth cut-off: contributes 0
+#ifdef RT_WG_TIMING
+    solo_clk[6] += 1;
+#endif
     // (1) closest hit (hitWorld, renderer.go:170)
     HitSel hs;
-    if (!solo_closest(g, o, d, hs)) {  // miss -> black (or the opted-in sky)
+    const bool found = solo_closest(g, o, d, hs);
+    SOLO_T(0);
+    if (!found) {  // miss -> black (or the opted-in sky)
       if constexpr (kSky) L = L + mul(T, sky_color(fresh()->sky, d));
       return L;
     }
@@ -587,9 +686,137 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
       mi = T0.mat;
       self = T0.obj;
     }
-    // (2) calculateDirectLighting (renderer.go:229-297), light by light
+    SOLO_T(1);
+    // (2) calculateDirectLighting (renderer.go:229-297)
     const DMat* __restrict__ m = h.mats + mi;
     d3 D = mk(m->ambient, m->ambient, m->ambient);
+    if (par) {
+      // every light at once: lane li (< nl) its light vector; lane
+      // li * ns + s the pair (light li, sphere s) for the shadow cone and the
+      // hard ray; then all lights' soft rays from the tries; then the
+      // lighting terms per lane li, added to D in light order (the same
+      // operations and sums as the loop below, so the same bits)
+      const int nl = h.nl, ns = g.ns;
+      // this bounce's stream tries (jump entry 64 read at use: uniform)
+      SoloTries tr{};
+      if (h.soft) tr = solo_tries(rng.x, jA, jC, jA64, jC64);
+      d3 lvd = mk(0, 0, 0);
+      double lvl = 0;
+      if (lane < nl) {
+        const d3 lv = ld3(h.lights[lane].pos) - P;
+        lvl = sqrt(lv.x * lv.x + lv.y * lv.y + lv.z * lv.z);
+        lvd = lvl == 0 ? mk(0, 0, 0) : divs(lv, lvl);
+      }
+      // (light values move across lanes by shuffles where they are used: held
+      // as wave-uniform values they would take SGPRs the bounce loop needs)
+      const unsigned long long litm = __ballot(lane < nl && !(lvl < 0.001));
+      const int lj = lane >= ns ? 1 : 0, sj = lane - lj * ns;  // this lane's pair
+      const d3 ldj = mk(__shfl(lvd.x, lj), __shfl(lvd.y, lj), __shfl(lvd.z, lj));
+      const double dlj = __shfl(lvl, lj);
+      bool cone = false, blk = false;
+      if (lane < nl * ns && ((litm >> lj) & 1ull)) {
+        const DSphere& S = g.spheres[sj];
+        const bool self_out = front && dot(N, ldj) >= KC(0.1015);
+        cone = !(self_out && S.obj == self && S.r > 0) && in_cone(S.c, S.r, P, ldj, dlj);
+        if (cone) {
+          const double a = len2(ldj);
+          double num;
+          blk = sphere_query(S, P, ldj, a, approx_rcp(a), 0.001, dlj, num) != 0;
+        }
+      }
+      const unsigned long long cones = __ballot(cone), blks = __ballot(blk);
+      const unsigned long long sm = ns >= 64 ? ~0ull : (1ull << ns) - 1ull;
+      const unsigned long long cm0 = cones & sm, cm1 = (cones >> ns) & sm;
+      const bool lit0 = litm & 1ull, lit1 = (litm >> 1) & 1ull;
+      const bool occ0 = (blks & sm) != 0, occ1 = ((blks >> ns) & sm) != 0;
+      const bool need0 = lit0 && !occ0 && h.soft, need1 = lit1 && !occ1 && h.soft;
+      // soft rays: light 0 takes the 16 accepted tries from try 0, light 1 the
+      // 16 after those (a light without soft rays draws nothing)
+      const int e0 = need0 ? solo_take16(tr, 0) : 0;
+      const int e1 = need1 && e0 >= 0 ? solo_take16(tr, e0) : e0;
+      SOLO_T(2);
+      int un0 = 16, un1 = 16;
+      if (e0 >= 0 && e1 >= 0) {
+        int cnt0 = 0, cnt1 = 0;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {  // try lane, then try 64 + lane
+          const int k = lane + 64 * half;
+          const bool acc = ((half ? tr.mb : tr.ma) >> lane) & 1ull;
+          const bool in0 = need0 && k < e0, in1 = need1 && k >= e0 && k < e1;
+          const int li = in1 ? 1 : 0;
+          const d3 lD = mk(__shfl(lvd.x, li), __shfl(lvd.y, li), __shfl(lvd.z, li));
+          const double lT = __shfl(lvl, li);
+          bool occ = false;
+          if (acc && (in0 || in1)) {
+            const d3 pt = half ? unit_ball_point(tr.b0, tr.b1, tr.b2) : unit_ball_point(tr.a0, tr.a1, tr.a2);
+            const d3 sd = normalize(lD + muls(pt, 0.1));
+            const double a = len2(sd);
+            const double ia = approx_rcp(a);
+            // (every candidate, no early exit: their loads issue together)
+            for (unsigned long long b = in1 ? cm1 : cm0; b; b &= b - 1) {
+              double num;
+              occ = (sphere_query(g.spheres[__builtin_ctzll(b)], P, sd, a, ia, 0.001, lT, num) != 0) || occ;
+            }
+          }
+          cnt0 += __popcll(__ballot(acc && in0 && !occ));
+          cnt1 += __popcll(__ballot(acc && in1 && !occ));
+        }
+        un0 = cnt0;
+        un1 = cnt1;
+        // the stream continues after the last try the lights took
+        const int used = e1;
+        if (used > 0) {  // the state before draw 3 used: jumps by 64 tries, then by used mod 64
+          uint64_t xb = rng.x;
+          for (int k = used; k >= 64; k -= 64) xb = rl64(jA64, 0) * xb + rl64(jC64, 0);
+          const int u = used & 63;
+          rng.x = rl64(jA, u) * xb + rl64(jC, u);
+        }
+      } else {
+        // (the 128 tries did not hold them: the lights' soft rays one light
+        // after the other from the stream, as below)
+        for (int li = 0; li < 2; ++li) {
+          if (!(li ? need1 : need0)) continue;
+          const Cand cl{li ? cm1 : cm0, 0ull};
+          const CoopOut r = soft_coop<false>(g, true, cl.s != 0, P, rl3(lvd, li), rld(lvl, li), cl, rng.x, h.jump,
+                                             stack, c);
+          (li ? un1 : un0) = r.unocc;
+          rng.x = r.x;
+        }
+      }
+      SOLO_T(3);
+      // the lighting terms of light lane (< nl), then D in light order
+      d3 tdif = mk(0, 0, 0), tspec = mk(0, 0, 0);
+      const double metallic = m->metallic;
+      if (lane < nl) {
+        const bool occ = lane ? occ1 : occ0;
+        const int un = lane ? un1 : un0;
+        const double sf = occ ? 0.0 : (h.soft ? (double)un / 16.0 : 1.0);  // shadowSum / 16
+        const DLight& Lt = h.lights[lane];
+        const double cos_t = gmax0(dot(N, lvd));
+        const double intensity = cos_t * Lt.intensity / (lvl * lvl);
+        tdif = muls(ld3(m->albedo), m->diffuse_strength * intensity * sf);
+        if (metallic > 0.5) {
+          const d3 view = normalize(neg(P));
+          const d3 half = normalize(lvd + view);
+          const double hc = gmax0(dot(N, half));
+          const int sp = m->spec_pow;
+          const double si = sp == 64 ? pow_n<64>(hc) : (sp == 48 ? pow_n<48>(hc) : pow_n<32>(hc));
+          tspec = muls(ld3(Lt.color), si * intensity * sf * metallic * 3.0);
+        }
+      }
+#pragma unroll
+      for (int li = 0; li < 2; ++li) {
+        if (li >= nl) break;
+        const bool lit = li ? lit1 : lit0, occ = li ? occ1 : occ0;
+        const int un = li ? un1 : un0;
+        const double sf = occ ? 0.0 : (h.soft ? (double)un / 16.0 : 1.0);
+        if (lit && sf > 0.0) {
+          D = D + rl3(tdif, li);
+          if (metallic > 0.5) D = D + rl3(tspec, li);
+        }
+      }
+      SOLO_T(4);
+    } else
     for (int li = 0; li < h.nl; ++li) {
       const DLight& Lt = h.lights[li];
       const d3 lv = ld3(Lt.pos) - P;
@@ -653,6 +880,7 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
     // (3) Material.Scatter and the traceRay combination (renderer.go:181-226)
     const d3 E = ld3(m->emit);
     const Scat sc = scatter<false>(m, d, N, front, rng, c);
+    SOLO_T(5);
     if (!sc.ok) return L + mul(T, E + D);
     L = L + mul(T, E + muls(D, m->dw));
     if (!h.recursive || depth + 1 >= h.max_depth) return L;
@@ -731,6 +959,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     for (int i = 0; i < kCounters; ++i) c.v[i] = culled.v[i] = 0;
   }
 #ifdef RT_WG_TIMING
+  if (lane < 8) solo_clk[lane] = 0;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   unsigned long long dbg_iter = 0;
   // wave-uniform section clocks (s_memtime): hit, lighting, soft; phase 1 (visibility)
@@ -1340,6 +1569,8 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       r[32 + i] = dbg_bclk[i];
       r[37 + i] = dbg_bcnt[i];
     }
+    if (solo_clk[6])  // a lone path ran: its section clocks replace the iteration stamps
+      for (int i = 0; i < 8; ++i) r[16 + i] = solo_clk[i];
   }
 #endif
 }

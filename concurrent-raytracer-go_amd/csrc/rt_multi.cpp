@@ -53,7 +53,7 @@ struct Rank {
   int device = 0;
   int comm_idx = 0;             // index of its device in the distinct-device list (0: the root device)
   rt_context* ctx = nullptr;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // its context's own stream
   hipEvent_t done = nullptr;    // its share is rendered
   void* share = nullptr;        // its own share buffer (devices other than the root's)
   size_t share_cap = 0;
@@ -66,17 +66,17 @@ struct DevBuf {
   int grow(int device, size_t bytes) {
     if (bytes <= cap) return RT_OK;
     HIP_TRY(hipSetDevice(device));
-    if (p) HIP_TRY(hipFree(p));
+    dev_free(p);
     p = nullptr;
     cap = 0;
-    HIP_TRY(hipMalloc(&p, bytes));
+    HIP_TRY((hipError_t)dev_alloc(&p, bytes));
     cap = bytes;
     return RT_OK;
   }
   void release(int device) {
     if (p) {
       (void)hipSetDevice(device);
-      (void)hipFree(p);
+      dev_free(p);
     }
     p = nullptr;
     cap = 0;
@@ -289,8 +289,8 @@ int rt_renderer_create(const int32_t* devices, int32_t n, rt_renderer** out) {
     if (it == r->devices.end()) r->devices.push_back(d);
     int rc = rt_context_create(d, &q.ctx);
     if (rc) return renderer_fail_cleanup(r, rc);
-    if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&q.done, hipEventDisableTiming) != hipSuccess) {
+    q.stream = (hipStream_t)context_stream(q.ctx);  // the rank renders on its context's own stream
+    if (hipSetDevice(d) != hipSuccess || hipEventCreateWithFlags(&q.done, hipEventDisableTiming) != hipSuccess) {
       set_error("rt_renderer_create: stream / event creation failed");
       return renderer_fail_cleanup(r, RT_E_DEVICE);
     }
@@ -328,10 +328,9 @@ void rt_renderer_destroy(rt_renderer* r) {
   r->img_rgba.release(root);
   for (Rank& q : r->ranks) {
     (void)hipSetDevice(q.device);
-    if (q.share) (void)hipFree(q.share);
+    dev_free(q.share);
     if (q.done) (void)hipEventDestroy(q.done);
-    if (q.stream) (void)hipStreamDestroy(q.stream);
-    rt_context_destroy(q.ctx);
+    rt_context_destroy(q.ctx);  // (and its stream, the rank's)
   }
   delete r;
 }
@@ -364,16 +363,19 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
   // scene upload (flatten + BVH) only when its content changed
   std::vector<uint8_t> key;
   scene_bytes(*scene, &key);
+  double bvh_s = 0;
   if (!r->have_scene || key != r->scene_key) {
     r->have_scene = false;
     for (Rank& q : r->ranks) {
       int rc = rt_context_set_scene(q.ctx, scene, 0);
       if (rc) return rc;
+      bvh_s += context_bvh_seconds(q.ctx);
     }
     r->scene_key.swap(key);
     r->have_scene = true;
     r->scene_gen += 1;
   }
+  const double t_scene = now_s();
   const size_t npix = (size_t)w * h;
   rc = r->img_lin.grow(root, npix * 3 * sizeof(float));
   if (!rc) rc = r->img_rgba.grow(root, npix * 4);
@@ -398,10 +400,10 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
       } else {
         if (share > q.share_cap) {
           HIP_TRY(hipSetDevice(q.device));
-          if (q.share) HIP_TRY(hipFree(q.share));
+          dev_free(q.share);
           q.share = nullptr;
           q.share_cap = 0;
-          HIP_TRY(hipMalloc(&q.share, share));
+          HIP_TRY((hipError_t)dev_alloc(&q.share, share));
           q.share_cap = share;
         }
         bufs[k] = (uint8_t*)q.share;
@@ -449,6 +451,7 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
     if (rc) return rc;
   }
   HIP_TRY(hipSetDevice(root));
+  const double t_launch = now_s();
   if (out_linear)
     HIP_TRY(hipMemcpyAsync(out_linear, r->img_lin.p, npix * 3 * sizeof(float), hipMemcpyDeviceToHost, root_s));
   if (out_rgba) HIP_TRY(hipMemcpyAsync(out_rgba, r->img_rgba.p, npix * 4, hipMemcpyDeviceToHost, root_s));
@@ -464,10 +467,17 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
     r->rank_secs[k] = s;
     ks = std::max(ks, s);
   }
-  const double secs = now_s() - t0;
+  const double t_end = now_s();
+  const double secs = t_end - t0;
   if (stats) {
     memset(stats, 0, sizeof *stats);
     stats->render_seconds = secs;
+    stats->scene_seconds = t_scene - t0;
+    stats->bvh_build_seconds = bvh_s;
+    stats->launch_seconds = t_launch - t_scene;
+    // (the copies wait for the kernels: this is the time after the launches
+    // were enqueued until the image was on the host, kernels included)
+    stats->download_seconds = t_end - t_launch;
     stats->kernel_seconds = ks;
     stats->rays_per_second = (double)npix * st->samples / secs;
     stats->pixels_per_second = (double)npix / secs;
@@ -485,9 +495,13 @@ int rt_render(const rt_scene* scene, int32_t w, int32_t h, const rt_settings* st
   rt_renderer* r = nullptr;
   rc = rt_renderer_create(nullptr, std::max(1, st->num_devices), &r);
   if (rc) return rc;
+  const double t_created = now_s();
   rc = rt_renderer_render(r, scene, w, h, st, out_linear, out_rgba, stats);
+  const double t_rendered = now_s();
   rt_renderer_destroy(r);
   if (!rc && stats) {  // Go's Render time covers everything (renderer.go:68,101)
+    stats->create_seconds = t_created - t0;
+    stats->destroy_seconds = now_s() - t_rendered;
     stats->render_seconds = now_s() - t0;
     stats->rays_per_second = (double)w * h * st->samples / stats->render_seconds;
     stats->pixels_per_second = (double)w * h / stats->render_seconds;

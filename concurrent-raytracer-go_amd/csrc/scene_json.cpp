@@ -571,6 +571,8 @@ static std::string go_vec(const double v[3]) {
 
 extern "C" {
 
+int rt_scene_print_hittables(const rt_scene_buf* b);
+
 int rt_scene_parse_json(const char* text, size_t len, int32_t verbose, rt_scene_buf** out) {
   if (!out || (!text && len)) {
     set_error("invalid arguments");
@@ -600,7 +602,10 @@ int rt_scene_parse_json(const char* text, size_t len, int32_t verbose, rt_scene_
   sb->view.num_objects = (int32_t)sb->objects.size();
   sb->view.lights = sb->lights.data();
   sb->view.num_lights = (int32_t)sb->lights.size();
-  (void)verbose;
+  // verbose: the lines GetHittables prints when Render flattens the scene
+  // (scene.go:62-88); a cgo caller that parses inside its Render wants them
+  // here (go/internal/renderer/gpu.go)
+  if (verbose) rt_scene_print_hittables(sb.get());
   *out = sb.release();
   return RT_OK;
 }

@@ -156,6 +156,12 @@ class Stats(ctypes.Structure):
         ("pixels_per_second", ctypes.c_double),
         ("objects", ctypes.c_int32),
         ("lights", ctypes.c_int32),
+        ("create_seconds", ctypes.c_double),
+        ("scene_seconds", ctypes.c_double),
+        ("bvh_build_seconds", ctypes.c_double),
+        ("launch_seconds", ctypes.c_double),
+        ("download_seconds", ctypes.c_double),
+        ("destroy_seconds", ctypes.c_double),
     ]
 
 
@@ -250,6 +256,7 @@ EXPORTED_SYMBOLS = [
     "rt_context_kernel_seconds",
     "rt_context_render_frames_async",
     "rt_unpack_partition_frames_async",
+    "rt_release_cached_memory",
 ]
 
 _lib = None
@@ -344,6 +351,7 @@ def lib():
              ctypes.POINTER(vp), ctypes.POINTER(vp), vp],
         ),
         "rt_unpack_partition_frames_async": (ctypes.c_int, [vp, i32, vp, vp, vp, vp]),
+        "rt_release_cached_memory": (ctypes.c_int, []),
         "rt_context_kernel_seconds": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
                                                      ctypes.POINTER(ctypes.c_int64)]),
     }

@@ -150,6 +150,19 @@ typedef struct {
   double pixels_per_second; /* W*H / render_seconds (README.md:60) */
   int32_t objects;          /* len(hittables): a cube counts as one (renderer.go:109) */
   int32_t lights;
+  /* Where render_seconds went (host wall clock): device state created
+   * (rt_render only: contexts, streams, RCCL), scene flattened and uploaded
+   * (0 when the renderer already holds it), of which building the BVH (the
+   * published benchmark JSON's bvh_build_time / setup_time), the launches
+   * enqueued (with a new work schedule: the pilot render and the scheduler,
+   * DESIGN.md §4.1), the image copied to the host after the kernels, and
+   * the device state freed again (rt_render only). */
+  double create_seconds;
+  double scene_seconds;
+  double bvh_build_seconds;
+  double launch_seconds;
+  double download_seconds;
+  double destroy_seconds;
 } rt_stats;
 
 /* Per-launch operation counts (for the roofline's algorithmic FLOPs). */
@@ -178,6 +191,10 @@ typedef struct {
 } rt_counts;
 
 void rt_settings_default(rt_settings* s);
+/* The library keeps device buffers freed by destroyed contexts and renderers
+ * for reuse (rt_render creates and frees its device state every call); this
+ * returns them to the device. */
+int rt_release_cached_memory(void);
 int32_t rt_abi_version(void);
 const char* rt_last_error(void);
 

@@ -17,7 +17,7 @@ for k in rt_kernel rt_wavefront rt_schedule; do
 done
 wait
 OBJS="$OUT/rt_kernel.o $OUT/rt_wavefront.o $OUT/rt_schedule.o"
-for o in rt_api scene_json image_io bvh schedule rt_multi scene_flat; do OBJS="$OBJS build/$o.o"; done
+for o in rt_api scene_json image_io bvh schedule rt_multi scene_flat dev_pool; do OBJS="$OBJS build/$o.o"; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/librtgo.so" $OBJS -L/opt/rocm/lib -lrccl -lz \
   -Wl,-soname,librtgo.so -Wl,-rpath,/opt/rocm/lib
 echo "$OUT/librtgo.so"

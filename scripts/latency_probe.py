@@ -66,7 +66,7 @@ if os.environ.get("PROBE_SECTIONS"):  # with an RT_WG_TIMING build (RTGO_LIB): s
         ctx.set_scene(sc)
         st = rtgo.default_settings()
         st.samples, st.max_depth, st.soft_shadows = 1, 51, soft
-        dbg = torch.zeros(64 * 48, dtype=torch.int64, device="cuda")
+        dbg = torch.zeros(4096 * 48, dtype=torch.int64, device="cuda")
         ctx.set_debug_buffer(dbg.data_ptr())
         lin = torch.zeros(W * 3, dtype=torch.float32, device="cuda")
         rgba = torch.zeros(W * 4, dtype=torch.uint8, device="cuda")
@@ -75,12 +75,19 @@ if os.environ.get("PROBE_SECTIONS"):  # with an RT_WG_TIMING build (RTGO_LIB): s
             ctx.render_async(W, 1, st, lin.data_ptr(), rgba.data_ptr(), torch.cuda.current_stream().cuda_stream)
             torch.cuda.synchronize()
         d = dbg.cpu().numpy().reshape(-1, 48)
-        d = d[d[:, 0] != 0]
+        d = d[(d[:, 0] != 0) & ((d[:, 22] != 0) | (d[:, 7] > 1))]  # the block that ran the path
         for r in d:
             it = max(int(r[7]), 1)
             print(f"W={W} {name:16s} wave {(r[2] - r[0]) / 100.0:7.1f} us, iters {it}, clocks/iter: hit {r[3] / it:6.0f}"
                   f" light {r[4] / it:6.0f} (cone+hard {r[8] / it:6.0f}, soft {r[5] / it:6.0f}) scatter {r[9] / it:6.0f}"
                   f" fill {r[6]:6.0f}", flush=True)
+            nb = int(r[22])
+            if nb:  # a lone path ran (solo_path): its section clocks per bounce (s_memtime: shader clocks)
+                names = ["loop+closest hit", "hit record", "tries+light vecs+cones+hard", "soft rays",
+                         "lighting terms", "scatter"]
+                print(f"   solo_path, {nb} bounces, clocks per bounce: " +
+                      ", ".join(f"{n} {r[16 + k] / nb:6.0f}" for k, n in enumerate(names)) +
+                      f"; total {sum(r[16:22]) / nb:6.0f}", flush=True)
         ctx.close()
     sys.exit(0)
 
