@@ -10,7 +10,8 @@
 // the next allocation of a similar size on the same device instead; at most
 // kCacheCap bytes per device stay cached, and rt_release_cached_memory()
 // returns them all.  Callers free a block only when no stream still uses it
-// (a context waits for its last render first).
+// (a context waits for its last render first).  Idle streams and events of
+// destroyed contexts are kept the same way.
 #include <hip/hip_runtime_api.h>
 
 #include <map>
@@ -34,6 +35,8 @@ struct Pool {
 
 std::mutex g_mu;
 std::map<int, Pool> g_pools;
+std::map<int, std::vector<hipStream_t>> g_streams;  // idle non-blocking streams per device
+std::map<int, std::vector<hipEvent_t>> g_events;    // idle timing events per device
 std::unordered_map<void*, std::pair<int, size_t>> g_live;  // block -> (device, size)
 
 size_t round_up(size_t n) { return ((n + kGrain - 1) / kGrain) * kGrain; }
@@ -97,6 +100,56 @@ void dev_free(void* p) {
   (void)hipSetDevice(cur);
 }
 
+// Streams and events of destroyed contexts, kept for the next context on the
+// same device (creating and destroying them cost ~0.1-0.2 ms per rt_render).
+int dev_stream_get(hipStream_t* s) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  {
+    std::lock_guard<std::mutex> lock(g_mu);
+    auto& v = g_streams[dev];
+    if (!v.empty()) {
+      *s = v.back();
+      v.pop_back();
+      return hipSuccess;
+    }
+  }
+  return (int)hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
+void dev_stream_put(hipStream_t s) {  // (idle: the caller synchronized it)
+  if (!s) return;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  std::lock_guard<std::mutex> lock(g_mu);
+  g_streams[dev].push_back(s);
+}
+
+int dev_event_get(hipEvent_t* ev) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  {
+    std::lock_guard<std::mutex> lock(g_mu);
+    auto& v = g_events[dev];
+    if (!v.empty()) {
+      *ev = v.back();
+      v.pop_back();
+      return hipSuccess;
+    }
+  }
+  return (int)hipEventCreate(ev);
+}
+
+void dev_event_put(hipEvent_t ev) {  // (complete: the caller waited for it)
+  if (!ev) return;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  std::lock_guard<std::mutex> lock(g_mu);
+  g_events[dev].push_back(ev);
+}
+
 }  // namespace rtgo
 
 extern "C" int rt_release_cached_memory(void) {
@@ -109,11 +162,30 @@ extern "C" int rt_release_cached_memory(void) {
       dp.second.cached = 0;
     }
   }
+  std::vector<std::pair<int, hipStream_t>> streams;
+  std::vector<std::pair<int, hipEvent_t>> events;
+  {
+    std::lock_guard<std::mutex> lock(rtgo::g_mu);
+    for (auto& ds : rtgo::g_streams)
+      for (hipStream_t s : ds.second) streams.emplace_back(ds.first, s);
+    for (auto& de : rtgo::g_events)
+      for (hipEvent_t e : de.second) events.emplace_back(de.first, e);
+    rtgo::g_streams.clear();
+    rtgo::g_events.clear();
+  }
   int cur = 0;
   (void)hipGetDevice(&cur);
   for (auto& b : blocks) {
     (void)hipSetDevice(b.first);
     (void)hipFree(b.second);
+  }
+  for (auto& s : streams) {
+    (void)hipSetDevice(s.first);
+    (void)hipStreamDestroy(s.second);
+  }
+  for (auto& e : events) {
+    (void)hipSetDevice(e.first);
+    (void)hipEventDestroy(e.second);
   }
   (void)hipSetDevice(cur);
   return RT_OK;

@@ -281,9 +281,9 @@ int rt_context_create(int32_t device, rt_context** out) {
   rt_context* c = new rt_context();
   c->device = device;
   rt_tuning_default(&c->tun);
-  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
-  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  hipError_t e = (hipError_t)dev_stream_get(&c->stream);
+  if (e == hipSuccess) e = (hipError_t)dev_event_get(&c->ev0);
+  if (e == hipSuccess) e = (hipError_t)dev_event_get(&c->ev1);
 
   if (e != hipSuccess) {
     set_error(std::string("context init failed: ") + hipGetErrorString(e));
@@ -309,9 +309,9 @@ void rt_context_destroy(rt_context* c) {
   for (hipEvent_t& e : c->wf_ev)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
-  if (c->ev0) (void)hipEventDestroy(c->ev0);
-  if (c->ev1) (void)hipEventDestroy(c->ev1);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
+  dev_event_put(c->ev0);  // (complete: ev1 was waited for, ev0 precedes it)
+  dev_event_put(c->ev1);
+  dev_stream_put(c->stream);  // (idle: synchronized above)
   delete c;
 }
 

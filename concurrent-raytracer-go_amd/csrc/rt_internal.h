@@ -7,6 +7,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "../../include/rt_api.h"
 #include "rt_scene_dev.h"
 
@@ -19,6 +21,11 @@ void set_error(const std::string& msg);
 // be in use by any stream when it is freed.
 int dev_alloc(void** p, size_t n);
 void dev_free(void* p);
+// non-blocking streams and timing events, reused the same way (current device)
+int dev_stream_get(hipStream_t* s);
+void dev_stream_put(hipStream_t s);
+int dev_event_get(hipEvent_t* e);
+void dev_event_put(hipEvent_t e);
 
 // ---------------------------------------------------------------- scene
 struct FlatScene {
