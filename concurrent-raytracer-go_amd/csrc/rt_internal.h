@@ -213,12 +213,15 @@ constexpr int kWfShards = 8;           // queues / path arrays are split in 8 sh
 constexpr int kWfBlockSlots = 256;     // threads per workgroup of the wavefront kernels
 constexpr int kWfTravBlock = 1024;     // ... of the traversal kernels (extend, occlude): one per CU, BVH in LDS
 constexpr uint32_t kDeadSid = 0xFFFFFFFFu;  // a slot with no sample (out-of-image pixel of an edge tile)
+constexpr int kWfConeK = 16;           // soft shadows: candidate spheres kept per shadow cone (more: traced rays)
 struct WfCtl {                 // device-resident loop state; counters of shard s at [32 s] (own 128-B line)
   int32_t cur_cnt[kWfShards * 32];   // live paths per shard of the current array
   int32_t next_cnt[kWfShards * 32];  // survivors appended per shard of the next array
   int32_t hard_cnt[kWfShards * 32];  // hard shadow rays queued per shard
   int32_t soft_cnt[kWfShards * 32];  // soft shadow rays queued per shard
-  int32_t job_head[3][kWfShards * 32];  // persistent kernels (extend, hard, soft): jobs taken per range
+  int32_t cone_cnt[kWfShards * 32];  // shadow cones queued per shard
+  int32_t list_cnt[kWfShards * 32];  // soft rays of listed cones per shard (from the far end of the soft queue)
+  int32_t job_head[4][kWfShards * 32];  // persistent kernels (extend, hard, soft, cone): jobs taken per range
   unsigned long long next_sample;    // first sample id of the chunk not started yet
   unsigned long long total;          // sample ids in the chunk
   int32_t live;                // live paths after the last bounce (wf_book)
@@ -262,6 +265,8 @@ struct WfParams {
   uint32_t* lstate;          // [slot][light]: kHardBit | blocked soft rays
   uint32_t* hardq;           // kWfShards queues of hard_cap entries: slot * nl + light
   uint32_t* softq;           // kWfShards queues of soft_cap entries, 4 words: {slot * nl + light, draws x, y, z}
+  uint32_t* coneq;           // kWfShards queues of hard_cap entries: slot * nl + light (clear hard ray)
+  int32_t* cand;             // [slot * nl + light][kWfConeK]: the shadow cone's candidate spheres, -1 ends
   double* rad;               // [sample id][3] radiance
   unsigned long long* counts;
   float* out_linear;
@@ -270,7 +275,7 @@ struct WfParams {
 // Kernel classes of one bounce (rt_context_profile): prof, when not null,
 // holds kWfProfEvents hipEvent_t recorded at their boundaries (event k opens
 // class k, event k + 1 closes it; a skipped kernel takes no time).
-enum { kWfExtend = 0, kWfShade1, kWfHard, kWfSoftgen, kWfSoft, kWfShade, kWfRegen, kWfResolve, kWfClasses };
+enum { kWfExtend = 0, kWfShade1, kWfHard, kWfCone, kWfSoftgen, kWfList, kWfSoft, kWfShade, kWfRegen, kWfResolve, kWfClasses };
 constexpr int kWfProfEvents = kWfClasses + 1;  // (one block serves any class range)
 int wf_launch_bounce(const WfParams& p, bool first, bool count, void* stream, const void* prof);
 // Quantized nodes the traversal kernels can stage in LDS next to their stacks

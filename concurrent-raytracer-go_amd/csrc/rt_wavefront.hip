@@ -69,17 +69,22 @@ constexpr int kLdsBytes = 160 * 1024;    // LDS per CU (MI355X), all of it avail
 #ifndef RT_WF_REFILL
 #define RT_WF_REFILL 24
 #endif
+#ifndef RT_WF_CONES
+#define RT_WF_CONES 1  // soft shadows through shadow cones (0: every soft ray traced; A/B builds)
+#endif
 #ifndef RT_WF_CHUNK
 #define RT_WF_CHUNK 128
 #endif
 constexpr int kRefill = RT_WF_REFILL;    // persistent traversal: refill once this many lanes are idle
 constexpr int kChunk = RT_WF_CHUNK;      // persistent traversal: jobs a wave takes per atomic
-constexpr uint32_t kHardBit = 1u << 16;
-constexpr uint32_t kUnlitBit = 1u << 17;  // lstate: the hit point is within 0.001 of the light (no shadow rays)
+// lstate per (path, light): blocked soft rays in the low 16 bits, and
+constexpr uint32_t kHardBit = 1u << 16;   // the hard shadow ray is blocked
+constexpr uint32_t kUnlitBit = 1u << 17;  // the hit point is within 0.001 of the light (no shadow rays)
+constexpr uint32_t kListBit = 1u << 18;   // the light's shadow cone left a candidate list (wf_cone)
 // hidx of a path whose ray hit nothing while a sky is opted in: wf_shade1
 // ends it with the sky's radiance (GetSkyColor, atmosphere.go:100-135) --
 // kept out of the traversal kernel, whose registers it would cost
-constexpr int kSkyMiss = -2;  // lstate: the hard shadow ray is blocked (low bits: blocked soft rays)
+constexpr int kSkyMiss = -2;
 
 extern __shared__ __attribute__((aligned(16))) unsigned char wf_lds[];
 
@@ -667,15 +672,300 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
   flush_counts<kCount>(p, c, kSoft);
 }
 
+// ---------------------------------------------------------------- cones
+// Soft shadows through shadow cones (the BVH form of the megakernel's cone
+// culling, rt_kernel.hip in_cone).  calculateSmartShadow's 16 soft rays of a
+// (path, light) all leave the hit point P inside the cone of half-angle
+// asin(0.1) around lightDir and end at the light (renderer.go:311-320).  A
+// sphere that cannot meet that cone segment cannot block any of them, so the
+// blocked count over the spheres that can (the candidates) is the count over
+// the scene.  wf_conegen queues every (path, light) whose hard ray is clear;
+// wf_cone walks the BVH with the cone and, when at most kWfConeK spheres are
+// candidates, leaves their list and kListBit in lstate; wf_softgen queues
+// such a light's 16 rays apart, and wf_listtest tests them against the list
+// -- the same Sphere.Hit test the traversal runs -- instead
+// of walking the tree.  C4 (scripts/cone_stats.py): 45 % of the clear cones
+// are empty, the median cone has 1 candidate, 6 % have more than 16.
+//
+// Node test (binary32, on the quantized bounds).  A point X of the cone
+// with projection t on the axis u lies within t tan(a) of P + t u, so on
+// every axis k, lo_k - t tan(a) <= P_k + t u_k <= hi_k + t tan(a) for a box
+// holding X.  With A = u_k + tau, B = u_k - tau (tau >= tan(asin 0.1)) that
+// is t A >= lo_k - P_k and t B <= hi_k - P_k: two linear bounds on t per axis
+// (lower or upper by the signs of A and B), intersected with [0, length].
+// Like the ray's slab test (ray_q_axis), each bound is one fma of the grid
+// index with its binary32 error bound folded outward, so a box the cone
+// meets is never rejected.  (scripts/cone_stats.py: 67 nodes per cone walk
+// against 98 with the nodes' bounding balls.)
+constexpr double kTau = 0.1006;  // > tan(asin(0.1)) = 0.10050378
+struct ConeQ {
+  f2 ax, ay, az;        // per axis: the coefficients of the (first, second) bound
+  f2 bx, by, bz;
+  f2 px, py, pz;        // per axis: (second -> lower, second -> upper) penalties
+  uint32_t sx, sy, sz;  // v_perm selector: which of lo / hi feeds the first bound
+  float len;            // the light distance, rounded up
+#if RT_CONE_NODE == 0
+  float bo[3], bh[3], bu[3], bm;
+#endif
+};
+// First bound: always a lower bound.  Second: an upper bound (u_k >= tau or
+// <= -tau: penalties (-3e38, 0)) or a lower bound (|u_k| < tau: (0, 3e38)).
+__device__ __forceinline__ void cone_q_axis(double q0, double qd, double P, double u, f2& a, f2& b, f2& pen,
+                                            uint32_t& sel, bool& ok) {
+  const double A = u + kTau, B = u - kTau;
+  const double iA = 1.0 / A, iB = 1.0 / B;
+  const double aL = qd * iA, bL = (q0 - P) * iA;  // (lo - P) / A
+  const double aH = qd * iB, bH = (q0 - P) * iB;  // (hi - P) / B
+  const double eL = 2.0 * fabs(aL) + (65536.0 * fabs(aL) + fabs(bL)) * 0x1p-22;
+  const double eH = 2.0 * fabs(aH) + (65536.0 * fabs(aH) + fabs(bH)) * 0x1p-22;
+  const double bpL = bL - 8388608.0 * aL, bpH = bH - 8388608.0 * aH;
+  double a1, b1, a2, b2;
+  if (B > 0) {  // lo: lower, hi: upper
+    a1 = aL, b1 = bpL - eL, a2 = aH, b2 = bpH + eH;
+    sel = kSelLo;
+    pen = f2{-3e38f, 0.f};
+  } else if (A < 0) {  // hi: lower, lo: upper
+    a1 = aH, b1 = bpH - eH, a2 = aL, b2 = bpL + eL;
+    sel = kSelHi;
+    pen = f2{-3e38f, 0.f};
+  } else {  // both lower
+    a1 = aL, b1 = bpL - eL, a2 = aH, b2 = bpH - eH;
+    sel = kSelLo;
+    pen = f2{0.f, 3e38f};
+  }
+  a = f2{(float)a1, (float)a2};
+  b = f2{(float)b1, (float)b2};
+  ok = ok && fabs(A) > 1e-6 && fabs(B) > 1e-6 && fabs(a1) < 1e30 && fabs(a2) < 1e30 && fabs(b1) < 1e37 &&
+       fabs(b2) < 1e37;
+}
+__device__ __forceinline__ ConeQ cone_q(const WfParams& p, d3 P, d3 u, double ldist) {
+  ConeQ k;
+  bool ok = __builtin_isfinite(ldist);
+  cone_q_axis(p.q0[0], p.qd[0], P.x, u.x, k.ax, k.bx, k.px, k.sx, ok);
+  cone_q_axis(p.q0[1], p.qd[1], P.y, u.y, k.ay, k.by, k.py, k.sy, ok);
+  cone_q_axis(p.q0[2], p.qd[2], P.z, u.z, k.az, k.bz, k.pz, k.sz, ok);
+  k.len = (float)(ldist * (1.0 + 1e-6));
+#if RT_CONE_NODE == 0
+  k.bm = (float)(1e-5 * 65536.0 * fmax(fmax(p.qd[0], p.qd[1]), p.qd[2])) + 1e-30f;
+  k.len += k.bm;
+  const double pp[3] = {P.x, P.y, P.z}, uu[3] = {u.x, u.y, u.z};
+  for (int a = 0; a < 3; ++a) {
+    k.bo[a] = (float)(p.q0[a] - pp[a]);
+    k.bh[a] = (float)(0.5 * p.qd[a]);
+    k.bu[a] = (float)uu[a];
+  }
+  return k;
+#endif
+  if (!ok) {  // every node is kept (exact, slower)
+    k.ax = k.ay = k.az = f2{0.f, 0.f};
+    k.bx = k.by = k.bz = f2{-1e30f, 1e30f};
+    k.px = k.py = k.pz = f2{-3e38f, 0.f};
+    k.len = 3e38f;
+  }
+  return k;
+}
+#ifndef RT_CONE_NODE
+#define RT_CONE_NODE 1
+#endif
+#if RT_CONE_NODE == 0
+// (A/B) the node's bounding ball against the cone, binary32
+__device__ __forceinline__ bool cone_node_ball(const uint4 n, const ConeQ& k) {
+  float v[3], e[3];
+  const uint32_t w[3] = {n.x, n.y, n.z};
+  for (int a = 0; a < 3; ++a) {
+    const float lo = (float)(w[a] & 0xFFFFu), hi = (float)(w[a] >> 16);
+    v[a] = __builtin_fmaf(lo + hi, k.bh[a], k.bo[a]);
+    e[a] = (hi - lo) * k.bh[a];
+  }
+  const float dc2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+  const float dc = __builtin_amdgcn_sqrtf(dc2);
+  const float ra = __builtin_amdgcn_sqrtf(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]) + k.bm + 1e-4f * dc;
+  const float tl = __builtin_amdgcn_sqrtf(fmaxf(dc2 - ra * ra, 0.f));
+  const float vu = v[0] * k.bu[0] + v[1] * k.bu[1] + v[2] * k.bu[2];
+  return !(dc > ra && (dc - ra > k.len || vu < 0.99498f * tl - 0.1f * ra));
+}
+#endif
+__device__ __forceinline__ bool cone_node(const uint4 n, const ConeQ& k) {
+#if RT_CONE_NODE == 0
+  return cone_node_ball(n, k);
+#endif
+  const f2 x = __builtin_elementwise_fma(q_near_far(n.x, k.sx), k.ax, k.bx);
+  const f2 y = __builtin_elementwise_fma(q_near_far(n.y, k.sy), k.ay, k.by);
+  const f2 z = __builtin_elementwise_fma(q_near_far(n.z, k.sz), k.az, k.bz);
+  const float lx = fmaxf(x.x, x.y + k.px.x), ly = fmaxf(y.x, y.y + k.py.x), lz = fmaxf(z.x, z.y + k.pz.x);
+  const float tn = fmaxf(fmaxf(lx, ly), fmaxf(lz, 0.f));
+  const float tf = fminf(fminf(x.y + k.px.y, y.y + k.py.y), fminf(z.y + k.pz.y, k.len));
+  return tn <= tf;
+}
+// A sphere: in_cone's binary64 test (the same margins), NaN kept
+__device__ __forceinline__ bool cone_keeps(const DSphere& S, d3 P, d3 u, double ldist) {
+  const d3 v = ld3(S.c) - P;
+  const double dc2 = len2(v);
+  const double dc = (double)__builtin_amdgcn_sqrtf((float)dc2);
+  const double ra = fabs(S.r) * (1.0 + 1e-5) + 1e-5 * dc + 1e-12;
+  const double tl = (double)__builtin_amdgcn_sqrtf((float)fmax(dc2 - ra * ra, 0.0));
+  const bool miss =
+      dc > ra && (dc - ra > ldist * (1.0 + 1e-5) + 1e-9 || dot(v, u) < 0.99498 * tl - 0.1 * ra - 1e-5 * dc);
+  return !miss;
+}
+
+template <bool kCount, bool kFull>
+__device__ __forceinline__ void cone_descend(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
+                                             const ConeQ& k, int& cur, int& sp, int* stack, Counters& c) {
+  while ((cur & 7) == 0) {
+    uint4 L, R;
+    load_pair<kFull>(qb, lt, nlds, cur >> 3, L, R);
+    cnt<kCount>(c, C_BOX, 2);
+    const bool hl = cone_node(L, k), hr = cone_node(R, k);
+    if (hl || hr) {
+      if (hl && hr) {
+        stack[sp * 64] = (int)R.w;
+        ++sp;
+      }
+      cur = hl ? (int)L.w : (int)R.w;
+    } else {
+      cur = sp == 0 ? -1 : stack[--sp * 64];
+    }
+  }
+}
+
+// lights base + i (i < 32) of a path that are lit (wf_shade1: not within
+// 0.001 of the hit point) and whose hard ray is clear; `listed`: those of
+// them whose cone left a candidate list
+__device__ __forceinline__ uint32_t clear_lights(const WfParams& p, size_t slot, bool hit, int base,
+                                                 uint32_t* listed = nullptr) {
+  uint32_t own = 0, lst = 0;
+  if (hit) {
+    const int end = min(p.nl, base + 32);
+    for (int li = base; li < end; ++li) {
+      const uint32_t ls = p.lstate[slot * p.nl + li];
+      if (!(ls & (kHardBit | kUnlitBit))) own |= 1u << (li - base);
+      if (ls & kListBit) lst |= 1u << (li - base);
+    }
+  }
+  if (listed) *listed = lst;
+  return own;
+}
+
+// One cone job per (path, light) with a clear hard ray, into the workgroup's
+// shard of the cone queue.
+__global__ __launch_bounds__(kWfBlock) void wf_conegen(const WfParams p) {
+  __shared__ int s_wave[kWfBlock / 64];
+  __shared__ int s_base;
+  const Dense dn = dense(p.ctl->cur_cnt);
+  const int n = dn.start[kWfShards];
+  if ((int)(blockIdx.x * kWfBlock) >= n) return;
+  const int j = blockIdx.x * kWfBlock + threadIdx.x;
+  size_t slot = 0;
+  bool hit = false;
+  if (j < n) {
+    slot = dense_at(dn, j, p.shard_cap);
+    hit = p.hidx[slot] >= 0;
+  }
+  const int shard = blockIdx.x % kWfShards;
+  uint32_t* cq = p.coneq + (size_t)shard * p.hard_cap;
+  for (int base = 0; base < p.nl; base += 32) {
+    const uint32_t own = clear_lights(p, slot, hit, base);
+    int q = block_append(__popc(own), &p.ctl->cone_cnt[shard * 32], s_wave, &s_base);
+    for (uint32_t m = own; m; m &= m - 1) cq[q++] = (uint32_t)(slot * p.nl) + (uint32_t)(base + __builtin_ctz(m));
+  }
+}
+
+// Persistent cone traversal of the queued cones (the job distribution and
+// LDS tree of the occlusion kernels): every sphere of every leaf the cone's
+// node tests reach gets cone_keeps; candidates go to the cone's list, up to
+// kWfConeK (one more ends the walk: the cone's rays are traced instead).
+// The hit sphere itself is left out as in cone_candidates (rt_kernel.hip)
+// when the cone leaves its front face at a clear angle.
+template <bool kCount, bool kFull>
+__global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
+  const Dense dn = dense(p.ctl->cone_cnt);
+  const int n = dn.start[kWfShards];
+  if (n == 0) return;
+  lds_node* lt = stage_tree(p);
+  JobSrc js{0, 0, 0};
+  bool more = true;  // wave-uniform: jobs may remain
+  Counters c;
+  if constexpr (kCount)
+    for (int k = 0; k < 9; ++k) c.v[k] = 0;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int* stack = wf_stack(p.stack_depth);
+  bool busy = false;
+  uint32_t key = 0;
+  d3 P = mk(0, 0, 0), u = mk(0, 0, 0);
+  double ldist = 0;
+  ConeQ k{};
+  int excl = -1, found = 0, cur = -1, sp = 0;
+  for (;;) {
+    const unsigned long long idle = __ballot(!busy);
+    if (more && (__popcll(idle) >= kRefill || idle == ~0ull) && js.next >= js.hi)
+      more = job_refill(js, p.ctl->job_head[3], n);
+    if (more && (__popcll(idle) >= kRefill || idle == ~0ull)) {
+      const int j = js.next + __popcll(idle & below), hi = js.hi;
+      js.next = min(hi, js.next + __popcll(idle));
+      if (!busy && j < hi) {
+        key = p.coneq[dense_at(dn, j, p.hard_cap)];
+        const uint32_t slot = key / (uint32_t)p.nl, li = key - slot * (uint32_t)p.nl;
+        P = ld_P(p, (int)slot);
+        light_vec(p.lights[li], P, u, ldist);
+        const DSphere& S0 = p.g.spheres[p.hidx[slot]];
+        const d3 outward = divs(P - ld3(S0.c), S0.r);
+        const bool self_out = dot(ld_d(p.cur, slot), outward) < 0 && dot(outward, u) >= 0.1015;
+        excl = self_out ? S0.obj : -1;
+        k = cone_q(p, P, u, ldist);
+        found = 0;
+        cur = bvh_code(p.g.bvh[0]);
+        sp = 0;
+        busy = true;
+      }
+    }
+    if (__ballot(busy) == 0) {
+      if (!more) break;
+      continue;
+    }
+    if (busy) {
+      cone_descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, k, cur, sp, stack, c);
+      if (cur != -1) {
+        const int first = cur >> 3, count = cur & 7;
+        DSphere ls[kLeafBatch];
+        load_leaf(p.g.spheres, first, count, ls);
+        int32_t* cl = p.cand + (size_t)key * kWfConeK;
+        for (int i = first; i < first + count; ++i) {
+          const DSphere& S = leaf_sphere(p.g.spheres, ls, first, i);
+          if (S.obj == excl && S.r > 0) continue;
+          cnt<kCount>(c, C_SPH);
+          if (cone_keeps(S, P, u, ldist)) {
+            if (found < kWfConeK) cl[found] = i;
+            ++found;
+          }
+        }
+        cur = found > kWfConeK || sp == 0 ? -1 : stack[--sp * 64];
+      }
+      if (cur == -1) {  // walked (or too many candidates: the rays are traced)
+        busy = false;
+        if (found <= kWfConeK) {
+          if (found < kWfConeK) p.cand[(size_t)key * kWfConeK + found] = -1;
+          p.lstate[key] = kListBit;
+        }
+      }
+    }
+  }
+  flush_counts<kCount>(p, c, true);
+}
+
 // ---------------------------------------------------------------- softgen
 // For every light whose hard ray is clear, in light order, the 16 points of
 // calculateSmartShadow's soft rays from the path's stream (rejection
-// sampling, vector.go:132-139), as 16 consecutive soft-queue entries.
+// sampling, vector.go:132-139), as 16 consecutive soft-queue entries.  A
+// light whose cone left a candidate list (wf_cone) has its 16 entries
+// written from the far end of the shard's queue instead (list_cnt counts
+// them), for wf_listtest; the others are traced by wf_occlude<soft>.
 template <bool kCount>
 __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
   __shared__ int s_wave[kWfBlock / 64];
   __shared__ int s_base;
-  __shared__ uint32_t s_slot[kWfBlock], s_own[kWfBlock];
+  __shared__ uint32_t s_slot[kWfBlock], s_own[kWfBlock], s_list[kWfBlock];
   const Dense dn = dense(p.ctl->cur_cnt);
   const int n = dn.start[kWfShards];
   if ((int)(blockIdx.x * kWfBlock) >= n) return;
@@ -690,29 +980,27 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
     hit = p.hidx[slot] >= 0;
   }
   const int shard = blockIdx.x % kWfShards;
-  // lights base + i of `own` that are lit (wf_shade1: not within 0.001 of the
-  // hit point) and whose hard ray is clear (i < 32)
-  auto clear_lights = [&](int base) {
-    uint32_t own = 0;
-    if (hit) {
-      const int end = min(p.nl, base + 32);
-      for (int li = base; li < end; ++li)
-        if (!(p.lstate[slot * p.nl + li] & (kHardBit | kUnlitBit))) own |= 1u << (li - base);
-    }
-    return own;
-  };
-  // the 16 points of each light of `own`, in light order, at entries q.. of the shard's queue
-  auto gen = [&](size_t sl, uint32_t own, int base, int q, rt_rng& rng) {
-    uint4* sq = reinterpret_cast<uint4*>(p.softq) + (size_t)shard * p.soft_cap + q;
-    int k = 0;  // entries written (an index, not a bumped pointer)
+  // the 16 points of each light of `own`, in light order: traced rays at
+  // entries q.. of the shard's queue, a listed light's at the 16 entries
+  // ending before soft_cap - ql (ql += 16)
+  auto gen = [&](size_t sl, uint32_t own, uint32_t listed, int base, int q, int ql, rt_rng& rng) {
+    uint4* sq = reinterpret_cast<uint4*>(p.softq) + (size_t)shard * p.soft_cap;
     for (uint32_t m = own; m; m &= m - 1) {
       const uint32_t key = (uint32_t)(sl * p.nl) + (uint32_t)(base + __builtin_ctz(m));
       cnt<kCount>(c, C_SHADOW, 16);
-      for (const int end = k + 16; k < end;) {
+      size_t at;  // (an index, not a bumped pointer)
+      if (listed & m & (0u - m)) {
+        at = (size_t)(p.soft_cap - ql - 16);
+        ql += 16;
+      } else {
+        at = (size_t)q;
+        q += 16;
+      }
+      for (int k = 0; k < 16;) {
         const uint32_t ux = rt_rng_next(&rng), uy = rt_rng_next(&rng), uz = rt_rng_next(&rng);
         cnt<kCount>(c, C_RNG, 3);
         const bool acc = unit_ball_accept(ux, uy, uz);
-        if (acc) sq[k] = make_uint4(key, ux, uy, uz);
+        if (acc) sq[at + k] = make_uint4(key, ux, uy, uz);
         k += acc ? 1 : 0;
       }
     }
@@ -722,20 +1010,24 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
     // paths that have one are gathered to the workgroup's first lanes, so
     // the rejection sampling runs on full waves and the other waves of the
     // workgroup skip it (one path per lane either way: same draws, same order)
-    const uint32_t own = clear_lights(0);
+    uint32_t listed;
+    const uint32_t own = clear_lights(p, slot, hit, 0, &listed);
     int total;
     const int at = block_prefix(own != 0 ? 1 : 0, s_wave, total);
     if (own) {
       s_slot[at] = (uint32_t)slot;
       s_own[at] = own;
+      s_list[at] = listed;
     }
     __syncthreads();
     const bool work = (int)threadIdx.x < total;
     const uint32_t ws = work ? s_slot[threadIdx.x] : 0u, wo = work ? s_own[threadIdx.x] : 0u;
-    const int q = block_append(16 * __popc(wo), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
+    const uint32_t wl = work ? s_list[threadIdx.x] : 0u;
+    const int q = block_append(16 * __popc(wo & ~wl), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
+    const int ql = block_append(16 * __popc(wl), &p.ctl->list_cnt[shard * 32], s_wave, &s_base);
     if (work) {
       rt_rng rng{p.cur.rng[ws]};
-      gen(ws, wo, 0, q, rng);
+      gen(ws, wo, wl, 0, q, ql, rng);
       p.cur.rng[ws] = rng.x;
     }
     flush_counts<kCount>(p, c);
@@ -744,12 +1036,74 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
   rt_rng rng{hit ? p.cur.rng[slot] : 0ull};
   // more than 32 lights: in chunks of 32 (one bit each), in light order
   for (int base = 0; base < p.nl; base += 32) {
-    const uint32_t own = clear_lights(base);
-    const int q = block_append(16 * __popc(own), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
-    if (own) gen(slot, own, base, q, rng);
+    uint32_t listed;
+    const uint32_t own = clear_lights(p, slot, hit, base, &listed);
+    const int q = block_append(16 * __popc(own & ~listed), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
+    const int ql = block_append(16 * __popc(listed), &p.ctl->list_cnt[shard * 32], s_wave, &s_base);
+    if (own) gen(slot, own, listed, base, q, ql, rng);
   }
   if (hit) p.cur.rng[slot] = rng.x;
   flush_counts<kCount>(p, c);
+}
+
+// ---------------------------------------------------------------- listtest
+// The 16 soft rays of a listed cone against its candidates, one cone per
+// thread: the ray (normalize(lightDir + 0.1 p), wf_occlude<soft>'s), the
+// range [0.001, distance) and the Sphere.Hit test of the traversal, so the
+// blocked count is the one the traversal would find.  Candidates four at a
+// time (their loads together, then every ray still clear against them).
+template <bool kCount>
+__global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
+  const Dense dn = dense(p.ctl->list_cnt);  // (entries: 16 per cone, so no cone spans two shards)
+  const int n = dn.start[kWfShards] / 16;
+  const int j = blockIdx.x * kWfBlock + threadIdx.x;
+  Counters c;
+  if constexpr (kCount)
+    for (int k = 0; k < 9; ++k) c.v[k] = 0;
+  if (j < n) {
+    const size_t at = dense_at(dn, 16 * j, p.soft_cap);
+    const size_t sh = at / (size_t)p.soft_cap, off = at - sh * (size_t)p.soft_cap;
+    const uint4* e = reinterpret_cast<const uint4*>(p.softq) + sh * (size_t)p.soft_cap + (p.soft_cap - off - 16);
+    const uint32_t key = e[0].x;
+    const uint32_t slot = key / (uint32_t)p.nl, li = key - slot * (uint32_t)p.nl;
+    const d3 o = ld_P(p, (int)slot);
+    d3 ldir;
+    double tmax;
+    light_vec(p.lights[li], o, ldir, tmax);
+    const int32_t* cl = p.cand + (size_t)key * kWfConeK;
+    uint32_t blocked = 0;  // one bit per ray
+    for (int g = 0; g < kWfConeK; g += 4) {
+      const int4 q4 = *reinterpret_cast<const int4*>(cl + g);
+      const int id[4] = {q4.x, q4.y, q4.z, q4.w};
+      bool valid[4];
+      DSphere ls[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        valid[k] = id[k] >= 0 && (k == 0 || valid[k - 1]);
+        ls[k] = p.g.spheres[valid[k] ? id[k] : 0];
+      }
+      if (!valid[0]) break;
+      for (int r = 0; r < 16; ++r) {
+        if (blocked & (1u << r)) continue;
+        const uint4 er = e[r];
+        const d3 pt = mk(rt_bits_to_unit(er.y) * 2 - 1, rt_bits_to_unit(er.z) * 2 - 1, rt_bits_to_unit(er.w) * 2 - 1);
+        const d3 d = normalize(ldir + muls(pt, 0.1));
+        const double av = len2(d), inv_a = approx_rcp(av);
+        bool b = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (valid[k] && !b) {
+            cnt<kCount>(c, C_SPH);
+            double num;
+            b = sphere_query(ls[k], o, d, av, inv_a, 0.001, tmax, num) != 0;
+          }
+        blocked |= b ? 1u << r : 0u;
+      }
+      if (!valid[3]) break;
+    }
+    p.lstate[key] = (uint32_t)__popc(blocked);
+  }
+  flush_counts<kCount>(p, c, true);
 }
 
 // ---------------------------------------------------------------- shade
@@ -923,6 +1277,9 @@ __global__ void wf_book(const WfParams p) {
     ctl->next_cnt[s * 32] = 0;
     ctl->hard_cnt[s * 32] = 0;
     ctl->soft_cnt[s * 32] = 0;
+    ctl->cone_cnt[s * 32] = 0;
+    ctl->list_cnt[s * 32] = 0;
+    ctl->job_head[3][s * 32] = 0;
     ctl->job_head[0][s * 32] = 0;
     ctl->job_head[1][s * 32] = 0;
     ctl->job_head[2][s * 32] = 0;
@@ -1017,7 +1374,7 @@ static void enqueue_trav(const WfParams& p, hipStream_t st, int which) {
   // drives its devices from one thread each (rt_multi.cpp), and contexts of
   // different scenes may share a device
   struct Grids {
-    int ext = 0, occ_h = 0, occ_s = 0;
+    int ext = 0, occ_h = 0, occ_s = 0, cone = 0;
   };
   static std::mutex mu;
   static std::map<std::tuple<int, size_t, int>, Grids> cache;
@@ -1033,6 +1390,7 @@ static void enqueue_trav(const WfParams& p, hipStream_t st, int which) {
       c.ext = resident_grid(wf_extend<kCount, kFull>, p.trav_block, sh);
       c.occ_h = resident_grid(wf_occlude<kCount, false, kFull>, p.trav_block, sh);
       c.occ_s = resident_grid(wf_occlude<kCount, true, kFull>, p.trav_block, sh);
+      c.cone = resident_grid(wf_cone<kCount, kFull>, p.trav_block, sh);
       it = cache.emplace(key, c).first;
     }
     g = it->second;
@@ -1040,6 +1398,7 @@ static void enqueue_trav(const WfParams& p, hipStream_t st, int which) {
   if (which == 0) hipLaunchKernelGGL((wf_extend<kCount, kFull>), dim3(g.ext), bt, sh, st, p);
   if (which == 1) hipLaunchKernelGGL((wf_occlude<kCount, false, kFull>), dim3(g.occ_h), bt, sh, st, p);
   if (which == 2) hipLaunchKernelGGL((wf_occlude<kCount, true, kFull>), dim3(g.occ_s), bt, sh, st, p);
+  if (which == 3) hipLaunchKernelGGL((wf_cone<kCount, kFull>), dim3(g.cone), bt, sh, st, p);
 }
 
 template <bool kCount>
@@ -1063,8 +1422,22 @@ static int enqueue_bounce(const WfParams& p, hipStream_t st, const hipEvent_t* e
   hipLaunchKernelGGL((wf_shade1<kCount>), gd, b, 0, st, p);
   mark(ev, kWfHard, st);
   if (p.nl > 0) trav(1);
+  mark(ev, kWfCone, st);
+#if RT_WF_CONES
+  if (p.nl > 0 && p.soft) {
+    hipLaunchKernelGGL(wf_conegen, gd, b, 0, st, p);
+    trav(3);
+  }
+#endif
   mark(ev, kWfSoftgen, st);
   if (p.nl > 0 && p.soft) hipLaunchKernelGGL((wf_softgen<kCount>), gd, b, 0, st, p);
+  mark(ev, kWfList, st);
+#if RT_WF_CONES
+  if (p.nl > 0 && p.soft) {  // (at most one listed cone per path and light)
+    const long long cones = live * p.nl;
+    hipLaunchKernelGGL((wf_listtest<kCount>), dim3((unsigned)((cones + kWfBlock - 1) / kWfBlock)), b, 0, st, p);
+  }
+#endif
   mark(ev, kWfSoft, st);
   if (p.nl > 0 && p.soft) trav(2);
   mark(ev, kWfShade, st);

@@ -45,7 +45,7 @@ SKIES = {"none": 0, "default": 1, "white": 2, "sunset": 3, "night": 4}  # RT_SKY
 RT_COMM_ID_BYTES = 128
 RT_MAX_FRAMES = 16  # frames per launch (rt_context_render_frames_async)
 # wavefront kernel classes (RT_WF_*, rt_context_kernel_seconds)
-WF_KERNELS = ["extend", "shade1", "occlude_hard", "softgen", "occlude_soft", "shade", "regen", "resolve"]
+WF_KERNELS = ["extend", "shade1", "occlude_hard", "cone", "softgen", "cone_rays", "occlude_soft", "shade", "regen", "resolve"]
 
 
 class RenderError(RuntimeError):

@@ -439,12 +439,14 @@ int rt_context_set_debug_buffer(rt_context* ctx, void* d_buf);
 #define RT_WF_EXTEND 0       /* closest hit of the live paths (hitWorld, renderer.go:333-346) */
 #define RT_WF_SHADE1 1       /* hit records + hard shadow rays queued */
 #define RT_WF_OCCLUDE_HARD 2 /* any-hit of the hard shadow rays (renderer.go:305) */
-#define RT_WF_SOFTGEN 3      /* the 16 jittered points per clear light (renderer.go:311-318) */
-#define RT_WF_OCCLUDE_SOFT 4 /* any-hit of the soft shadow rays (renderer.go:320) */
-#define RT_WF_SHADE 5        /* direct lighting + scatter (renderer.go:181-297) */
-#define RT_WF_REGEN 6        /* new camera samples + loop bookkeeping */
-#define RT_WF_RESOLVE 7      /* per-pixel in-order sums, tone map, write */
-#define RT_WF_KERNELS 8
+#define RT_WF_CONE 3         /* shadow cones of the clear hard rays: candidate lists (renderer.go:311-320) */
+#define RT_WF_SOFTGEN 4      /* the 16 jittered points per clear light (renderer.go:311-318) */
+#define RT_WF_CONE_RAYS 5    /* the soft rays of cones with a candidate list, against the list */
+#define RT_WF_OCCLUDE_SOFT 6 /* any-hit of the other soft shadow rays through the BVH (renderer.go:320) */
+#define RT_WF_SHADE 7        /* direct lighting + scatter (renderer.go:181-297) */
+#define RT_WF_REGEN 8        /* new camera samples + loop bookkeeping */
+#define RT_WF_RESOLVE 9      /* per-pixel in-order sums, tone map, write */
+#define RT_WF_KERNELS 10
 int rt_context_profile(rt_context* ctx, int32_t on);  /* on / off; resets the totals */
 int rt_context_kernel_seconds(rt_context* ctx, double* seconds /* RT_WF_KERNELS */,
                               int64_t* launches /* RT_WF_KERNELS or NULL */);

@@ -43,10 +43,15 @@ def main():
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         ks = ctx.kernel_seconds()
+        row = {"variant": var, "frame_ms": round(wall * 1e3, 2),
+               "kernel_ms": {k: round(v[0] * 1e3, 2) for k, v in ks.items()},
+               "checksum": float(lin.double().sum())}
+        if os.environ.get("PROBE_COUNT"):  # one counted frame: the soft-shadow stage's own counts
+            c = ctx.count(W, H, st, lin.data_ptr(), 0, full=True)
+            row["counts"] = c.as_dict()
+            row["soft_stage_counts"] = c.soft_occlusion_dict()
         ctx.close()
-        print(json.dumps({"variant": var, "frame_ms": round(wall * 1e3, 2),
-                          "kernel_ms": {k: round(v[0] * 1e3, 2) for k, v in ks.items()},
-                          "checksum": float(lin.double().sum())}), flush=True)
+        print(json.dumps(row), flush=True)
 
 
 if __name__ == "__main__":
