@@ -106,9 +106,11 @@ KERNELS = {  # the dominant kernel of each config (rocprofv3 --stats, profiles/)
     "c2": "rtgo::render_kernel<false, true, false, false>",
     "c2_committed": "rtgo::render_kernel<false, true, false, false>",
     "c3": "rtgo::render_kernel<false, true, false, false>",
-    "c4": "rtgo::wf_occlude<false, true, true>",
-    "c5": "rtgo::wf_occlude<false, true, true>",
+    # the soft-shadow stage: cone walks, list tests, traced soft rays
+    "c4": "rtgo::wf_cone<false, true> + rtgo::wf_listtest<false> + rtgo::wf_occlude<false, true, true>",
+    "c5": "rtgo::wf_cone<false, true> + rtgo::wf_listtest<false> + rtgo::wf_occlude<false, true, true>",
 }
+SOFT_STAGE = ("cone", "cone_rays", "occlude_soft")  # its kernel classes (rtgo.WF_KERNELS)
 
 
 def parse():
@@ -362,8 +364,12 @@ def executed(counts):
 
 def fp_split(ex, soft=None):
     """(binary64 ops, binary32 ops) of executed event counts ex.  soft: the
-    soft-shadow traversal kernel's own counts (its ray set-up instead of the
-    generic per-event costs)."""
+    soft-shadow stage's own counts (rt_counts.soft_occlusion): shadow_rays =
+    the rays it traced through the BVH (their set-up instead of the generic
+    per-event cost), sphere_tests = the cone walks' sphere tests + the list
+    tests + the traced rays' tests, box_tests = the cone walks' node tests +
+    the traced rays' (the cone set-up and the listed rays' directions are
+    not counted: an under-count)."""
     if soft is not None:
         jobs = soft["shadow_rays"]
         f64 = jobs * SOFT_RAY_SETUP_FLOPS + soft["sphere_tests"] * FLOPS_PER_EVENT["sphere_tests"]
@@ -649,10 +655,13 @@ def main():
     hbm_bytes = npix_local * 16 + 4096
     workload = "%s %dx%d %dspp depth %d" % (label, W, H, args.spp, args.depth)
     if cfg in WAVEFRONT:
-        # the dominant kernel: the soft-shadow traversal (wf_occlude<soft>),
-        # its own counts over its own launches (HIP events of the timed frames)
+        # the soft-shadow stage (cone walks, the rays of
+        # listed cones against their lists, the other soft rays through the
+        # BVH): its own counts over its own launches (HIP events of the timed
+        # frames)
         soft = counts.soft_occlusion_dict()
-        k_s, k_n = kernel_prof["occlude_soft"]
+        k_s = sum(kernel_prof[k][0] for k in SOFT_STAGE)
+        k_n = kernel_prof["occlude_soft"][1]
         frames_timed = max(1, kernel_prof["resolve"][1])
         per_frame_s = k_s / frames_timed
         f64, f32 = fp_split(ex, soft=soft)

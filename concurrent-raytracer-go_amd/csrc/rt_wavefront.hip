@@ -81,6 +81,7 @@ constexpr int kChunk = RT_WF_CHUNK;      // persistent traversal: jobs a wave ta
 constexpr uint32_t kHardBit = 1u << 16;   // the hard shadow ray is blocked
 constexpr uint32_t kUnlitBit = 1u << 17;  // the hit point is within 0.001 of the light (no shadow rays)
 constexpr uint32_t kListBit = 1u << 18;   // the light's shadow cone left a candidate list (wf_cone)
+constexpr uint32_t kEmptyBit = 1u << 19;  // ... an empty one: no soft ray can be blocked
 // hidx of a path whose ray hit nothing while a sky is opted in: wf_shade1
 // ends it with the sky's radiance (GetSkyColor, atmosphere.go:100-135) --
 // kept out of the traversal kernel, whose registers it would cost
@@ -833,17 +834,19 @@ __device__ __forceinline__ void cone_descend(glb_node* __restrict__ qb, lds_node
 // 0.001 of the hit point) and whose hard ray is clear; `listed`: those of
 // them whose cone left a candidate list
 __device__ __forceinline__ uint32_t clear_lights(const WfParams& p, size_t slot, bool hit, int base,
-                                                 uint32_t* listed = nullptr) {
-  uint32_t own = 0, lst = 0;
+                                                 uint32_t* listed = nullptr, uint32_t* empty = nullptr) {
+  uint32_t own = 0, lst = 0, emp = 0;
   if (hit) {
     const int end = min(p.nl, base + 32);
     for (int li = base; li < end; ++li) {
       const uint32_t ls = p.lstate[slot * p.nl + li];
       if (!(ls & (kHardBit | kUnlitBit))) own |= 1u << (li - base);
       if (ls & kListBit) lst |= 1u << (li - base);
+      if (ls & kEmptyBit) emp |= 1u << (li - base);
     }
   }
   if (listed) *listed = lst;
+  if (empty) *empty = emp;
   return own;
 }
 
@@ -944,7 +947,9 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
       }
       if (cur == -1) {  // walked (or too many candidates: the rays are traced)
         busy = false;
-        if (found <= kWfConeK) {
+        if (found == 0) {
+          p.lstate[key] = kListBit | kEmptyBit;
+        } else if (found <= kWfConeK) {
           if (found < kWfConeK) p.cand[(size_t)key * kWfConeK + found] = -1;
           p.lstate[key] = kListBit;
         }
@@ -965,7 +970,7 @@ template <bool kCount>
 __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
   __shared__ int s_wave[kWfBlock / 64];
   __shared__ int s_base;
-  __shared__ uint32_t s_slot[kWfBlock], s_own[kWfBlock], s_list[kWfBlock];
+  __shared__ uint32_t s_slot[kWfBlock], s_own[kWfBlock], s_list[kWfBlock], s_empty[kWfBlock];
   const Dense dn = dense(p.ctl->cur_cnt);
   const int n = dn.start[kWfShards];
   if ((int)(blockIdx.x * kWfBlock) >= n) return;
@@ -982,25 +987,31 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
   const int shard = blockIdx.x % kWfShards;
   // the 16 points of each light of `own`, in light order: traced rays at
   // entries q.. of the shard's queue, a listed light's at the 16 entries
-  // ending before soft_cap - ql (ql += 16)
-  auto gen = [&](size_t sl, uint32_t own, uint32_t listed, int base, int q, int ql, rt_rng& rng) {
+  // ending before soft_cap - ql (ql += 16); an empty cone's are drawn and
+  // dropped (none can be blocked)
+  auto gen = [&](size_t sl, uint32_t own, uint32_t listed, uint32_t empty, int base, int q, int ql,
+                 rt_rng& rng) {
     uint4* sq = reinterpret_cast<uint4*>(p.softq) + (size_t)shard * p.soft_cap;
     for (uint32_t m = own; m; m &= m - 1) {
       const uint32_t key = (uint32_t)(sl * p.nl) + (uint32_t)(base + __builtin_ctz(m));
+      const uint32_t bit = m & (0u - m);
       cnt<kCount>(c, C_SHADOW, 16);
       size_t at;  // (an index, not a bumped pointer)
-      if (listed & m & (0u - m)) {
+      if (empty & bit) {
+        at = 0;
+      } else if (listed & bit) {
         at = (size_t)(p.soft_cap - ql - 16);
         ql += 16;
       } else {
         at = (size_t)q;
         q += 16;
       }
+      const bool keep = !(empty & bit);
       for (int k = 0; k < 16;) {
         const uint32_t ux = rt_rng_next(&rng), uy = rt_rng_next(&rng), uz = rt_rng_next(&rng);
         cnt<kCount>(c, C_RNG, 3);
         const bool acc = unit_ball_accept(ux, uy, uz);
-        if (acc) sq[at + k] = make_uint4(key, ux, uy, uz);
+        if (acc && keep) sq[at + k] = make_uint4(key, ux, uy, uz);
         k += acc ? 1 : 0;
       }
     }
@@ -1010,24 +1021,25 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
     // paths that have one are gathered to the workgroup's first lanes, so
     // the rejection sampling runs on full waves and the other waves of the
     // workgroup skip it (one path per lane either way: same draws, same order)
-    uint32_t listed;
-    const uint32_t own = clear_lights(p, slot, hit, 0, &listed);
+    uint32_t listed, empty;
+    const uint32_t own = clear_lights(p, slot, hit, 0, &listed, &empty);
     int total;
     const int at = block_prefix(own != 0 ? 1 : 0, s_wave, total);
     if (own) {
       s_slot[at] = (uint32_t)slot;
       s_own[at] = own;
       s_list[at] = listed;
+      s_empty[at] = empty;
     }
     __syncthreads();
     const bool work = (int)threadIdx.x < total;
     const uint32_t ws = work ? s_slot[threadIdx.x] : 0u, wo = work ? s_own[threadIdx.x] : 0u;
-    const uint32_t wl = work ? s_list[threadIdx.x] : 0u;
+    const uint32_t wl = work ? s_list[threadIdx.x] : 0u, we = work ? s_empty[threadIdx.x] : 0u;
     const int q = block_append(16 * __popc(wo & ~wl), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
-    const int ql = block_append(16 * __popc(wl), &p.ctl->list_cnt[shard * 32], s_wave, &s_base);
+    const int ql = block_append(16 * __popc(wl & ~we), &p.ctl->list_cnt[shard * 32], s_wave, &s_base);
     if (work) {
       rt_rng rng{p.cur.rng[ws]};
-      gen(ws, wo, wl, 0, q, ql, rng);
+      gen(ws, wo, wl, we, 0, q, ql, rng);
       p.cur.rng[ws] = rng.x;
     }
     flush_counts<kCount>(p, c);
@@ -1036,11 +1048,11 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
   rt_rng rng{hit ? p.cur.rng[slot] : 0ull};
   // more than 32 lights: in chunks of 32 (one bit each), in light order
   for (int base = 0; base < p.nl; base += 32) {
-    uint32_t listed;
-    const uint32_t own = clear_lights(p, slot, hit, base, &listed);
+    uint32_t listed, empty;
+    const uint32_t own = clear_lights(p, slot, hit, base, &listed, &empty);
     const int q = block_append(16 * __popc(own & ~listed), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
-    const int ql = block_append(16 * __popc(listed), &p.ctl->list_cnt[shard * 32], s_wave, &s_base);
-    if (own) gen(slot, own, listed, base, q, ql, rng);
+    const int ql = block_append(16 * __popc(listed & ~empty), &p.ctl->list_cnt[shard * 32], s_wave, &s_base);
+    if (own) gen(slot, own, listed, empty, base, q, ql, rng);
   }
   if (hit) p.cur.rng[slot] = rng.x;
   flush_counts<kCount>(p, c);
@@ -1052,6 +1064,8 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
 // range [0.001, distance) and the Sphere.Hit test of the traversal, so the
 // blocked count is the one the traversal would find.  Candidates four at a
 // time (their loads together, then every ray still clear against them).
+// (One ray per thread, the cone's 16 lanes sharing its loads and a ballot
+// for the count: 41 vs 31 ms per C4 frame.)
 template <bool kCount>
 __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
   const Dense dn = dense(p.ctl->list_cnt);  // (entries: 16 per cone, so no cone spans two shards)
