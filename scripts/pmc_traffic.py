@@ -12,9 +12,9 @@ reports half the bytes of wide streaming reads on gfx950 (x2 here);
 WRITE_SIZE is exact for this code's store patterns (calibrated on
 unpack_kernel, profiles/r02_pmc_calibration.json).
 c2 / c3: the render kernel, the median over its launches.  c4 / c5: the
-soft-shadow traversal kernel (wf_occlude<soft>, the roofline's kernel for
-those configs), summed over a frame's launches (bench.py prices it per
-frame), and the whole frame's bytes beside it.
+soft-shadow stage's kernels (wf_cone, wf_listtest, wf_occlude<soft>: the
+roofline's kernels for those configs), summed over a frame's launches
+(bench.py prices them per frame), and the whole frame's bytes beside it.
 """
 import csv
 import glob
@@ -48,23 +48,23 @@ def main():
     cfg, fdir, wdir, out, frames = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5])
     spec, W, H, SPP, label = CONFIGS[cfg][:5]
     workload = "%s %dx%d %dspp depth 50" % (label, W, H, SPP)
-    kern = KERNELS[cfg].replace("rtgo::", "")
+    kerns = [k.strip() for k in KERNELS[cfg].replace("rtgo::", "").split("+")]  # (c4/c5: the soft-shadow stage)
     fetch = per_dispatch(fdir, "FETCH_SIZE")
     write = per_dispatch(wdir, "WRITE_SIZE")
 
     def pick(rows):
-        return [v for n, v in rows if kern in n]
+        return [v for n, v in rows if any(k in n for k in kerns)]
 
     kf, kw = pick(fetch), pick(write)
     if not kf or not kw:
-        raise SystemExit(f"no {kern} rows")
+        raise SystemExit(f"no {kerns} rows")
     res = {"kernel": KERNELS[cfg], "frames_profiled": frames}
     if cfg in WAVEFRONT:
         fb = sum(kf) / frames * 1024 * 2
         wb = sum(kw) / frames * 1024
         res.update({
             "unit": "per frame (the kernel's launches of one frame)",
-            "launches_per_frame": len(kf) / frames,
+            "launches_per_frame": len(kf) / frames,  # (all three kernels' launches)
             "fetch_bytes_corrected": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
             "frame_fetch_bytes_all_kernels": sum(v for _, v in fetch) / frames * 1024 * 2,
             "frame_write_bytes_all_kernels": sum(v for _, v in write) / frames * 1024,
