@@ -599,21 +599,47 @@ __device__ __forceinline__ int solo_take16(const SoloTries& t, int from) {
   if (ca + __popcll(b) < 16) return -1;
   return 64 + fb + nth_set_bit(b, 16 - ca) + 1;
 }
+// The index after the 16th and after the 32nd accepted try of the 128 (-1:
+// fewer): every lane ranks its two tries among the accepted ones (v_mbcnt)
+// and four ballots find the 16th and the 32nd -- instead of solo_take16's
+// bit-serial search on the critical path (the lights' soft rays take the
+// accepted tries in order: light 0 the first 16, light 1 the next 16, or
+// the first 16 when light 0 takes none).
+__device__ __forceinline__ void solo_take_16_32(const SoloTries& t, int& i16, int& i32) {
+  const int lane = (int)(threadIdx.x & 63);
+  const bool aa = (t.ma >> lane) & 1ull, ab = (t.mb >> lane) & 1ull;
+  const int ra = lanes_below(t.ma) + 1, rb = __popcll(t.ma) + lanes_below(t.mb) + 1;  // ranks, 1-based
+  const unsigned long long a16 = __ballot(aa && ra == 16), b16 = __ballot(ab && rb == 16);
+  const unsigned long long a32 = __ballot(aa && ra == 32), b32 = __ballot(ab && rb == 32);
+  i16 = a16 ? __builtin_ctzll(a16) + 1 : (b16 ? 65 + __builtin_ctzll(b16) : -1);
+  i32 = a32 ? __builtin_ctzll(a32) + 1 : (b32 ? 65 + __builtin_ctzll(b32) : -1);
+}
 
 // RT_WG_TIMING builds: s_memtime clocks of a lone path's bounce by section
 // (solo_clk[k], wave-uniform; scripts/latency_probe.py PROBE_SECTIONS):
 // 0 loop top + closest hit, 1 hit record, 2 stream tries + light vectors +
-// cones + hard rays, 3 soft rays, 4 lighting terms, 5 scatter, 6 bounces.
+// cones + hard rays, 3 soft rays, 4 lighting terms, 5 scatter, 6 bounces;
+// SOLO_S(k), k >= 8: clocks from the start of the current section to that
+// point of it (the parallel-lights form: 8 tries, 9 light vectors, 10 their
+// shuffles, 11 cones + hard rays + ballots; 12 the soft rays of tries
+// 0..63, 13 of tries 64..127; 14 the lighting terms before the sum)
 #ifdef RT_WG_TIMING
-__shared__ unsigned long long solo_clk[8];
+__shared__ unsigned long long solo_clk[16];
 #define SOLO_T(k)                                          \
   do {                                                     \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
     solo_clk[k] += now_ - solo_t0;                         \
     solo_t0 = now_;                                        \
   } while (0)
+#define SOLO_S(k)                                                           \
+  do {                                                                      \
+    solo_clk[k] += __builtin_amdgcn_s_memtime() - solo_t0;                  \
+  } while (0)
 #else
 #define SOLO_T(k) \
+  do {            \
+  } while (0)
+#define SOLO_S(k) \
   do {            \
   } while (0)
 #endif
@@ -655,6 +681,9 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
 #ifdef RT_WG_TIMING
     solo_clk[6] += 1;
 #endif
+    // this bounce's stream tries (the parallel-lights form's soft shadows):
+    // the stream does not move before the lighting, so their integer work
+    // goes ahead of the closest hit, independent of it
     // (1) closest hit (hitWorld, renderer.go:170)
     HitSel hs;
     const bool found = solo_closest(g, o, d, hs);
@@ -697,22 +726,42 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
       // lighting terms per lane li, added to D in light order (the same
       // operations and sums as the loop below, so the same bits)
       const int nl = h.nl, ns = g.ns;
-      // this bounce's stream tries (jump entry 64 read at use: uniform)
       SoloTries tr{};
       if (h.soft) tr = solo_tries(rng.x, jA, jC, jA64, jC64);
+      SOLO_S(8);
       d3 lvd = mk(0, 0, 0);
       double lvl = 0;
+      // the lighting terms' parts that do not depend on the shadows (lane
+      // li < nl, light li): diffuse_strength * intensity and si * intensity,
+      // the left operands of calculateDirectLighting's products, computed
+      // here so their square roots and divisions overlap the light vector's
+      // (the same operations in the same order: the same bits)
+      double di = 0, sii = 0;
+      const double metallic = m->metallic;
       if (lane < nl) {
         const d3 lv = ld3(h.lights[lane].pos) - P;
+        const d3 view = normalize(neg(P));  // (independent of the light: interleaves with lv's chain)
         lvl = sqrt(lv.x * lv.x + lv.y * lv.y + lv.z * lv.z);
         lvd = lvl == 0 ? mk(0, 0, 0) : divs(lv, lvl);
+        const double cos_t = gmax0(dot(N, lvd));
+        const double intensity = cos_t * h.lights[lane].intensity / (lvl * lvl);
+        di = m->diffuse_strength * intensity;
+        if (metallic > 0.5) {
+          const d3 half = normalize(lvd + view);
+          const double hc = gmax0(dot(N, half));
+          const int sp = m->spec_pow;
+          const double si = sp == 64 ? pow_n<64>(hc) : (sp == 48 ? pow_n<48>(hc) : pow_n<32>(hc));
+          sii = si * intensity;
+        }
       }
       // (light values move across lanes by shuffles where they are used: held
       // as wave-uniform values they would take SGPRs the bounce loop needs)
       const unsigned long long litm = __ballot(lane < nl && !(lvl < 0.001));
+      SOLO_S(9);
       const int lj = lane >= ns ? 1 : 0, sj = lane - lj * ns;  // this lane's pair
       const d3 ldj = mk(__shfl(lvd.x, lj), __shfl(lvd.y, lj), __shfl(lvd.z, lj));
       const double dlj = __shfl(lvl, lj);
+      SOLO_S(10);
       bool cone = false, blk = false;
       if (lane < nl * ns && ((litm >> lj) & 1ull)) {
         const DSphere& S = g.spheres[sj];
@@ -725,6 +774,7 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
         }
       }
       const unsigned long long cones = __ballot(cone), blks = __ballot(blk);
+      SOLO_S(11);
       const unsigned long long sm = ns >= 64 ? ~0ull : (1ull << ns) - 1ull;
       const unsigned long long cm0 = cones & sm, cm1 = (cones >> ns) & sm;
       const bool lit0 = litm & 1ull, lit1 = (litm >> 1) & 1ull;
@@ -732,8 +782,10 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
       const bool need0 = lit0 && !occ0 && h.soft, need1 = lit1 && !occ1 && h.soft;
       // soft rays: light 0 takes the 16 accepted tries from try 0, light 1 the
       // 16 after those (a light without soft rays draws nothing)
-      const int e0 = need0 ? solo_take16(tr, 0) : 0;
-      const int e1 = need1 && e0 >= 0 ? solo_take16(tr, e0) : e0;
+      int i16 = -1, i32 = -1;
+      solo_take_16_32(tr, i16, i32);
+      const int e0 = need0 ? i16 : 0;
+      const int e1 = need1 && e0 >= 0 ? (need0 ? i32 : i16) : e0;
       SOLO_T(2);
       int un0 = 16, un1 = 16;
       if (e0 >= 0 && e1 >= 0) {
@@ -760,7 +812,9 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
           }
           cnt0 += __popcll(__ballot(acc && in0 && !occ));
           cnt1 += __popcll(__ballot(acc && in1 && !occ));
+          if (half == 0) SOLO_S(12);
         }
+        SOLO_S(13);
         un0 = cnt0;
         un1 = cnt1;
         // the stream continues after the last try the lights took
@@ -786,24 +840,14 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
       SOLO_T(3);
       // the lighting terms of light lane (< nl), then D in light order
       d3 tdif = mk(0, 0, 0), tspec = mk(0, 0, 0);
-      const double metallic = m->metallic;
       if (lane < nl) {
         const bool occ = lane ? occ1 : occ0;
         const int un = lane ? un1 : un0;
         const double sf = occ ? 0.0 : (h.soft ? (double)un / 16.0 : 1.0);  // shadowSum / 16
-        const DLight& Lt = h.lights[lane];
-        const double cos_t = gmax0(dot(N, lvd));
-        const double intensity = cos_t * Lt.intensity / (lvl * lvl);
-        tdif = muls(ld3(m->albedo), m->diffuse_strength * intensity * sf);
-        if (metallic > 0.5) {
-          const d3 view = normalize(neg(P));
-          const d3 half = normalize(lvd + view);
-          const double hc = gmax0(dot(N, half));
-          const int sp = m->spec_pow;
-          const double si = sp == 64 ? pow_n<64>(hc) : (sp == 48 ? pow_n<48>(hc) : pow_n<32>(hc));
-          tspec = muls(ld3(Lt.color), si * intensity * sf * metallic * 3.0);
-        }
+        tdif = muls(ld3(m->albedo), di * sf);
+        if (metallic > 0.5) tspec = muls(ld3(h.lights[lane].color), sii * sf * metallic * 3.0);
       }
+      SOLO_S(14);
 #pragma unroll
       for (int li = 0; li < 2; ++li) {
         if (li >= nl) break;
@@ -959,7 +1003,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     for (int i = 0; i < kCounters; ++i) c.v[i] = culled.v[i] = 0;
   }
 #ifdef RT_WG_TIMING
-  if (lane < 8) solo_clk[lane] = 0;
+  if (lane < 16) solo_clk[lane] = 0;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   unsigned long long dbg_iter = 0;
   // wave-uniform section clocks (s_memtime): hit, lighting, soft; phase 1 (visibility)
@@ -1570,7 +1614,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       r[37 + i] = dbg_bcnt[i];
     }
     if (solo_clk[6])  // a lone path ran: its section clocks replace the iteration stamps
-      for (int i = 0; i < 8; ++i) r[16 + i] = solo_clk[i];
+      for (int i = 0; i < 16; ++i) r[16 + i] = solo_clk[i];
   }
 #endif
 }

@@ -88,6 +88,10 @@ if os.environ.get("PROBE_SECTIONS"):  # with an RT_WG_TIMING build (RTGO_LIB): s
                 print(f"   solo_path, {nb} bounces, clocks per bounce: " +
                       ", ".join(f"{n} {r[16 + k] / nb:6.0f}" for k, n in enumerate(names)) +
                       f"; total {sum(r[16:22]) / nb:6.0f}", flush=True)
+                sub = ["tries", "light vectors", "their shuffles", "cones+hard+ballots", "soft rays of tries 0-63",
+                       "soft rays of tries 0-127", "lighting terms"]
+                print("   cumulative clocks within a section (parallel-lights form): " +
+                      ", ".join(f"{n} {r[24 + k] / nb:6.0f}" for k, n in enumerate(sub)), flush=True)
         ctx.close()
     sys.exit(0)
 
