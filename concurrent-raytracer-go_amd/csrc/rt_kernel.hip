@@ -517,16 +517,26 @@ __device__ __forceinline__ bool solo_closest(const Geo& g, d3 o, d3 d, HitSel& h
   for (int tri = 0; tri < 2; ++tri) {
     double t = 0, nm = 0, u = 0, v = 0;
     bool f;
+    int myobj = 0;  // (the lane's hittable index, read with its primitive: the replay takes it by readlane)
     if (!tri) {
-      f = lane < g.ns && sphere_query(g.spheres[lane], o, d, a, inv_a, 0.001, __builtin_inf(), nm) != 0;
+      f = false;
+      if (lane < g.ns) {
+        const DSphere& S = g.spheres[lane];
+        myobj = S.obj;
+        f = sphere_query(S, o, d, a, inv_a, 0.001, __builtin_inf(), nm) != 0;
+      }
       if (f) t = nm / a;
     } else {
-      f = lane < g.nt && tri_test(g.tris[lane], o, d, 0.001, __builtin_inf(), t, u, v);
+      f = false;
+      if (lane < g.nt) {
+        myobj = g.tris[lane].obj;
+        f = tri_test(g.tris[lane], o, d, 0.001, __builtin_inf(), t, u, v);
+      }
     }
     for (unsigned long long b = __ballot(f); b; b &= b - 1) {
       const int i = __builtin_ctzll(b);
       const double ti = rld(t, i);
-      const int obj = tri ? g.tris[i].obj : g.spheres[i].obj;
+      const int obj = (int)rl32((uint32_t)myobj, i);
       if (closest < ti || (ti == closest && best_obj > obj)) continue;
       closest = ti;
       best_obj = obj;
@@ -792,6 +802,7 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
         int cnt0 = 0, cnt1 = 0;
 #pragma unroll
         for (int half = 0; half < 2; ++half) {  // try lane, then try 64 + lane
+          if (half == 1 && e0 <= 64 && e1 <= 64) break;  // (the lights took tries of the first 64 only)
           const int k = lane + 64 * half;
           const bool acc = ((half ? tr.mb : tr.ma) >> lane) & 1ull;
           const bool in0 = need0 && k < e0, in1 = need1 && k >= e0 && k < e1;
