@@ -278,6 +278,24 @@ int rt_context_create(int32_t device, rt_context** out) {
     return RT_E_DEVICE;
   }
   HIP_TRY(hipSetDevice(device));
+  {
+    // the kernels' code objects, once per device and process: the
+    // constructor's work (NewParallelRenderer), not the first Render's
+    static std::mutex mu;
+    static std::vector<bool> loaded;
+    std::lock_guard<std::mutex> lock(mu);
+    if ((int)loaded.size() < n) loaded.resize(n, false);
+    if (!loaded[device]) {
+      hipError_t e = (hipError_t)preload_render_kernels();
+      if (e == hipSuccess) e = (hipError_t)preload_sched_kernels();
+      if (e == hipSuccess) e = (hipError_t)preload_wf_kernels();
+      if (e != hipSuccess) {
+        set_error(std::string("kernel code object load failed: ") + hipGetErrorString(e));
+        return RT_E_DEVICE;
+      }
+      loaded[device] = true;
+    }
+  }
   rt_context* c = new rt_context();
   c->device = device;
   rt_tuning_default(&c->tun);

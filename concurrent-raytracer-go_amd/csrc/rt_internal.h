@@ -283,6 +283,11 @@ constexpr int kWfProfEvents = kWfClasses + 1;  // (one block serves any class ra
 int wf_launch_bounce(const WfParams& p, bool first, bool count, void* stream, const void* prof);
 // Quantized nodes the traversal kernels can stage in LDS next to their stacks
 // (all of them when they fit; else an odd count, so no child pair is split).
+// Load each kernel file's code object onto the current device (HIP loads
+// them lazily, at a file's first launch otherwise): rt_context_create.
+int preload_render_kernels();
+int preload_sched_kernels();
+int preload_wf_kernels();
 int wf_lds_nodes(int stack_depth, int nodes, int block, int wgs_per_cu);
 int wf_launch_resolve(const WfParams& p, int npix, void* stream);
 

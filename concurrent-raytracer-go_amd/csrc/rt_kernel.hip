@@ -1684,6 +1684,14 @@ size_t render_shmem(const KParams& p) {
   return (size_t)p.stack_off + (p.use_bvh ? sizeof(int) * p.stack_depth * 64 : 0);
 }
 
+// Loads this file's code object onto the current device now: with HIP's lazy
+// loading it would otherwise be loaded inside the first render launch
+// (rt_context_create calls it once per device and process).
+int preload_render_kernels() {
+  hipFuncAttributes a;
+  return (int)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(render_kernel<false, true, false, false>));
+}
+
 int launch_render(const KParams& pin, bool count, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (pin.num_wgs <= 0) return hipSuccess;

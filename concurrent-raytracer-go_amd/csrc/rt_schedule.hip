@@ -424,6 +424,12 @@ void sched_layout(void* scratch, int local, SchedParams* p) {
   p->totals = p->cursor + kBuckets;
 }
 
+// (see preload_render_kernels)
+int preload_sched_kernels() {
+  hipFuncAttributes a;
+  return (int)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(sched_est));
+}
+
 int sched_launch_pixels(const SchedParams& p, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (p.local <= 0) return hipSuccess;

@@ -1471,6 +1471,12 @@ int wf_launch_bounce(const WfParams& p, bool first, bool count, void* stream, co
   return count ? enqueue_bounce<true>(p, st, ev) : enqueue_bounce<false>(p, st, ev);
 }
 
+// (see preload_render_kernels)
+int preload_wf_kernels() {
+  hipFuncAttributes a;
+  return (int)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(wf_book));
+}
+
 int wf_launch_resolve(const WfParams& p, int npix, void* stream) {
   if (npix <= 0) return hipSuccess;
   hipLaunchKernelGGL(wf_resolve, dim3((npix + kWfBlock - 1) / kWfBlock), dim3(kWfBlock), 0, (hipStream_t)stream, p,

@@ -9,8 +9,11 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/profiles_${R}
 mkdir -p $O
+# (one frame per launch, one launch in flight: the launches rocprof averages
+# are the one-frame launches whose HIP-event time the roofline uses)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${R}_trace -o run --output-format csv \
-  -- python3 bench.py --no-cpu-baseline --no-e2e > $O/${R}_bench_under_rocprof.json
+  -- python3 bench.py --no-cpu-baseline --no-e2e --frames-per-launch 1 --frames-in-flight 1 \
+  > $O/${R}_bench_under_rocprof.json
 cp "$(find gpurun_out/prof_${R}_trace -name '*kernel_stats.csv' | head -1)" $O/${R}_kernel_stats.csv
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${R}_c4trace -o run --output-format csv \
   -- python3 bench.py --config c4 --steps 2 --no-cpu-baseline > $O/${R}_c4_bench_under_rocprof.json
