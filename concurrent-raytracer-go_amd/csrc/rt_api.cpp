@@ -302,6 +302,21 @@ int rt_context_create(int32_t device, rt_context** out) {
   hipError_t e = (hipError_t)dev_stream_get(&c->stream);
   if (e == hipSuccess) e = (hipError_t)dev_event_get(&c->ev0);
   if (e == hipSuccess) e = (hipError_t)dev_event_get(&c->ev1);
+  {
+    // the runtime's first-launch / first-copy set-up, once per device and
+    // process, on the context's stream (constructor work, as above)
+    static std::mutex mu;
+    static std::vector<bool> warmed;
+    std::lock_guard<std::mutex> lock(mu);
+    if ((int)warmed.size() < n) warmed.resize(n, false);
+    if (e == hipSuccess && !warmed[device]) {
+      void* d4 = nullptr;
+      e = (hipError_t)dev_alloc(&d4, 4096);
+      if (e == hipSuccess) e = (hipError_t)warm_device(c->stream, d4);
+      dev_free(d4);
+      if (e == hipSuccess) warmed[device] = true;
+    }
+  }
 
   if (e != hipSuccess) {
     set_error(std::string("context init failed: ") + hipGetErrorString(e));

@@ -286,6 +286,9 @@ int wf_launch_bounce(const WfParams& p, bool first, bool count, void* stream, co
 // Load each kernel file's code object onto the current device (HIP loads
 // them lazily, at a file's first launch otherwise): rt_context_create.
 int preload_render_kernels();
+// An empty launch and a 4-KB copy each way on the stream (dev4k: 4 KB of
+// device memory): the runtime's first-launch and first-copy set-up.
+int warm_device(void* stream, void* dev4k);
 int preload_sched_kernels();
 int preload_wf_kernels();
 int wf_lds_nodes(int stack_depth, int nodes, int block, int wgs_per_cu);

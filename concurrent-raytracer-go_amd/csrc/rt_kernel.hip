@@ -1692,6 +1692,23 @@ int preload_render_kernels() {
   return (int)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(render_kernel<false, true, false, false>));
 }
 
+// An empty launch and a small copy each way on `stream`: the runtime's
+// first-launch and first-copy set-up (kernel argument pool, staging
+// buffers) happens here instead of inside the first render.
+__global__ void warm_kernel(int* p) {
+  if (p && threadIdx.x == 0 && blockIdx.x == 0) p[0] = 0;
+}
+int warm_device(void* stream, void* dev4k) {
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(warm_kernel, dim3(1), dim3(64), 0, st, (int*)dev4k);
+  static thread_local unsigned char host[4096];
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(dev4k, host, sizeof host, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(host, dev4k, sizeof host, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  return (int)e;
+}
+
 int launch_render(const KParams& pin, bool count, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (pin.num_wgs <= 0) return hipSuccess;

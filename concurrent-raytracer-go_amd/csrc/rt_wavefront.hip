@@ -1065,7 +1065,8 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
 // blocked count is the one the traversal would find.  Candidates four at a
 // time (their loads together, then every ray still clear against them).
 // (One ray per thread, the cone's 16 lanes sharing its loads and a ballot
-// for the count: 41 vs 31 ms per C4 frame.)
+// for the count: 41 vs 31 ms per C4 frame; rays outer, each entry read once
+// and the candidates re-read from L2 per ray: 51 vs 31 ms.)
 template <bool kCount>
 __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
   const Dense dn = dense(p.ctl->list_cnt);  // (entries: 16 per cone, so no cone spans two shards)
