@@ -132,3 +132,73 @@ def test_more_than_1024_samples_on_both_bvh_paths():
         lin, rgba, _ = _render(scene, w, h, st, mega)
         assert lin.tobytes() == ref32.tobytes(), mega
         assert rgba.tobytes() == ref_rgba.reshape(-1, 4).tobytes(), mega
+
+
+@pytest.mark.parametrize("name", sorted(__import__("scene_cases").EDGE_SCENES))
+def test_cone_edge_scenes_on_the_wavefront_path(name):
+    """The shadow cones of the wavefront path (wf_cone's binary32 node test
+    and binary64 sphere test, the hit sphere's exclusion)
+    at the culling edge scenes: radius-1e6 ground, coordinates near 1e5,
+    radius-1e-3 spheres seen from 2 cm, lights 2e-3 above a surface.  The
+    scene's spheres (cubes dropped: the BVH path is sphere-only) through the
+    forced BVH, against the oracle's linear scan."""
+    from scene_cases import EDGE_SCENES
+
+    sc = copy.deepcopy(EDGE_SCENES[name])
+    sc["objects"] = [o for o in sc["objects"] if o["type"] == "sphere"]
+    scene = rtgo.Scene.from_json_text(json.dumps(sc))
+    w, h = 60, 40
+    for seed in (1, 2):
+        st = make_settings(rtgo, {"samples": 4}, seed)
+        lin, rgba, _ = _render(scene, w, h, st, mega=False, force_bvh=1)
+        ref, ref_rgba, _ = oracle.render(scene, w, h, st)
+        assert lin.reshape(h, w, 3).tobytes() == ref.astype(np.float32).tobytes(), (name, seed)
+        assert rgba.reshape(h, w, 4).tobytes() == ref_rgba.tobytes(), (name, seed)
+
+
+def _curtain_scene():
+    """Spheres under a light with a dense curtain of 360 small spheres
+    between them: the clear hard rays' shadow cones meet from zero to many
+    candidates, so every soft-shadow route of the wavefront path runs
+    (empty cone, a candidate list, more than 16 candidates: traced)."""
+    objs = [{"type": "sphere", "position": [0, -1001, -8], "radius": 1000,
+             "material": {"type": "lambertian", "color": [0.6, 0.6, 0.5]}}]
+    for i in range(9):
+        objs.append({"type": "sphere", "position": [-4 + i, -0.3, -8 - (i % 3)], "radius": 0.6,
+                     "material": {"type": ["metal", "glass", "lambertian"][i % 3], "color": [0.8, 0.7, 0.6],
+                                  "roughness": 0.05}})
+    for i in range(360):  # a 24 x 15 curtain at y = 3, gaps of ~0.1
+        x, z = i % 24, i // 24
+        objs.append({"type": "sphere", "position": [-6 + 0.5 * x, 3.0, -4 - 0.5 * z], "radius": 0.2,
+                     "material": {"type": "lambertian", "color": [0.3, 0.4, 0.8]}})
+    return {"camera": {"position": [0, 1, 2], "aspectRatio": 1.5}, "objects": objs,
+            "lights": [{"position": [1, 9, -7], "color": [1, 1, 1], "intensity": 200},
+                       {"position": [-9, 4, -2], "color": [1, 0.9, 0.8], "intensity": 120}]}
+
+
+def test_cone_routes_match_megakernel_and_oracle():
+    scene = rtgo.Scene.from_json_text(json.dumps(_curtain_scene()))
+    st = make_settings(rtgo, {"samples": 4, "max_depth": 6})
+    w, h = 60, 40
+    lw, rw, cw = _render(scene, w, h, st, mega=False, count=True)
+    lm, rm, cm = _render(scene, w, h, st, mega=True, count=True)
+    assert lw.tobytes() == lm.tobytes() and rw.tobytes() == rm.tobytes()
+    assert {k: cw[k] for k in PATH_KEYS} == {k: cm[k] for k in PATH_KEYS}
+    ref, ref_rgba, _ = oracle.render(scene, w, h, st)
+    assert lw.reshape(h, w, 3).tobytes() == ref.astype(np.float32).tobytes()
+    assert rw.reshape(h, w, 4).tobytes() == ref_rgba.tobytes()
+    # every route ran: soft rays traced through the BVH (cones with more
+    # than 16 candidates) and list tests (the soft stage's sphere tests
+    # exceed what its traced rays' leaves alone would give)
+    ctx = rtgo.Context(0)
+    ctx.set_tuning(rtgo.default_tuning())
+    ctx.set_scene(scene)
+    import torch
+
+    lin = torch.zeros(w * h * 3, dtype=torch.float32, device="cuda")
+    c = ctx.count(w, h, st, lin.data_ptr(), 0, full=True)
+    soft = c.soft_occlusion_dict()
+    ctx.close()
+    assert soft["shadow_rays"] > 0, soft                     # traced (overflowing cones)
+    assert soft["shadow_rays"] < c.shadow_rays, (soft, c.shadow_rays)  # not all: lists and empty cones
+    assert soft["sphere_tests"] > 0 and soft["box_tests"] > 0
