@@ -553,7 +553,19 @@ def main():
         # host-side coordination only (barriers, the max over ranks, the RCCL
         # id, the partition check); the frame's data moves through librtgo's
         # RCCL communicator
-        dist.init_process_group("gloo")
+        # (gloo prints its "[Gloo] Rank r is connected to ..." lines on stdout
+        # while the group forms: sent to stderr, so stdout holds the one JSON
+        # line only)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
 
     cfg = args.config
     spec, W, H, spp, label, steps_default, fif_default = CONFIGS[cfg]
@@ -760,7 +772,9 @@ def main():
             },
             "rank_kernel_ms": [round(x, 4) for x in rank_kernel_ms],
             "check_equals_one_rank": check,
-            "rank_estimated_work": [round(part.work(r)) for r in range(world)] if world > 1 else None,
+            # (a strided partition carries no estimate: null)
+            "rank_estimated_work": ([round(part.work(r)) for r in range(world)]
+                                    if world > 1 and part_kind and part_kind.startswith("balanced") else None),
             "counts_rank0": counts.as_dict(),
             "counts_rank0_executed": ex,
             "cpu_baseline": cpu,
