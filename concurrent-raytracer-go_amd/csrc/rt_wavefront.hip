@@ -72,6 +72,9 @@ constexpr int kLdsBytes = 160 * 1024;    // LDS per CU (MI355X), all of it avail
 #ifndef RT_WF_CONES
 #define RT_WF_CONES 1  // soft shadows through shadow cones (0: every soft ray traced; A/B builds)
 #endif
+#ifndef RT_LIST_SORT
+#define RT_LIST_SORT 1
+#endif
 #ifndef RT_WF_CHUNK
 #define RT_WF_CHUNK 128
 #endif
@@ -1071,10 +1074,40 @@ template <bool kCount>
 __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
   const Dense dn = dense(p.ctl->list_cnt);  // (entries: 16 per cone, so no cone spans two shards)
   const int n = dn.start[kWfShards] / 16;
-  const int j = blockIdx.x * kWfBlock + threadIdx.x;
+  if ((int)(blockIdx.x * kWfBlock) >= n) return;
+  int j = blockIdx.x * kWfBlock + threadIdx.x;
   Counters c;
   if constexpr (kCount)
     for (int k = 0; k < 9; ++k) c.v[k] = 0;
+#if RT_LIST_SORT
+  // the workgroup's cones ordered by their candidate groups of four (1..4),
+  // so a wave's lanes loop over about as many groups each (a wave waits
+  // for its longest list)
+  {
+    __shared__ int s_bucket[4], s_order[kWfBlock];
+    if (threadIdx.x < 4) s_bucket[threadIdx.x] = 0;
+    __syncthreads();
+    int b = 0;
+    if (j < n) {
+      const size_t at = dense_at(dn, 16 * j, p.soft_cap);
+      const size_t sh = at / (size_t)p.soft_cap, off = at - sh * (size_t)p.soft_cap;
+      const uint32_t key = reinterpret_cast<const uint4*>(p.softq)[sh * (size_t)p.soft_cap + (p.soft_cap - off - 16)].x;
+      // groups of four up to the one holding the list's end (-1; entries
+      // past it are stale): bucket 1, 2, 3-4, 5+ groups
+      const int4* cl = reinterpret_cast<const int4*>(p.cand + (size_t)key * kWfConeK);
+      int g = 1;
+      while (g < kWfConeK / 4 && (cl[g - 1].x | cl[g - 1].y | cl[g - 1].z | cl[g - 1].w) >= 0) ++g;
+      b = g == 1 ? 0 : (g == 2 ? 1 : (g <= 4 ? 2 : 3));
+    }
+    const int pos = atomicAdd(&s_bucket[b], 1);
+    __syncthreads();
+    int base = 0;
+    for (int k = 0; k < b; ++k) base += s_bucket[k];
+    s_order[base + pos] = j;
+    __syncthreads();
+    j = s_order[threadIdx.x];
+  }
+#endif
   if (j < n) {
     const size_t at = dense_at(dn, 16 * j, p.soft_cap);
     const size_t sh = at / (size_t)p.soft_cap, off = at - sh * (size_t)p.soft_cap;

@@ -48,7 +48,7 @@ def _worker(rank, world, port, outdir):
         nb = rtgo.packed_bytes(W, H, world)
         g = torch.empty(world * nb, dtype=torch.uint8) if rank == 0 else None
         g = shard.gather_packed(dist, share, world, rank, g)
-        # per-rank work sums to the whole frame (weak-scaling accounting in bench.py)
+        # per-rank work sums to the whole frame (bench.py's value: all ranks' rays / the slowest rank's time)
         cam = torch.tensor([counts["camera_rays"]], dtype=torch.int64)
         dist.all_reduce(cam)
         if rank == 0:

@@ -3,8 +3,10 @@
 - C2 / C3 (the headline 800x600x100 and silver 1200x900x100): the kernel
   against the CPU oracle over the whole frame, bit for bit (the oracle runs
   them in well under a second on 16 host threads).
-- The weak-scaling frame of `bench.py --gpus 8` (800 x 4800 x 100): the
-  eight ranks' packed tiles, gathered and unpacked, equal the one-rank image.
+- The frame of `bench.py --gpus 8 --weak` (800 x 4800 x 100, strided
+  tiles): the eight ranks' packed tiles, gathered and unpacked, equal the
+  one-rank image.  (The default N-GPU bench strong-scales 800x600x100
+  through the balanced partition: tests/test_gpu_partition.py.)
 - C4 (10k spheres 1920x1080x64): the 10k-sphere linear-scan oracle is out of
   reach at this size (~10^13 sphere tests), so the wavefront path is checked
   against the megakernel's BVH traversal (a different traversal order and
@@ -49,9 +51,9 @@ def test_full_frame_matches_oracle(name, w, h):
 
 
 def test_weak_scaling_frame_of_eight_ranks_equals_one():
-    """bench.py --gpus 8 renders 800 x (600*8) split over 8 ranks (tile t ->
-    rank t % 8) and gathers packed tiles to rank 0: the assembled frame is
-    the single-rank frame."""
+    """bench.py --gpus 8 --weak renders 800 x (600*8) split over 8 ranks
+    (tile t -> rank t % 8) and gathers packed tiles to rank 0: the assembled
+    frame is the single-rank frame."""
     scene = rtgo.Scene.load_from_file(scene_path("sphere_reflections_light_facing.json"))
     st = make_settings(rtgo, {"samples": 100}, seed=1)
     w, h, world = 800, 600 * 8, 8
