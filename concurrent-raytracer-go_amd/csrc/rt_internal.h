@@ -216,7 +216,7 @@ constexpr uint32_t kDeadSid = 0xFFFFFFFFu;  // a slot with no sample (out-of-ima
 // soft shadows: candidate spheres kept per shadow cone (more: its rays are
 // traced).  Host allocation and kernels must agree: a constant, not a build
 // knob (C4: 16 -> 412.6 ms per frame, 24 -> 416.0, 32 -> 421.1)
-constexpr int kWfConeK = 32;
+constexpr int kWfConeK = 16;
 struct WfCtl {                 // device-resident loop state; counters of shard s at [32 s] (own 128-B line)
   int32_t cur_cnt[kWfShards * 32];   // live paths per shard of the current array
   int32_t next_cnt[kWfShards * 32];  // survivors appended per shard of the next array

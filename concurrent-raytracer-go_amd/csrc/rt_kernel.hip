@@ -628,7 +628,8 @@ __device__ __forceinline__ void solo_take_16_32(const SoloTries& t, int& i16, in
 // RT_WG_TIMING builds: s_memtime clocks of a lone path's bounce by section
 // (solo_clk[k], wave-uniform; scripts/latency_probe.py PROBE_SECTIONS):
 // 0 loop top + closest hit, 1 hit record, 2 stream tries + light vectors +
-// cones + hard rays, 3 soft rays, 4 lighting terms, 5 scatter, 6 bounces;
+// cones + hard rays, 3 soft rays, 4 lighting terms, 5 scatter, 6 bounces,
+// 7 entries;
 // SOLO_S(k), k >= 8: clocks from the start of the current section to that
 // point of it (the parallel-lights form: 8 tries, 9 light vectors, 10 their
 // shuffles, 11 cones + hard rays + ballots; 12 the soft rays of tries
@@ -684,6 +685,9 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
     jC64 = h0.jump[129];
     asm volatile("" : "+v"(jA64), "+v"(jC64));
   }
+#ifdef RT_WG_TIMING
+  solo_clk[7] += 1;
+#endif
   for (;;) {
     const Hot h = hot<true>();
     const Geo& g = h.g;
@@ -1626,6 +1630,8 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     }
     if (solo_clk[6])  // a lone path ran: its section clocks replace the iteration stamps
       for (int i = 0; i < 16; ++i) r[16 + i] = solo_clk[i];
+    r[42] = solo_clk[6];  // lone-path bounces (0: none ran)
+    r[43] = solo_clk[7];  // entries into solo_path
   }
 #endif
 }

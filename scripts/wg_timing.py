@@ -98,9 +98,9 @@ for i in order[:4]:
 late = end.max(axis=1) > 0.7 * span
 print(f"  WGs ending after 70% of the span: {int(late.sum())}; of them split {int((d[late, 0, 14] > 0).sum())}, "
       f"mean iters {it[late].mean():.0f}, mean start {start[late].mean():.0f} us")
-solo = d[:, 0, 22] != 0  # (a lone path ran: solo_path's bounce count replaces the iteration stamps)
-print(f"  WGs that ran a lone path (solo_path): {int(solo.sum())} of {nwg}; lone-path bounces "
-      f"{int(d[solo, 0, 22].sum())}")
+solo = d[:, 0, 42] != 0  # lone-path bounces (slot 42) / entries into solo_path (slot 43)
+print(f"  WGs that ran a lone path (solo_path): {int(solo.sum())} of {nwg}; entries {int(d[:, 0, 43].sum())}, "
+      f"lone-path bounces {int(d[:, 0, 42].sum())}")
 busy = dur.sum()
 print(f"  mean waves in flight {busy / span:.1f}")
 bclk = d[:, 0, 32:37].astype(np.float64)
