@@ -695,9 +695,6 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
 #ifdef RT_WG_TIMING
     solo_clk[6] += 1;
 #endif
-    // this bounce's stream tries (the parallel-lights form's soft shadows):
-    // the stream does not move before the lighting, so their integer work
-    // goes ahead of the closest hit, independent of it
     // (1) closest hit (hitWorld, renderer.go:170)
     HitSel hs;
     const bool found = solo_closest(g, o, d, hs);
