@@ -215,7 +215,8 @@ constexpr int kWfTravBlock = 1024;     // ... of the traversal kernels (extend, 
 constexpr uint32_t kDeadSid = 0xFFFFFFFFu;  // a slot with no sample (out-of-image pixel of an edge tile)
 // soft shadows: candidate spheres kept per shadow cone (more: its rays are
 // traced).  Host allocation and kernels must agree: a constant, not a build
-// knob (C4: 16 -> 412.6 ms per frame, 24 -> 416.0, 32 -> 421.1)
+// knob (C4: 16 -> 412.6 ms per frame, 24 -> 416.0, 32 -> 421.1; with the
+// list tests ordered by length: 16 -> 403.4, 32 -> 405.7)
 constexpr int kWfConeK = 16;
 struct WfCtl {                 // device-resident loop state; counters of shard s at [32 s] (own 128-B line)
   int32_t cur_cnt[kWfShards * 32];   // live paths per shard of the current array
