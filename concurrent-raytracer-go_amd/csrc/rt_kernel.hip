@@ -778,11 +778,12 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
         const DSphere& S = g.spheres[sj];
         const bool self_out = front && dot(N, ldj) >= KC(0.1015);
         cone = !(self_out && S.obj == self && S.r > 0) && in_cone(S.c, S.r, P, ldj, dlj);
-        if (cone) {
-          const double a = len2(ldj);
-          double num;
-          blk = sphere_query(S, P, ldj, a, approx_rcp(a), 0.001, dlj, num) != 0;
-        }
+        // the hard ray against every sphere, as hitWorld does, independent
+        // of the cone test so the two chains overlap (a sphere outside the
+        // cone cannot be hit: the same answer as testing the candidates only)
+        const double a = len2(ldj);
+        double num;
+        blk = sphere_query(S, P, ldj, a, approx_rcp(a), 0.001, dlj, num) != 0;
       }
       const unsigned long long cones = __ballot(cone), blks = __ballot(blk);
       SOLO_S(11);
