@@ -68,7 +68,7 @@ static std::string rfc3339nano_now() {
     while (n > 1 && frac[n - 1] == '0') frac[--n] = 0;
   }
   long off = tmv.tm_gmtoff;
-  char tz[16];
+  char tz[24];
   if (off == 0)
     snprintf(tz, sizeof tz, "Z");
   else
