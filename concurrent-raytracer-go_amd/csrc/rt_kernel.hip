@@ -49,6 +49,11 @@
 // cooperative soft shadows when at most this many lanes need them (measured
 // best of 0/2/4/8 in round 1; 4 and 16 within noise in round 2)
 constexpr int kCoopMax = 8;
+// soft_queue: the owners still drawing finish cooperatively once at most
+// this many are left (0: never)
+#ifndef RT_SQ_TAIL
+#define RT_SQ_TAIL 2
+#endif
 
 namespace rtgo {
 
@@ -314,36 +319,100 @@ __device__ __forceinline__ CoopOut soft_coop(const Geo p, bool masks, bool trace
 // traced does not change it.  Returns the owner's count (0 elsewhere).
 template <bool kCount>
 __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_soft, bool trace, d3 P, d3 ldir,
-                                          double ldist, Cand cm, rt_rng& rng, int* stack, Counters& c) {
-  __shared__ uint4 sq[128];   // queued points: raw draws x, y, z, owner lane (a ring)
+                                          double ldist, Cand cm, rt_rng& rng, const uint64_t* jump, int* stack,
+                                          Counters& c) {
+  __shared__ uint4 sq[256];  // queued points: raw draws x, y, z, owner lane (a ring)
   __shared__ int sq_unocc[64];  // per owner: unoccluded rays
   const int lane = (int)(threadIdx.x & 63);
   sq_unocc[lane] = 0;
   int need = need_soft ? 16 : 0, free_rays = 0;  // free_rays: points of an owner with nothing to trace
   int head = 0, tail = 0;  // wave-uniform ring positions
   for (;;) {
-    bool acc = false;
-    uint32_t ux = 0, uy = 0, uz = 0;
+    // Two tries per pass: the second is drawn ahead and consumed only when
+    // the owner still needs a point after the first (then the stream
+    // advances by exactly the draws the sequential loop takes).
+    bool acc0 = false, acc1 = false;
+    uint32_t ux = 0, uy = 0, uz = 0, vx = 0, vy = 0, vz = 0;
     if (need > 0) {
       ux = rt_rng_next(&rng);
       uy = rt_rng_next(&rng);
       uz = rt_rng_next(&rng);
+      rt_rng r2 = rng;
+      vx = rt_rng_next(&r2);
+      vy = rt_rng_next(&r2);
+      vz = rt_rng_next(&r2);
       cnt<kCount>(c, C_RNG, 3);
       if (unit_ball_accept(ux, uy, uz)) {
         --need;
         cnt<kCount>(c, C_SHADOW);
-        if (trace) acc = true;  // only rays that can be blocked are queued
+        if (trace) acc0 = true;  // only rays that can be blocked are queued
         else ++free_rays;
       }
+      if (need > 0) {
+        rng = r2;
+        cnt<kCount>(c, C_RNG, 3);
+        if (unit_ball_accept(vx, vy, vz)) {
+          --need;
+          cnt<kCount>(c, C_SHADOW);
+          if (trace) acc1 = true;
+          else ++free_rays;
+        }
+      }
     }
-    const unsigned long long am = __ballot(acc);
-    if (acc) sq[(tail + lanes_below(am)) & 127] = make_uint4(ux, uy, uz, (uint32_t)lane);
-    tail += __popcll(am);
+    const unsigned long long am0 = __ballot(acc0), am1 = __ballot(acc1);
+    if (acc0) sq[(tail + lanes_below(am0)) & 255] = make_uint4(ux, uy, uz, (uint32_t)lane);
+    tail += __popcll(am0);
+    if (acc1) sq[(tail + lanes_below(am1)) & 255] = make_uint4(vx, vy, vz, (uint32_t)lane);
+    tail += __popcll(am1);
+#if RT_SQ_TAIL > 0
+    // The last few owners still drawing finish cooperatively, one at a
+    // time: lane h evaluates try h of the owner's stream (jump table), as
+    // in soft_coop; the first `need` accepted tries are its points, queued
+    // in try order, and the stream advances past the last one taken.  The
+    // wave no longer loops on its unluckiest owners' tries one by one.
+    // (tail - head < 64 here, plus at most 16 points per owner: the ring holds them.)
+    const unsigned long long rem = __ballot(need > 0);
+    if (rem != 0 && __popcll(rem) <= RT_SQ_TAIL) {
+      for (unsigned long long b = rem; b; b &= b - 1) {
+        const int ow = __builtin_ctzll(b);
+        int nd = __builtin_amdgcn_readlane(need, ow);
+        const bool tr = __builtin_amdgcn_readlane(trace ? 1 : 0, ow) != 0;
+        uint64_t x = rl64(rng.x, ow);
+        int got = 0, tries = 0;
+        while (nd > 0) {
+          const uint64_t x0 = state_at3(x, jump, lane), x1 = x0 * RT_PCG_MULT + RT_PCG_INC,
+                         x2 = x1 * RT_PCG_MULT + RT_PCG_INC;
+          const uint32_t o0 = rt_pcg_out(x0), o1 = rt_pcg_out(x1), o2 = rt_pcg_out(x2);
+          const bool acc = unit_ball_accept(o0, o1, o2);
+          const unsigned long long am = __ballot(acc);
+          const bool chosen = acc && lanes_below(am) < nd;
+          const unsigned long long chm = __ballot(chosen);
+          const int nch = __popcll(chm);
+          const int used = nch == nd ? 64 - __clzll(chm) : 64;
+          if (tr) {
+            if (chosen) sq[(tail + lanes_below(chm)) & 255] = make_uint4(o0, o1, o2, (uint32_t)ow);
+            tail += nch;
+          }
+          got += nch;
+          nd -= nch;
+          tries += used;
+          x = state_at3(x, jump, used);
+        }
+        if (lane == ow) {
+          rng.x = x;
+          need = 0;
+          if (!tr) free_rays += got;
+          cnt<kCount>(c, C_RNG, 3ull * tries);
+          cnt<kCount>(c, C_SHADOW, got);
+        }
+      }
+    }
+#endif
     const bool more = __ballot(need > 0) != 0;
-    if (tail - head >= 64 || (!more && tail > head)) {
+    while (tail - head >= 64 || (!more && tail > head)) {
       __syncthreads();
       const int n = min(64, tail - head);
-      const uint4 e = sq[(head + lane) & 127];
+      const uint4 e = sq[(head + lane) & 255];
       const int ow = lane < n ? (int)e.w : lane;
       // the owner's ray inputs, read across lanes (every lane takes part)
       const d3 Po = mk(__shfl(P.x, ow), __shfl(P.y, ow), __shfl(P.z, ow));
@@ -1450,7 +1519,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
                 }
               }
             } else {
-              unocc = soft_queue<kCount>(gg, masks, need_soft, trace, P, ldir, ldist, cm, rng, stack, c);
+              unocc = soft_queue<kCount>(gg, masks, need_soft, trace, P, ldir, ldist, cm, rng, h.jump, stack, c);
             }
           }
 #ifdef RT_WG_TIMING
