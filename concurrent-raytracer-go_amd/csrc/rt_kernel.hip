@@ -48,7 +48,10 @@
 #endif
 // cooperative soft shadows when at most this many lanes need them (measured
 // best of 0/2/4/8 in round 1; 4 and 16 within noise in round 2)
-constexpr int kCoopMax = 8;
+#ifndef RT_COOP_MAX
+#define RT_COOP_MAX 8
+#endif
+constexpr int kCoopMax = RT_COOP_MAX;
 // soft_queue: the owners still drawing finish cooperatively once at most
 // this many are left (0: never)
 #ifndef RT_SQ_TAIL
