@@ -57,6 +57,10 @@ constexpr int kCoopMax = RT_COOP_MAX;
 #ifndef RT_SQ_TAIL
 #define RT_SQ_TAIL 2
 #endif
+// soft_queue: rejection tries per pass of its loop
+#ifndef RT_SQ_TRIES
+#define RT_SQ_TRIES 2
+#endif
 
 namespace rtgo {
 
@@ -331,49 +335,51 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
   int need = need_soft ? 16 : 0, free_rays = 0;  // free_rays: points of an owner with nothing to trace
   int head = 0, tail = 0;  // wave-uniform ring positions
   for (;;) {
-    // Two tries per pass: the second is drawn ahead and consumed only when
-    // the owner still needs a point after the first (then the stream
-    // advances by exactly the draws the sequential loop takes).
-    bool acc0 = false, acc1 = false;
-    uint32_t ux = 0, uy = 0, uz = 0, vx = 0, vy = 0, vz = 0;
+    // RT_SQ_TRIES tries per pass: the later tries are drawn ahead and each
+    // is consumed only when the owner still needs a point after the ones
+    // before it (so the stream advances by exactly the draws the sequential
+    // loop takes).
+    constexpr int K = RT_SQ_TRIES;
+    static_assert(64 * K + 63 + 16 * RT_SQ_TAIL <= 256, "soft_queue ring too small");
+    bool acc[K];
+    uint32_t u[K][3];
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      acc[t] = false;
+      u[t][0] = u[t][1] = u[t][2] = 0;
+    }
     if (need > 0) {
-      ux = rt_rng_next(&rng);
-      uy = rt_rng_next(&rng);
-      uz = rt_rng_next(&rng);
-      rt_rng r2 = rng;
-      vx = rt_rng_next(&r2);
-      vy = rt_rng_next(&r2);
-      vz = rt_rng_next(&r2);
-      cnt<kCount>(c, C_RNG, 3);
-      if (unit_ball_accept(ux, uy, uz)) {
-        --need;
-        cnt<kCount>(c, C_SHADOW);
-        if (trace) acc0 = true;  // only rays that can be blocked are queued
-        else ++free_rays;
-      }
-      if (need > 0) {
-        rng = r2;
-        cnt<kCount>(c, C_RNG, 3);
-        if (unit_ball_accept(vx, vy, vz)) {
-          --need;
-          cnt<kCount>(c, C_SHADOW);
-          if (trace) acc1 = true;
-          else ++free_rays;
+      rt_rng r = rng;
+#pragma unroll
+      for (int t = 0; t < K; ++t) {
+        u[t][0] = rt_rng_next(&r);
+        u[t][1] = rt_rng_next(&r);
+        u[t][2] = rt_rng_next(&r);
+        if (need > 0) {
+          rng = r;
+          cnt<kCount>(c, C_RNG, 3);
+          if (unit_ball_accept(u[t][0], u[t][1], u[t][2])) {
+            --need;
+            cnt<kCount>(c, C_SHADOW);
+            if (trace) acc[t] = true;  // only rays that can be blocked are queued
+            else ++free_rays;
+          }
         }
       }
     }
-    const unsigned long long am0 = __ballot(acc0), am1 = __ballot(acc1);
-    if (acc0) sq[(tail + lanes_below(am0)) & 255] = make_uint4(ux, uy, uz, (uint32_t)lane);
-    tail += __popcll(am0);
-    if (acc1) sq[(tail + lanes_below(am1)) & 255] = make_uint4(vx, vy, vz, (uint32_t)lane);
-    tail += __popcll(am1);
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const unsigned long long am = __ballot(acc[t]);
+      if (acc[t]) sq[(tail + lanes_below(am)) & 255] = make_uint4(u[t][0], u[t][1], u[t][2], (uint32_t)lane);
+      tail += __popcll(am);
+    }
 #if RT_SQ_TAIL > 0
     // The last few owners still drawing finish cooperatively, one at a
     // time: lane h evaluates try h of the owner's stream (jump table), as
     // in soft_coop; the first `need` accepted tries are its points, queued
     // in try order, and the stream advances past the last one taken.  The
     // wave no longer loops on its unluckiest owners' tries one by one.
-    // (tail - head < 64 here, plus at most 16 points per owner: the ring holds them.)
+    // (at most 16 points per owner: the ring holds them, see the static_assert above)
     const unsigned long long rem = __ballot(need > 0);
     if (rem != 0 && __popcll(rem) <= RT_SQ_TAIL) {
       for (unsigned long long b = rem; b; b &= b - 1) {
@@ -421,7 +427,7 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
       const d3 Po = mk(__shfl(P.x, ow), __shfl(P.y, ow), __shfl(P.z, ow));
       const d3 Lo = mk(__shfl(ldir.x, ow), __shfl(ldir.y, ow), __shfl(ldir.z, ow));
       const double dist = __shfl(ldist, ow);
-      const Cand co{__shfl(cm.s, ow), __shfl(cm.t, ow)};
+      const Cand co{__shfl(cm.s, ow), p.nt ? __shfl(cm.t, ow) : 0ull};  // (no triangles: cm.t is 0)
       if (lane < n) {
         const d3 pt = mk(rt_bits_to_unit(e.x) * 2 - 1, rt_bits_to_unit(e.y) * 2 - 1, rt_bits_to_unit(e.z) * 2 - 1);
         if (!shadow_blocked<kCount>(p, masks, Po, normalize(Lo + muls(pt, 0.1)), dist, co, stack, c))
