@@ -328,7 +328,13 @@ template <bool kCount>
 __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_soft, bool trace, d3 P, d3 ldir,
                                           double ldist, Cand cm, rt_rng& rng, const uint64_t* jump, int* stack,
                                           Counters& c) {
-  __shared__ uint4 sq[256];  // queued points: raw draws x, y, z, owner lane (a ring)
+  // queued points: raw draws x, y, z, owner lane (a ring).  It holds what
+  // a pass can leave: < 64 points not yet traced, 64 per try of the pass and
+  // 16 per owner of the cooperative tail (256 or more entries; a power of 2
+  // up to 256, so the index is a mask there)
+  constexpr int kRingNeed = 64 * RT_SQ_TRIES + 64 + 16 * RT_SQ_TAIL;
+  constexpr unsigned kRing = kRingNeed <= 256 ? 256u : (unsigned)kRingNeed;
+  __shared__ uint4 sq[kRing];
   __shared__ int sq_unocc[64];  // per owner: unoccluded rays
   const int lane = (int)(threadIdx.x & 63);
   sq_unocc[lane] = 0;
@@ -340,7 +346,6 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
     // before it (so the stream advances by exactly the draws the sequential
     // loop takes).
     constexpr int K = RT_SQ_TRIES;
-    static_assert(64 * K + 63 + 16 * RT_SQ_TAIL <= 256, "soft_queue ring too small");
     bool acc[K];
     uint32_t u[K][3];
 #pragma unroll
@@ -370,7 +375,7 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
 #pragma unroll
     for (int t = 0; t < K; ++t) {
       const unsigned long long am = __ballot(acc[t]);
-      if (acc[t]) sq[(tail + lanes_below(am)) & 255] = make_uint4(u[t][0], u[t][1], u[t][2], (uint32_t)lane);
+      if (acc[t]) sq[(unsigned)(tail + lanes_below(am)) % kRing] = make_uint4(u[t][0], u[t][1], u[t][2], (uint32_t)lane);
       tail += __popcll(am);
     }
 #if RT_SQ_TAIL > 0
@@ -379,7 +384,7 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
     // in soft_coop; the first `need` accepted tries are its points, queued
     // in try order, and the stream advances past the last one taken.  The
     // wave no longer loops on its unluckiest owners' tries one by one.
-    // (at most 16 points per owner: the ring holds them, see the static_assert above)
+    // (at most 16 points per owner: the ring holds them, see kRing)
     const unsigned long long rem = __ballot(need > 0);
     if (rem != 0 && __popcll(rem) <= RT_SQ_TAIL) {
       for (unsigned long long b = rem; b; b &= b - 1) {
@@ -399,7 +404,7 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
           const int nch = __popcll(chm);
           const int used = nch == nd ? 64 - __clzll(chm) : 64;
           if (tr) {
-            if (chosen) sq[(tail + lanes_below(chm)) & 255] = make_uint4(o0, o1, o2, (uint32_t)ow);
+            if (chosen) sq[(unsigned)(tail + lanes_below(chm)) % kRing] = make_uint4(o0, o1, o2, (uint32_t)ow);
             tail += nch;
           }
           got += nch;
@@ -421,7 +426,7 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
     while (tail - head >= 64 || (!more && tail > head)) {
       __syncthreads();
       const int n = min(64, tail - head);
-      const uint4 e = sq[(head + lane) & 255];
+      const uint4 e = sq[(unsigned)(head + lane) % kRing];
       const int ow = lane < n ? (int)e.w : lane;
       // the owner's ray inputs, read across lanes (every lane takes part)
       const d3 Po = mk(__shfl(P.x, ow), __shfl(P.y, ow), __shfl(P.z, ow));
