@@ -135,7 +135,9 @@ def parse():
                     help="TEST MODE (not a bench line): gather the shares over gloo host copies instead of RCCL, "
                          "so N ranks can share one GPU (RCCL refuses two ranks on one device); --check compares "
                          "rank 0's last image with a 1-rank render")
-    ap.add_argument("--check", action="store_true", help="compare the last frame with a 1-rank render (N > 1)")
+    ap.add_argument("--check", action="store_true", help="(default at N > 1; kept for old command lines)")
+    ap.add_argument("--no-check", action="store_true",
+                    help="N > 1: skip the post-run check of the last frame against a 1-rank render")
     return ap.parse_args()
 
 
@@ -632,21 +634,35 @@ def main():
     elapsed1, kms1 = (time_steps(slots[:1], torch, dist, world, sts, args.warmup, comm, gstream, 1)
                       if F * B > 1 else (elapsed, kms))
     first_ms = first_frame_ms(rtgo, torch, scene, W, H, sts[0], local) if world == 1 else None
-    check = None
-    if args.check and world > 1:
-        # the last timed frame (rank 0; slot 0 rendered it last, one frame at
-        # a time) against a 1-rank render of the same settings
+    check = share_sums = gathered_ok = None
+    if world > 1 and not args.no_check:
+        # After the timed region, always at N > 1: the last timed frame (slot 0
+        # rendered it last, one frame per launch) proves its own image.  Every
+        # rank hashes its packed share; rank 0 hashes each rank's slot of the
+        # gather buffer the RCCL group filled (the transport check), then
+        # compares its unpacked image with a 1-rank render of the same settings
+        # on its own device (createRenderTasks' frame, renderer.go:398-436).
         torch.cuda.synchronize()
+        sl = slots[0]
+        nb = sl.share_bytes
+
+        def sha(t):
+            return hashlib.sha256(t.cpu().numpy().tobytes()).hexdigest()[:16]
+
+        share_sums = [None] * world
+        dist.all_gather_object(share_sums, sha(sl.share[:nb]))
         if rank == 0:
-            lin, rgba = slots[0].image(0)
+            got = [sha(sl.gbuf[r * sl.n * nb:r * sl.n * nb + nb]) for r in range(world)]
+            gathered_ok = got == share_sums
+            lin, rgba = sl.image(0)
             ref = Slot(rtgo, torch, scene, W, H, 0, 1, local, None, 1)
             ref.render([sts[-1]])
             torch.cuda.synchronize()
-            check = bool(torch.equal(lin, ref.lin[0]) and torch.equal(rgba, ref.rgba[0]))
+            check = bool(gathered_ok and torch.equal(lin, ref.lin[0]) and torch.equal(rgba, ref.rgba[0]))
             ref.close()
         ok = [None] * world
-        dist.all_gather_object(ok, check)
-        check = ok[0]
+        dist.all_gather_object(ok, (check, gathered_ok))
+        check, gathered_ok = ok[0]
     e2e = None
     if world == 1 and not args.no_e2e and cfg in ("c2", "c2_committed", "c3"):
         e2e = render_e2e(rtgo, scene, W, H, args, local)
@@ -772,6 +788,8 @@ def main():
             },
             "rank_kernel_ms": [round(x, 4) for x in rank_kernel_ms],
             "check_equals_one_rank": check,
+            "check_gathered_equals_rank_shares": gathered_ok,
+            "rank_share_sha256_16": share_sums,
             # (a strided partition carries no estimate: null)
             "rank_estimated_work": ([round(part.work(r)) for r in range(world)]
                                     if world > 1 and part_kind and part_kind.startswith("balanced") else None),

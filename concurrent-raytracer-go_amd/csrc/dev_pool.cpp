@@ -26,7 +26,12 @@ namespace rtgo {
 namespace {
 
 constexpr size_t kGrain = 256 * 1024;              // sizes are rounded up to this
-constexpr size_t kCacheCap = size_t(32) << 30;     // cached bytes per device at most (HBM: 288 GB)
+// cached bytes per device at most.  The cache is invisible to the process's
+// other allocators (PyTorch's caching allocator, RCCL), so it holds only what
+// a one-shot render of a linear-scan scene re-allocates every call (a few MB
+// to a few hundred MB); a BVH scene's wavefront arrays (GBs) go back to
+// hipFree.  Mixed-allocator callers can empty it with rt_release_cached_memory.
+constexpr size_t kCacheCap = size_t(4) << 30;
 
 struct Pool {
   std::multimap<size_t, void*> free_blocks;  // size -> block

@@ -144,6 +144,16 @@ int main(int argc, char** argv) {
     printf("Error loading scene: %s\n", rt_last_error());
     return 1;
   }
+  if (w <= 0 || h <= 0) {
+    // image.NewRGBA of an empty rectangle renders nothing; png.Encode then
+    // fails on a zero-sized image.  Decided before any device state exists,
+    // so a machine without a GPU gives the same answer (exit 1).
+    printf("Rendering at %lldx%lld resolution...\n", w, h);
+    rt_scene_print_hittables(sb);
+    printf("Error saving image: invalid image size %lldx%lld\n", w, h);
+    rt_scene_free(sb);
+    return 1;
+  }
   // renderer := renderer.NewParallelRenderer(numWorkers) (main.go:46-47):
   // the device state (HIP runtime, context, stream, the kernels' code
   // objects) is the GPU renderer's constructor work, made before Render and
@@ -160,14 +170,6 @@ int main(int argc, char** argv) {
   fflush(stdout);
   rt_scene_print_hittables(sb);
   const rt_scene* scene = rt_scene_view(sb);
-  if (w <= 0 || h <= 0) {
-    // image.NewRGBA of an empty rectangle renders nothing; png.Encode then
-    // fails on a zero-sized image
-    printf("Error saving image: invalid image size %lldx%lld\n", w, h);
-    rt_renderer_destroy(rr);
-    rt_scene_free(sb);
-    return 1;
-  }
   const size_t npix = (size_t)w * (size_t)h;
   std::vector<uint8_t> rgba(npix * 4);
   rt_stats stats;

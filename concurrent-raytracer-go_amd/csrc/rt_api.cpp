@@ -257,6 +257,26 @@ int rt_context_set_tuning(rt_context* c, const rt_tuning* t) {
 
 int32_t rt_abi_version(void) { return RT_ABI_VERSION; }
 
+int rt_debug_xlane_faults(int32_t device, int32_t reset, uint64_t* out) {
+  if (!out) {
+    set_error("out is NULL");
+    return RT_E_INVALID;
+  }
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipDeviceSynchronize());
+  const long long a = xlane_faults_kernel(reset != 0), b = xlane_faults_wavefront(reset != 0);
+  if (a == -1 || b == -1) {
+    set_error("not a cross-lane checking build (make xlane)");
+    return RT_E_INVALID;
+  }
+  if (a < 0 || b < 0) {
+    set_error("reading the cross-lane fault counters failed");
+    return RT_E_DEVICE;
+  }
+  *out = (uint64_t)(a + b);
+  return RT_OK;
+}
+
 int rt_validate(const rt_scene* scene, int32_t w, int32_t h, const rt_settings* st) {
   int rc = validate_scene(scene);
   if (rc) return rc;
@@ -457,10 +477,17 @@ static size_t split_flags_bytes(int nsplit, int spp) {
   return (size_t)nsplit * ((spp + 31) / 32) * sizeof(uint32_t) + (size_t)nsplit * sizeof(int32_t);
 }
 
-// device buffer *ptr of *cap bytes, grown to at least n bytes
-static int grow(void* ptr, size_t* cap, size_t n) {
+// device buffer *ptr of *cap bytes, grown to at least n bytes.  dev_free
+// hands the old block straight to the device cache (no implicit device sync,
+// unlike hipFree), where another context may take it at once: the context's
+// last render, which may still use it, is waited for first.
+static int grow(rt_context* c, void* ptr, size_t* cap, size_t n) {
   void** p = (void**)ptr;
   if (n <= *cap) return RT_OK;
+  if (*p) {
+    int rc = quiesce(c);
+    if (rc) return rc;
+  }
   dev_free(*p);
   *p = nullptr;
   *cap = 0;
@@ -642,7 +669,7 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
       tile_cost(f, w, h, tiles, &cost);
       const size_t scratch = sched_scratch_bytes(local);
       const size_t inputs = c->masks_host.size() * sizeof(unsigned long long) + cost.size() * sizeof(float);
-      rc = grow(&c->d_sched, &c->sched_cap, scratch + inputs + 256);
+      rc = grow(c, &c->d_sched, &c->sched_cap, scratch + inputs + 256);
       if (rc) return rc;
       char* in = (char*)c->d_sched + ((scratch + 255) & ~size_t(255));
       c->d_masks = masks ? (unsigned long long*)in : nullptr;
@@ -664,7 +691,7 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
         sp.work_sum = sp.work_max + (size_t)local * 1024;
         sp.work_n = st->samples;
       } else if (pilot && st->samples > 0 && st->max_depth > 0) {
-        rc = grow(&c->d_pilot, &c->pilot_cap, (size_t)local * 1024 * 24 + 256);
+        rc = grow(c, &c->d_pilot, &c->pilot_cap, (size_t)local * 1024 * 24 + 256);
         if (rc) return rc;
         rc = run_pilot(c, *p, &sp, c->d_pilot, s);
         if (rc) return rc;
@@ -677,7 +704,7 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
       HIP_TRY(hipMemcpyAsync(c->h_totals, sp.totals, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
       const int nblocks = c->h_totals[0], nsplit = c->h_totals[1];
-      rc = grow(&c->d_blocks, &c->d_blocks_cap, (size_t)std::max(nblocks, 1) * kBlockInts * sizeof(int32_t));
+      rc = grow(c, &c->d_blocks, &c->d_blocks_cap, (size_t)std::max(nblocks, 1) * kBlockInts * sizeof(int32_t));
       if (rc) return rc;
       sp.blocks = c->d_blocks;
       e = sched_launch_blocks(sp, true, s);
@@ -704,7 +731,7 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
   if (c->nsplit && c->split_frames < frames) {
     int rc = quiesce(c);  // earlier launches may still use the rows
     if (rc) return rc;
-    rc = grow(&c->d_split, &c->split_cap, (rows + flags) * (size_t)frames + 256);
+    rc = grow(c, &c->d_split, &c->split_cap, (rows + flags) * (size_t)frames + 256);
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync((char*)c->d_split + rows * (size_t)frames, 0, flags * (size_t)frames, s));
     c->split_frames = frames;
@@ -970,7 +997,7 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
   const int npass = wf ? 1 : std::max(1, (spp + kMaxBlockSamples - 1) / kMaxBlockSamples);
   p.spp_total = spp;
   if (npass > 1) {
-    rc = grow(&c->d_acc, &c->acc_cap, (size_t)local_tiles(c, w, h, rank, world) * 1024 * 3 * sizeof(double));
+    rc = grow(c, &c->d_acc, &c->acc_cap, (size_t)local_tiles(c, w, h, rank, world) * 1024 * 3 * sizeof(double));
     if (rc) return rc;
     p.acc = (double*)c->d_acc;
   }
@@ -993,7 +1020,7 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
     // blocks are cut from them (prepare_schedule)
     if (!wf && npass == 1 && c->meas_state == 1 && !counts && st->sky == RT_SKY_NONE && p.num_blocks > 0) {
       const size_t npx = (size_t)local_tiles(c, w, h, rank, world) * 1024;
-      rc = grow(&c->d_meas, &c->meas_cap, npx * 8);
+      rc = grow(c, &c->d_meas, &c->meas_cap, npx * 8);
       if (rc) return rc;
       p.work_max = (unsigned int*)c->d_meas;
       p.work_sum = p.work_max + npx;
@@ -1056,7 +1083,7 @@ int rt_context_set_partition(rt_context* c, const rt_partition* p) {
     return RT_OK;
   }
   auto d = std::make_shared<const PartitionData>(partition_data(p));
-  rc = grow(&c->d_part, &c->d_part_cap, std::max<size_t>(d->lists.size(), 1) * sizeof(int32_t));
+  rc = grow(c, &c->d_part, &c->d_part_cap, std::max<size_t>(d->lists.size(), 1) * sizeof(int32_t));
   if (rc) return rc;
   if (!d->lists.empty())
     HIP_TRY(hipMemcpy(c->d_part, d->lists.data(), d->lists.size() * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -1210,16 +1237,17 @@ int rt_context_render_frames_async(rt_context* c, int32_t w, int32_t h, const rt
   // one frame at a time where a launch cannot hold several: the wavefront
   // path (host-driven bounce loop), sample passes, a measuring frame
   const int npass = std::max(1, (st->samples + kMaxBlockSamples - 1) / kMaxBlockSamples);
-  if (nframes == 1 || use_wavefront(c) || npass > 1 || (c->tun.measure && c->meas_state != 3)) {
+  auto one_by_one = [&]() {
     for (int f = 0; f < nframes; ++f) {
       rt_settings sf = *st;
       sf.seed = seeds[f];
-      rc = rt_context_render_async(c, w, h, &sf, rank, world, layout, d_linear[f], d_rgba ? d_rgba[f] : nullptr,
-                                   stream, nullptr);
-      if (rc) return rc;
+      int r = rt_context_render_async(c, w, h, &sf, rank, world, layout, d_linear[f], d_rgba ? d_rgba[f] : nullptr,
+                                      stream, nullptr);
+      if (r) return r;
     }
-    return RT_OK;
-  }
+    return (int)RT_OK;
+  };
+  if (nframes == 1 || use_wavefront(c) || npass > 1 || (c->tun.measure && c->meas_state != 3)) return one_by_one();
   HIP_TRY(hipSetDevice(c->device));
   KParams p;
   base_params(c, w, h, st, rank, world, layout, &p);
@@ -1227,6 +1255,9 @@ int rt_context_render_frames_async(rt_context* c, int32_t w, int32_t h, const rt
   if (c->have_timing && s != c->last_stream) HIP_TRY(hipStreamWaitEvent(s, c->ev1, 0));
   rc = prepare_schedule(c, &p, st, s, nframes);
   if (rc) return rc;
+  // a new schedule key whose first frame is to measure (rt_tuning.measure):
+  // that frame goes through the single-frame path, which records the paths
+  if (c->tun.measure && c->meas_state == 1) return one_by_one();
   p.spp_total = st->samples;
   p.nframes = nframes;
   for (int f = 0; f < nframes; ++f) {

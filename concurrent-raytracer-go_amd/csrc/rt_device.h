@@ -11,6 +11,29 @@
 #include "../../include/rt_rng.h"
 #include "rt_internal.h"
 
+// Cross-lane reads belong in CONVERGED code.  __shfl (ds_bpermute) from a
+// lane that is inactive at the read returns no data, so an owner's state
+// read inside an owner-only branch silently becomes 0: a rejected r03
+// soft-shadow variant hung that way (a stream restarted from state 0 every
+// round and never accepted a point).  The checking build
+// (`make xlane`, -DRT_CHECK_XLANE) routes every __shfl of the kernels through
+// rt_checked_shfl, which counts reads whose source lane is inactive; the GPU
+// test suite renders with it and requires zero (tests/test_gpu_xlane.py).
+#ifdef RT_CHECK_XLANE
+namespace rtgo {
+__device__ unsigned long long g_xlane_faults;  // (one per translation unit: see xlane_faults_*)
+}
+template <typename T>
+__device__ __forceinline__ T rt_checked_shfl(T v, int src, int width = 64) {
+  const unsigned long long ex = __builtin_amdgcn_read_exec();
+  const int lane = (int)(threadIdx.x & 63);
+  const int from = (lane & ~(width - 1)) + (src & (width - 1));
+  if (!((ex >> (from & 63)) & 1ull)) atomicAdd(&rtgo::g_xlane_faults, 1ull);
+  return __shfl(v, src, width);
+}
+#define __shfl(...) rt_checked_shfl(__VA_ARGS__)
+#endif
+
 namespace rtgo {
 
 // ------------------------------------------------------------ Vec3 (vector.go)

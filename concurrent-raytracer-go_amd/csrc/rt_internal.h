@@ -292,6 +292,9 @@ int preload_render_kernels();
 int warm_device(void* stream, void* dev4k);
 int preload_sched_kernels();
 int preload_wf_kernels();
+// RT_CHECK_XLANE builds: inactive-lane __shfl reads per file (-1: not such a build)
+long long xlane_faults_kernel(bool reset);
+long long xlane_faults_wavefront(bool reset);
 int wf_lds_nodes(int stack_depth, int nodes, int block, int wgs_per_cu);
 int wf_launch_resolve(const WfParams& p, int npix, void* stream);
 

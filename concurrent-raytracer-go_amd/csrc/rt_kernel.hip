@@ -48,19 +48,13 @@
 #endif
 // cooperative soft shadows when at most this many lanes need them (measured
 // best of 0/2/4/8 in round 1; 4 and 16 within noise in round 2)
-#ifndef RT_COOP_MAX
-#define RT_COOP_MAX 8
-#endif
-constexpr int kCoopMax = RT_COOP_MAX;
+constexpr int kCoopMax = 8;
 // soft_queue: the owners still drawing finish cooperatively once at most
-// this many are left (0: never)
-#ifndef RT_SQ_TAIL
-#define RT_SQ_TAIL 2
-#endif
-// soft_queue: rejection tries per pass of its loop
-#ifndef RT_SQ_TRIES
-#define RT_SQ_TRIES 2
-#endif
+// this many are left (measured best of 0/1/2/4, r03)
+constexpr int kSqTail = 2;
+// soft_queue: rejection tries per pass of its loop (measured best of 1..6
+// within the LDS budget, r03)
+constexpr int kSqTries = 2;
 
 namespace rtgo {
 
@@ -101,24 +95,32 @@ __device__ __forceinline__ bool in_cone(const double* cc, double r, d3 P, d3 ldi
   return inside || (!beyond && meets);
 }
 
-// `self` is the hittable that was hit.  When the hit is on its outside
-// (front face) and every cone direction leaves the surface by a clear angle
-// (N.ldir >= 0.1015 > sin(alpha)), a convex hittable (sphere of positive
-// radius, or createCube's box) cannot be hit again at t >= 0.001.
+// `self` is the hittable that was hit.  When the hit is on its OUTSIDE and
+// every cone direction leaves the surface by a clear angle (N.ldir >= 0.1015
+// > sin(alpha), N the normal facing the ray's side), a convex hittable
+// (sphere of positive radius, or createCube's box) cannot be hit again at
+// t >= 0.001.  A hit from inside is never left out: the shadow ray has to
+// cross the object.  "Outside" per kind:
+//   sphere: FrontFace (sphere.go:42-48 takes the true outward normal);
+//   cube:   FrontFace != "its normals point in" (DBox.front_out): createCube
+//           winds them inward, so FrontFace there means a hit from inside.
+__device__ __forceinline__ bool box_self_out(const DBox& B, bool front) { return (int)front == B.front_out; }
+
 __device__ __forceinline__ Cand cone_candidates(const Geo& p, d3 P, d3 N, bool front, int self, d3 ldir,
                                                 double ldist) {
-  const bool self_out = front && dot(N, ldir) >= KC(0.1015);
+  const bool leaves = dot(N, ldir) >= KC(0.1015);
+  const bool sphere_out = front && leaves;
   Cand m{0ull, 0ull};
   for (int i = 0; i < p.ns; ++i) {
     const DSphere& S = p.spheres[i];
-    if (self_out && S.obj == self && S.r > 0) continue;
+    if (sphere_out && S.obj == self && S.r > 0) continue;
     if (in_cone(S.c, S.r, P, ldir, ldist)) m.s |= 1ull << i;
   }
   // triangles by cube: one cone test against the bounding sphere of the
   // cube's box admits its 12 triangles (their exact tests follow per ray)
   for (int j = 0; j < p.nb; ++j) {
     const DBox& B = p.boxes[j];
-    if (self_out && B.obj == self) continue;
+    if (leaves && B.obj == self && box_self_out(B, front)) continue;
     if (in_cone(B.bc, B.br, P, ldir, ldist)) m.t |= 0xFFFull << B.first;
   }
   return m;
@@ -332,7 +334,7 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
   // a pass can leave: < 64 points not yet traced, 64 per try of the pass and
   // 16 per owner of the cooperative tail (256 or more entries; a power of 2
   // up to 256, so the index is a mask there)
-  constexpr int kRingNeed = 64 * RT_SQ_TRIES + 64 + 16 * RT_SQ_TAIL;
+  constexpr int kRingNeed = 64 * kSqTries + 64 + 16 * kSqTail;
   constexpr unsigned kRing = kRingNeed <= 256 ? 256u : (unsigned)kRingNeed;
   __shared__ uint4 sq[kRing];
   __shared__ int sq_unocc[64];  // per owner: unoccluded rays
@@ -341,11 +343,11 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
   int need = need_soft ? 16 : 0, free_rays = 0;  // free_rays: points of an owner with nothing to trace
   int head = 0, tail = 0;  // wave-uniform ring positions
   for (;;) {
-    // RT_SQ_TRIES tries per pass: the later tries are drawn ahead and each
+    // kSqTries tries per pass: the later tries are drawn ahead and each
     // is consumed only when the owner still needs a point after the ones
     // before it (so the stream advances by exactly the draws the sequential
     // loop takes).
-    constexpr int K = RT_SQ_TRIES;
+    constexpr int K = kSqTries;
     bool acc[K];
     uint32_t u[K][3];
 #pragma unroll
@@ -378,50 +380,50 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
       if (acc[t]) sq[(unsigned)(tail + lanes_below(am)) % kRing] = make_uint4(u[t][0], u[t][1], u[t][2], (uint32_t)lane);
       tail += __popcll(am);
     }
-#if RT_SQ_TAIL > 0
-    // The last few owners still drawing finish cooperatively, one at a
-    // time: lane h evaluates try h of the owner's stream (jump table), as
-    // in soft_coop; the first `need` accepted tries are its points, queued
-    // in try order, and the stream advances past the last one taken.  The
-    // wave no longer loops on its unluckiest owners' tries one by one.
-    // (at most 16 points per owner: the ring holds them, see kRing)
-    const unsigned long long rem = __ballot(need > 0);
-    if (rem != 0 && __popcll(rem) <= RT_SQ_TAIL) {
-      for (unsigned long long b = rem; b; b &= b - 1) {
-        const int ow = __builtin_ctzll(b);
-        int nd = __builtin_amdgcn_readlane(need, ow);
-        const bool tr = __builtin_amdgcn_readlane(trace ? 1 : 0, ow) != 0;
-        uint64_t x = rl64(rng.x, ow);
-        int got = 0, tries = 0;
-        while (nd > 0) {
-          const uint64_t x0 = state_at3(x, jump, lane), x1 = x0 * RT_PCG_MULT + RT_PCG_INC,
-                         x2 = x1 * RT_PCG_MULT + RT_PCG_INC;
-          const uint32_t o0 = rt_pcg_out(x0), o1 = rt_pcg_out(x1), o2 = rt_pcg_out(x2);
-          const bool acc = unit_ball_accept(o0, o1, o2);
-          const unsigned long long am = __ballot(acc);
-          const bool chosen = acc && lanes_below(am) < nd;
-          const unsigned long long chm = __ballot(chosen);
-          const int nch = __popcll(chm);
-          const int used = nch == nd ? 64 - __clzll(chm) : 64;
-          if (tr) {
-            if (chosen) sq[(unsigned)(tail + lanes_below(chm)) % kRing] = make_uint4(o0, o1, o2, (uint32_t)ow);
-            tail += nch;
+    if constexpr (kSqTail > 0) {
+      // The last few owners still drawing finish cooperatively, one at a
+      // time: lane h evaluates try h of the owner's stream (jump table), as
+      // in soft_coop; the first `need` accepted tries are its points, queued
+      // in try order, and the stream advances past the last one taken.  The
+      // wave no longer loops on its unluckiest owners' tries one by one.
+      // (at most 16 points per owner: the ring holds them, see kRing)
+      const unsigned long long rem = __ballot(need > 0);
+      if (rem != 0 && __popcll(rem) <= kSqTail) {
+        for (unsigned long long b = rem; b; b &= b - 1) {
+          const int ow = __builtin_ctzll(b);
+          int nd = __builtin_amdgcn_readlane(need, ow);
+          const bool tr = __builtin_amdgcn_readlane(trace ? 1 : 0, ow) != 0;
+          uint64_t x = rl64(rng.x, ow);
+          int got = 0, tries = 0;
+          while (nd > 0) {
+            const uint64_t x0 = state_at3(x, jump, lane), x1 = x0 * RT_PCG_MULT + RT_PCG_INC,
+                           x2 = x1 * RT_PCG_MULT + RT_PCG_INC;
+            const uint32_t o0 = rt_pcg_out(x0), o1 = rt_pcg_out(x1), o2 = rt_pcg_out(x2);
+            const bool acc = unit_ball_accept(o0, o1, o2);
+            const unsigned long long am = __ballot(acc);
+            const bool chosen = acc && lanes_below(am) < nd;
+            const unsigned long long chm = __ballot(chosen);
+            const int nch = __popcll(chm);
+            const int used = nch == nd ? 64 - __clzll(chm) : 64;
+            if (tr) {
+              if (chosen) sq[(unsigned)(tail + lanes_below(chm)) % kRing] = make_uint4(o0, o1, o2, (uint32_t)ow);
+              tail += nch;
+            }
+            got += nch;
+            nd -= nch;
+            tries += used;
+            x = state_at3(x, jump, used);
           }
-          got += nch;
-          nd -= nch;
-          tries += used;
-          x = state_at3(x, jump, used);
-        }
-        if (lane == ow) {
-          rng.x = x;
-          need = 0;
-          if (!tr) free_rays += got;
-          cnt<kCount>(c, C_RNG, 3ull * tries);
-          cnt<kCount>(c, C_SHADOW, got);
+          if (lane == ow) {
+            rng.x = x;
+            need = 0;
+            if (!tr) free_rays += got;
+            cnt<kCount>(c, C_RNG, 3ull * tries);
+            cnt<kCount>(c, C_SHADOW, got);
+          }
         }
       }
     }
-#endif
     const bool more = __ballot(need > 0) != 0;
     while (tail - head >= 64 || (!more && tail > head)) {
       __syncthreads();
@@ -964,15 +966,15 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
       const d3 ldir = ldist == 0 ? mk(0, 0, 0) : divs(lv, ldist);
       if (ldist < 0.001) continue;  // renderer.go:252-254
       // the shadow cone's candidates, one primitive per lane (cone_candidates)
-      const bool self_out = front && dot(N, ldir) >= KC(0.1015);
+      const bool leaves = dot(N, ldir) >= KC(0.1015);
       bool cs = false, cb = false;
       if (lane < g.ns) {
         const DSphere& S = g.spheres[lane];
-        cs = !(self_out && S.obj == self && S.r > 0) && in_cone(S.c, S.r, P, ldir, ldist);
+        cs = !(front && leaves && S.obj == self && S.r > 0) && in_cone(S.c, S.r, P, ldir, ldist);
       }
       if (lane < g.nb) {  // (nb <= 5: 12 triangles per cube)
         const DBox& B = g.boxes[lane];
-        cb = !(self_out && B.obj == self) && in_cone(B.bc, B.br, P, ldir, ldist);
+        cb = !(leaves && B.obj == self && box_self_out(B, front)) && in_cone(B.bc, B.br, P, ldir, ldist);
       }
       Cand cm{__ballot(cs), 0ull};
       for (unsigned long long b = __ballot(cb); b; b &= b - 1) cm.t |= 0xFFFull << g.boxes[__builtin_ctzll(b)].first;
@@ -1869,6 +1871,24 @@ int launch_unpack_map(int32_t W, int32_t H, int32_t nframes, const int32_t* slot
                      nframes, reinterpret_cast<const int2*>(slot), (const uint8_t*)gathered, share_bytes, rgba_off, ol,
                      orgba);
   return (int)hipGetLastError();
+}
+
+
+// Cross-lane reads from inactive lanes counted by this file's kernels in an
+// RT_CHECK_XLANE build (rt_device.h); -1 in a normal build.  reset: zero it.
+long long xlane_faults_kernel(bool reset) {
+#ifdef RT_CHECK_XLANE
+  unsigned long long v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_xlane_faults), sizeof v) != hipSuccess) return -2;
+  if (reset) {
+    const unsigned long long z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_xlane_faults), &z, sizeof z) != hipSuccess) return -2;
+  }
+  return (long long)v;
+#else
+  (void)reset;
+  return -1;
+#endif
 }
 
 }  // namespace rtgo

@@ -47,6 +47,17 @@ using namespace rtgo;
     }                                                                                   \
   } while (0)
 
+// Inside ncclGroupStart / ncclGroupEnd: the first failing call is recorded
+// and the rest are skipped, but the group is always closed, so a failure
+// leaves the communicator usable (NCCL_TRY would return with the group open).
+#define NCCL_GROUP_TRY(err, expr)                                                       \
+  do {                                                                                  \
+    if ((err) == ncclSuccess) {                                                         \
+      (err) = (expr);                                                                   \
+      if ((err) != ncclSuccess) set_error(std::string(#expr) + " failed: " + ncclGetErrorString(err)); \
+    }                                                                                   \
+  } while (0)
+
 namespace {
 
 struct Rank {
@@ -184,14 +195,17 @@ int group_gather(rt_renderer* r, size_t share_bytes) {
     HIP_TRY(hipStreamWaitEvent(r->comm_streams[q.comm_idx], q.done, 0));
   }
   NCCL_TRY(ncclGroupStart());
+  ncclResult_t ge = ncclSuccess;
   for (int k = 1; k < n; ++k) {
     Rank& q = r->ranks[k];
     if (q.comm_idx == 0) continue;
-    NCCL_TRY(ncclSend(q.share, share_bytes, ncclUint8, 0, r->comms[q.comm_idx], r->comm_streams[q.comm_idx]));
-    NCCL_TRY(ncclRecv((uint8_t*)r->gathered.p + (size_t)k * share_bytes, share_bytes, ncclUint8, q.comm_idx,
-                      r->comms[0], root_s));
+    NCCL_GROUP_TRY(ge, ncclSend(q.share, share_bytes, ncclUint8, 0, r->comms[q.comm_idx], r->comm_streams[q.comm_idx]));
+    NCCL_GROUP_TRY(ge, ncclRecv((uint8_t*)r->gathered.p + (size_t)k * share_bytes, share_bytes, ncclUint8,
+                                q.comm_idx, r->comms[0], root_s));
   }
-  NCCL_TRY(ncclGroupEnd());
+  const ncclResult_t ee = ncclGroupEnd();
+  if (ge != ncclSuccess) return RT_E_DEVICE;
+  NCCL_TRY(ee);
   return RT_OK;
 }
 
@@ -615,9 +629,14 @@ int rt_unpack_partition_async(const rt_partition* p, const void* d_gathered, flo
   return rt_unpack_partition_frames_async(p, 1, d_gathered, d_linear, d_rgba, stream);
 }
 
-int rt_renderer_rank_seconds(const rt_renderer* r, double* out) {
+int rt_renderer_rank_seconds(const rt_renderer* r, double* out, int32_t capacity) {
   if (!r || !out) {
     set_error("renderer or out is NULL");
+    return RT_E_INVALID;
+  }
+  if (capacity < (int64_t)r->ranks.size()) {
+    set_error("rt_renderer_rank_seconds: out holds " + std::to_string(capacity) + " values, the renderer has " +
+              std::to_string(r->ranks.size()) + " ranks");
     return RT_E_INVALID;
   }
   if (r->rank_secs.size() != r->ranks.size()) {
@@ -627,6 +646,8 @@ int rt_renderer_rank_seconds(const rt_renderer* r, double* out) {
   for (size_t k = 0; k < r->rank_secs.size(); ++k) out[k] = r->rank_secs[k];
   return RT_OK;
 }
+
+int32_t rt_renderer_num_ranks(const rt_renderer* r) { return r ? (int32_t)r->ranks.size() : 0; }
 
 // ------------------------------------------------------------ multi-process
 
@@ -680,13 +701,16 @@ int rt_comm_gather_bytes_async(rt_comm* c, size_t share, const void* d_share, vo
   hipStream_t s = (hipStream_t)stream;
   HIP_TRY(hipSetDevice(c->device));
   NCCL_TRY(ncclGroupStart());
+  ncclResult_t ge = ncclSuccess;
   if (c->rank == 0) {
     for (int k = 1; k < c->world; ++k)
-      NCCL_TRY(ncclRecv((uint8_t*)d_gathered + (size_t)k * share, share, ncclUint8, k, c->comm, s));
+      NCCL_GROUP_TRY(ge, ncclRecv((uint8_t*)d_gathered + (size_t)k * share, share, ncclUint8, k, c->comm, s));
   } else {
-    NCCL_TRY(ncclSend(d_share, share, ncclUint8, 0, c->comm, s));
+    NCCL_GROUP_TRY(ge, ncclSend(d_share, share, ncclUint8, 0, c->comm, s));
   }
-  NCCL_TRY(ncclGroupEnd());
+  const ncclResult_t ee = ncclGroupEnd();
+  if (ge != ncclSuccess) return RT_E_DEVICE;
+  NCCL_TRY(ee);
   return RT_OK;
 }
 

@@ -48,7 +48,13 @@ struct alignas(16) DBox {  // 96 B
   int32_t first;  // first triangle (12 consecutive)
   int32_t count;
   int32_t obj;
-  int32_t pad;
+  // What FrontFace (triangle.go:70-73) means on this cube's triangles.
+  // createCube's face table winds every normal INTO the box when
+  // size.x*size.y*size.z > 0, so a front-face hit comes from inside (0); an
+  // odd number of negative size components mirrors the box and its normals
+  // point out (1: front = outside); a zero or non-finite product: unknown
+  // (-1, the hit cube is never left out of its own shadow rays).
+  int32_t front_out;
 };
 
 // Material kinds: RT_MAT_* of rt_api.h.

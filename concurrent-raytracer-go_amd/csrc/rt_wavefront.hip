@@ -69,12 +69,6 @@ constexpr int kLdsBytes = 160 * 1024;    // LDS per CU (MI355X), all of it avail
 #ifndef RT_WF_REFILL
 #define RT_WF_REFILL 24
 #endif
-#ifndef RT_WF_CONES
-#define RT_WF_CONES 1  // soft shadows through shadow cones (0: every soft ray traced; A/B builds)
-#endif
-#ifndef RT_LIST_SORT
-#define RT_LIST_SORT 1
-#endif
 #ifndef RT_WF_CHUNK
 #define RT_WF_CHUNK 128
 #endif
@@ -708,9 +702,6 @@ struct ConeQ {
   f2 px, py, pz;        // per axis: (second -> lower, second -> upper) penalties
   uint32_t sx, sy, sz;  // v_perm selector: which of lo / hi feeds the first bound
   float len;            // the light distance, rounded up
-#if RT_CONE_NODE == 0
-  float bo[3], bh[3], bu[3], bm;
-#endif
 };
 // First bound: always a lower bound.  Second: an upper bound (u_k >= tau or
 // <= -tau: penalties (-3e38, 0)) or a lower bound (|u_k| < tau: (0, 3e38)).
@@ -749,17 +740,6 @@ __device__ __forceinline__ ConeQ cone_q(const WfParams& p, d3 P, d3 u, double ld
   cone_q_axis(p.q0[1], p.qd[1], P.y, u.y, k.ay, k.by, k.py, k.sy, ok);
   cone_q_axis(p.q0[2], p.qd[2], P.z, u.z, k.az, k.bz, k.pz, k.sz, ok);
   k.len = (float)(ldist * (1.0 + 1e-6));
-#if RT_CONE_NODE == 0
-  k.bm = (float)(1e-5 * 65536.0 * fmax(fmax(p.qd[0], p.qd[1]), p.qd[2])) + 1e-30f;
-  k.len += k.bm;
-  const double pp[3] = {P.x, P.y, P.z}, uu[3] = {u.x, u.y, u.z};
-  for (int a = 0; a < 3; ++a) {
-    k.bo[a] = (float)(p.q0[a] - pp[a]);
-    k.bh[a] = (float)(0.5 * p.qd[a]);
-    k.bu[a] = (float)uu[a];
-  }
-  return k;
-#endif
   if (!ok) {  // every node is kept (exact, slower)
     k.ax = k.ay = k.az = f2{0.f, 0.f};
     k.bx = k.by = k.bz = f2{-1e30f, 1e30f};
@@ -768,31 +748,7 @@ __device__ __forceinline__ ConeQ cone_q(const WfParams& p, d3 P, d3 u, double ld
   }
   return k;
 }
-#ifndef RT_CONE_NODE
-#define RT_CONE_NODE 1
-#endif
-#if RT_CONE_NODE == 0
-// (A/B) the node's bounding ball against the cone, binary32
-__device__ __forceinline__ bool cone_node_ball(const uint4 n, const ConeQ& k) {
-  float v[3], e[3];
-  const uint32_t w[3] = {n.x, n.y, n.z};
-  for (int a = 0; a < 3; ++a) {
-    const float lo = (float)(w[a] & 0xFFFFu), hi = (float)(w[a] >> 16);
-    v[a] = __builtin_fmaf(lo + hi, k.bh[a], k.bo[a]);
-    e[a] = (hi - lo) * k.bh[a];
-  }
-  const float dc2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
-  const float dc = __builtin_amdgcn_sqrtf(dc2);
-  const float ra = __builtin_amdgcn_sqrtf(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]) + k.bm + 1e-4f * dc;
-  const float tl = __builtin_amdgcn_sqrtf(fmaxf(dc2 - ra * ra, 0.f));
-  const float vu = v[0] * k.bu[0] + v[1] * k.bu[1] + v[2] * k.bu[2];
-  return !(dc > ra && (dc - ra > k.len || vu < 0.99498f * tl - 0.1f * ra));
-}
-#endif
 __device__ __forceinline__ bool cone_node(const uint4 n, const ConeQ& k) {
-#if RT_CONE_NODE == 0
-  return cone_node_ball(n, k);
-#endif
   const f2 x = __builtin_elementwise_fma(q_near_far(n.x, k.sx), k.ax, k.bx);
   const f2 y = __builtin_elementwise_fma(q_near_far(n.y, k.sy), k.ay, k.by);
   const f2 z = __builtin_elementwise_fma(q_near_far(n.z, k.sz), k.az, k.bz);
@@ -1079,7 +1035,6 @@ __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
   Counters c;
   if constexpr (kCount)
     for (int k = 0; k < 9; ++k) c.v[k] = 0;
-#if RT_LIST_SORT
   // the workgroup's cones ordered by their candidate groups of four (1..4),
   // so a wave's lanes loop over about as many groups each (a wave waits
   // for its longest list)
@@ -1107,7 +1062,6 @@ __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
     __syncthreads();
     j = s_order[threadIdx.x];
   }
-#endif
   if (j < n) {
     const size_t at = dense_at(dn, 16 * j, p.soft_cap);
     const size_t sh = at / (size_t)p.soft_cap, off = at - sh * (size_t)p.soft_cap;
@@ -1471,21 +1425,17 @@ static int enqueue_bounce(const WfParams& p, hipStream_t st, const hipEvent_t* e
   mark(ev, kWfHard, st);
   if (p.nl > 0) trav(1);
   mark(ev, kWfCone, st);
-#if RT_WF_CONES
   if (p.nl > 0 && p.soft) {
     hipLaunchKernelGGL(wf_conegen, gd, b, 0, st, p);
     trav(3);
   }
-#endif
   mark(ev, kWfSoftgen, st);
   if (p.nl > 0 && p.soft) hipLaunchKernelGGL((wf_softgen<kCount>), gd, b, 0, st, p);
   mark(ev, kWfList, st);
-#if RT_WF_CONES
   if (p.nl > 0 && p.soft) {  // (at most one listed cone per path and light)
     const long long cones = live * p.nl;
     hipLaunchKernelGGL((wf_listtest<kCount>), dim3((unsigned)((cones + kWfBlock - 1) / kWfBlock)), b, 0, st, p);
   }
-#endif
   mark(ev, kWfSoft, st);
   if (p.nl > 0 && p.soft) trav(2);
   mark(ev, kWfShade, st);
@@ -1516,6 +1466,24 @@ int wf_launch_resolve(const WfParams& p, int npix, void* stream) {
   hipLaunchKernelGGL(wf_resolve, dim3((npix + kWfBlock - 1) / kWfBlock), dim3(kWfBlock), 0, (hipStream_t)stream, p,
                      npix);
   return (int)hipGetLastError();
+}
+
+
+// Cross-lane reads from inactive lanes counted by this file's kernels in an
+// RT_CHECK_XLANE build (rt_device.h); -1 in a normal build.  reset: zero it.
+long long xlane_faults_wavefront(bool reset) {
+#ifdef RT_CHECK_XLANE
+  unsigned long long v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_xlane_faults), sizeof v) != hipSuccess) return -2;
+  if (reset) {
+    const unsigned long long z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_xlane_faults), &z, sizeof z) != hipSuccess) return -2;
+  }
+  return (long long)v;
+#else
+  (void)reset;
+  return -1;
+#endif
 }
 
 }  // namespace rtgo

@@ -244,6 +244,13 @@ void flatten_scene(const rt_scene& s, FlatScene* fs) {
         r2 += (b.hi[a] - b.bc[a]) * (b.hi[a] - b.bc[a]);
       }
       b.br = sqrt(r2) * (1.0 + 1e-12);  // covers the padded box (the kernel adds its own margins)
+      // the winding of createCube's face table (scene.go:164-171): normals
+      // inward for a positive size product, outward for a negative one
+      // (DBox.front_out).  A size difference that rounds away in a vertex
+      // makes the box flat in that axis (its other faces zero-area, normal 0),
+      // where leaving the plane never returns, whichever side is "out".
+      const double vol = h.x * h.y * h.z;
+      b.front_out = vol > 0 && isfinite(vol) ? 0 : (vol < 0 && isfinite(vol) ? 1 : -1);
       fs->boxes.push_back(b);
     }
   }

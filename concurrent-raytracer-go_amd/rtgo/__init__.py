@@ -252,6 +252,8 @@ EXPORTED_SYMBOLS = [
     "rt_unpack_partition_async",
     "rt_comm_gather_bytes_async",
     "rt_renderer_rank_seconds",
+    "rt_renderer_num_ranks",
+    "rt_debug_xlane_faults",
     "rt_context_profile",
     "rt_context_kernel_seconds",
     "rt_context_render_frames_async",
@@ -343,7 +345,9 @@ def lib():
         "rt_context_set_partition": (ctypes.c_int, [vp, vp]),
         "rt_unpack_partition_async": (ctypes.c_int, [vp, vp, vp, vp, vp]),
         "rt_comm_gather_bytes_async": (ctypes.c_int, [vp, sz, vp, vp, vp]),
-        "rt_renderer_rank_seconds": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
+        "rt_renderer_rank_seconds": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int32]),
+        "rt_renderer_num_ranks": (ctypes.c_int32, [vp]),
+        "rt_debug_xlane_faults": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64)]),
         "rt_context_profile": (ctypes.c_int, [vp, i32]),
         "rt_context_render_frames_async": (
             ctypes.c_int,
@@ -612,9 +616,10 @@ class ParallelRenderer:
 
     def rank_seconds(self) -> list:
         """Device seconds of each rank's render launches in the last render (load balance)."""
-        n = max(1, len(self.devices) if self.devices else self.settings.num_devices)
-        out = (ctypes.c_double * n)()
-        _check(lib().rt_renderer_rank_seconds(self._renderer(), out))
+        r = self._renderer()
+        n = lib().rt_renderer_num_ranks(r)  # (the renderer's own count, not the mutable settings)
+        out = (ctypes.c_double * max(1, n))()
+        _check(lib().rt_renderer_rank_seconds(r, out, n))
         return list(out)
 
     def save_image(self, img: np.ndarray, filename: str):

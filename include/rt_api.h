@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4  /* 4: rt_renderer_rank_seconds takes a capacity */
 
 /* status codes */
 #define RT_OK 0
@@ -192,10 +192,17 @@ typedef struct {
 
 void rt_settings_default(rt_settings* s);
 /* The library keeps device buffers freed by destroyed contexts and renderers
- * for reuse (rt_render creates and frees its device state every call); this
- * returns them to the device. */
+ * for reuse (rt_render creates and frees its device state every call), at
+ * most 4 GB per device; this returns them to the device.  A caller that also
+ * allocates device memory elsewhere (PyTorch, RCCL) and runs short should
+ * call it: the cached blocks are invisible to other allocators. */
 int rt_release_cached_memory(void);
 int32_t rt_abi_version(void);
+/* Debug: __shfl reads of the kernels whose source lane was inactive (they
+ * return no data) since the last reset, on `device`.  Only the checking build
+ * (`make xlane`, build/xlane/librtgo.so) counts them; a normal build returns
+ * RT_E_INVALID. */
+int rt_debug_xlane_faults(int32_t device, int32_t reset, uint64_t* out);
 const char* rt_last_error(void);
 
 /* ---------------------------------------------------------------- scene */
@@ -420,8 +427,11 @@ int rt_unpack_partition_frames_async(const rt_partition* p, int32_t nframes, con
 int rt_comm_gather_bytes_async(rt_comm* comm, size_t share_bytes, const void* d_share, void* d_gathered,
                                void* hip_stream);
 /* Per rank of the renderer's last render: device seconds of its render launches
- * (out[num_devices]) -- the load balance of a multi-GPU frame. */
-int rt_renderer_rank_seconds(const rt_renderer* r, double* out);
+ * (out[capacity], capacity >= rt_renderer_num_ranks(r), else RT_E_INVALID) --
+ * the load balance of a multi-GPU frame. */
+int rt_renderer_rank_seconds(const rt_renderer* r, double* out, int32_t capacity);
+/* The renderer's rank count (the device list given to rt_renderer_create). */
+int32_t rt_renderer_num_ranks(const rt_renderer* r);
 
 /* Debug hook: a device buffer of 48 u64 per workgroup that
  * RT_WG_TIMING builds of the kernel fill: s_memrealtime at start / loop end

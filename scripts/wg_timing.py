@@ -93,6 +93,13 @@ for i in order[:6]:
               f"scat {int(scat[i, w])}; coop {int(coop[i, w])} seq {int(seq[i, w])}; wave us {end[i, w] - start[i, w]:.0f}"
               f" start {start[i, w]:.0f}")
 for i in order[:4]:
+    # slots 16..31: s_memrealtime at every 4th shade iteration, unless the
+    # workgroup ran a lone path (slot 42 != 0): then the kernel stores the lone
+    # path's section clocks there instead (rt_kernel.hip, RT_WG_TIMING epilogue)
+    if d[i, 0, 42] != 0:
+        print(f"    WG {int(i)} ran a lone path ({int(d[i, 0, 42])} bounces): its section clocks",
+              [int(v) for v in d[i, 0, 16:32]])
+        continue
     ts = [(int(v) - t0) / 100.0 for v in d[i, 0, 17:32] if v != 0]
     print(f"    WG {int(i)} time at every 4th shade iteration (us):", [round(t, 1) for t in ts])
 late = end.max(axis=1) > 0.7 * span

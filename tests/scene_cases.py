@@ -164,3 +164,95 @@ def _edge_scenes():
 
 
 EDGE_SCENES = _edge_scenes()
+
+
+def _cube_scenes():
+    """Rays inside cubes.  createCube (scene.go:150-190) winds every
+    triangle so that its normal (triangle.go:29-33) points INTO the box:
+    FrontFace (triangle.go:70-73) is true only for a hit from inside.  These
+    scenes put hit points on the inner faces of glass / dielectric cubes, the
+    camera inside a cube, lights inside and outside cubes, and cubes with
+    negative sizes (mirrored: their normals point out), so every shadow-ray
+    shortcut of the kernels (rt_kernel.hip cone_candidates: the hit object's
+    self-exclusion; box slab pruning; quiet lights; primary-ray masks) meets
+    both orientations."""
+    def sph(p, r, m):
+        return {"type": "sphere", "position": list(p), "radius": r, "material": m}
+
+    def cube(p, s, m):
+        return {"type": "cube", "position": list(p), "size": list(s), "material": m}
+
+    glass = {"type": "glass", "color": [0.9, 0.95, 1.0], "refractionIndex": 1.5}
+    diel = {"type": "dielectric", "refractionIndex": 1.33}
+    lamb = {"type": "lambertian", "color": [0.7, 0.6, 0.5]}
+    red = {"type": "lambertian", "color": [0.8, 0.2, 0.2]}
+    metal = {"type": "metal", "color": [0.9, 0.8, 0.7], "roughness": 0.1, "metallic": 0.9}
+    mirror = {"type": "metal", "color": [0.95, 0.95, 0.95], "roughness": 0.0, "metallic": 1.0}
+    cam = {"position": [0, 0.5, 6], "aspectRatio": 1.5}
+    out = {}
+    # a glass and a dielectric cube in front of the camera, lights above and
+    # behind them: refracted paths hit the inner faces, whose shadow rays
+    # toward the lights must cross the cube's far faces
+    out["glass_dielectric_cubes"] = {
+        "camera": cam,
+        "objects": [sph((0, -1001, 0), 1000, lamb), cube((-1.3, 0, 0), (1.6, 1.6, 1.6), glass),
+                    cube((1.3, 0.1, 0.3), (1.4, 1.2, 1.4), diel), sph((0, 0.3, -2.5), 1.0, metal),
+                    cube((0.2, -0.7, 2.0), (0.5, 0.5, 0.5), red)],
+        "lights": [{"position": [0, 6, 1], "color": [1, 1, 1], "intensity": 60},
+                   {"position": [-4, 1, -4], "color": [1, 0.9, 0.8], "intensity": 40}],
+    }
+    # the camera inside a large lambertian cube (every camera ray starts
+    # inside it), a light inside it and one outside
+    out["camera_inside_cube"] = {
+        "camera": {"position": [0, 0, 2], "aspectRatio": 1.5},
+        "objects": [cube((0, 0, 0), (10, 8, 10), lamb), sph((-1.2, -1.5, -2), 1.0, metal),
+                    cube((1.5, 0.5, -2.5), (1.2, 1.2, 1.2), glass), sph((0.3, 1.6, -1.5), 0.6, diel)],
+        "lights": [{"position": [1, 2.5, 0], "color": [1, 1, 1], "intensity": 20},
+                   {"position": [0, 30, 0], "color": [1, 1, 1], "intensity": 900}],
+    }
+    # a light inside a glass cube, a second light outside
+    out["light_inside_glass_cube"] = {
+        "camera": cam,
+        "objects": [sph((0, -1001, 0), 1000, lamb), cube((0, 0, 0), (2, 2, 2), glass),
+                    sph((-2.3, -0.2, 0.5), 0.8, red), sph((2.3, 0, -0.5), 0.9, metal)],
+        "lights": [{"position": [0, 0.2, 0], "color": [1, 1, 1], "intensity": 6},
+                   {"position": [3, 7, 4], "color": [1, 1, 1], "intensity": 70}],
+    }
+    # negative sizes: one or three negative components mirror the box (its
+    # normals then point out, so FrontFace means "from outside"), two restore
+    # the inward winding; glass so that paths reach both sides
+    out["mirrored_cubes"] = {
+        "camera": cam,
+        "objects": [sph((0, -1001, 0), 1000, lamb), cube((-2.2, 0, 0), (-1.4, 1.4, 1.4), glass),
+                    cube((0, 0, 0.4), (-1.3, -1.3, 1.3), diel), cube((2.2, 0, 0), (-1.4, -1.4, -1.4), glass),
+                    cube((0, 1.6, -1), (1.0, -0.6, 1.0), metal)],
+        "lights": [{"position": [1, 6, 2], "color": [1, 1, 1], "intensity": 60},
+                   {"position": [-3, 2, -5], "color": [0.8, 0.8, 1], "intensity": 40}],
+    }
+    # the camera inside a hollow mirror sphere around a glass cube and a light:
+    # 50-bounce paths, so the lone-path form (solo_path) runs them
+    out["mirror_probe_glass_cube"] = {
+        "camera": {"position": [0, 0, 3.2], "aspectRatio": 1.5},
+        "objects": [sph((0, 0, 0), 5.0, mirror), cube((0, -0.2, 0), (1.6, 1.6, 1.6), glass),
+                    sph((1.8, 1.2, -1.0), 0.5, lamb)],
+        "lights": [{"position": [0, 3.2, 0.5], "color": [1, 1, 1], "intensity": 8},
+                   {"position": [-2.5, -1.0, 1.5], "color": [1, 0.8, 0.6], "intensity": 5}],
+    }
+    # a glass cube and a lambertian cube among 70 spheres (more than 64: the
+    # scene has no shadow-cone masks and scans linearly)
+    field = [sph((0, -1001, 0), 1000, lamb)]
+    for i in range(70):
+        x = (i % 10) * 0.7 - 3.15
+        z = -(i // 10) * 0.7 + 1.0
+        field.append(sph((x, -0.8 + 0.1 * (i % 3), z), 0.22, [metal, glass, red, diel][i % 4]))
+    field += [cube((-0.6, 0.2, 1.4), (1.0, 1.0, 1.0), glass), cube((1.1, 0.0, 0.6), (0.8, 0.8, 0.8), red)]
+    out["cubes_among_70_spheres"] = {
+        "camera": cam,
+        "objects": field,
+        "lights": [{"position": [0, 6, 3], "color": [1, 1, 1], "intensity": 60},
+                   {"position": [-4, 2, -2], "color": [1, 0.9, 0.8], "intensity": 30}],
+    }
+    return out
+
+
+CUBE_SCENES = _cube_scenes()

@@ -181,6 +181,20 @@ def test_cli_fails_loudly_without_gpu(tmp_path):
     assert "device" in (p.stdout + p.stderr).lower()
 
 
+@pytest.mark.parametrize("w,h", [("0", "8"), ("8", "-3")])
+def test_cli_invalid_size_is_decided_before_the_device(tmp_path, w, h):
+    """A zero or negative size fails at SaveImage in the reference (exit 1,
+    'Error saving image'), on any machine: the CLI decides it before it makes
+    device state, so no GPU is needed for that answer."""
+    exe = os.path.join(ROOT, "concurrent-raytracer-go_amd", "build", "raytracer")
+    out = tmp_path / "o.png"
+    p = subprocess.run([exe, os.path.join(ROOT, "scenes", "sphere_reflections_light_facing.json"), str(out), w, h],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 1, p.stdout + p.stderr
+    assert "Error saving image" in p.stdout
+    assert not out.exists()
+
+
 def test_invalid_arguments_are_rejected_without_a_device():
     lib = rtgo.lib()
     assert lib.rt_context_create(0, None) != 0
