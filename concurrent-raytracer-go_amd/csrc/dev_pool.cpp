@@ -155,6 +155,59 @@ void dev_event_put(hipEvent_t ev) {  // (complete: the caller waited for it)
   g_events[dev].push_back(ev);
 }
 
+// Pinned (page-locked) host staging buffers, cached the same way.  A copy
+// between device memory and PAGEABLE host memory makes the runtime set up
+// its own staging the first time (the fresh `raytracer` process's first
+// Render waited 9.6 ms in the scene's hipMemcpy and 8 ms before the image's
+// device->host copy started, profiles/r04_cli_trace.json); the contexts and
+// renderers copy through these instead, allocated by their constructors.
+namespace {
+std::multimap<size_t, void*> g_host_free;  // size -> pinned block
+std::unordered_map<void*, size_t> g_host_live;
+size_t g_host_cached = 0;
+constexpr size_t kHostCacheCap = size_t(256) << 20;
+}  // namespace
+
+int host_alloc(void** p, size_t n) {
+  *p = nullptr;
+  const size_t sz = round_up(n == 0 ? 1 : n);
+  {
+    std::lock_guard<std::mutex> lock(g_mu);
+    auto it = g_host_free.lower_bound(sz);
+    if (it != g_host_free.end() && it->first <= 2 * sz + (size_t(16) << 20)) {
+      *p = it->second;
+      g_host_cached -= it->first;
+      g_host_live[*p] = it->first;
+      g_host_free.erase(it);
+      return hipSuccess;
+    }
+  }
+  const hipError_t e = hipHostMalloc(p, sz, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return (int)e;
+  }
+  std::lock_guard<std::mutex> lock(g_mu);
+  g_host_live[*p] = sz;
+  return hipSuccess;
+}
+
+void host_free(void* p) {  // (no copy may still use it: the caller synchronized)
+  if (!p) return;
+  std::unique_lock<std::mutex> lock(g_mu);
+  auto it = g_host_live.find(p);
+  if (it == g_host_live.end()) return;
+  const size_t sz = it->second;
+  g_host_live.erase(it);
+  if (g_host_cached + sz <= kHostCacheCap) {
+    g_host_free.emplace(sz, p);
+    g_host_cached += sz;
+    return;
+  }
+  lock.unlock();
+  (void)hipHostFree(p);
+}
+
 }  // namespace rtgo
 
 extern "C" int rt_release_cached_memory(void) {
@@ -167,6 +220,14 @@ extern "C" int rt_release_cached_memory(void) {
       dp.second.cached = 0;
     }
   }
+  std::vector<void*> host_blocks;
+  {
+    std::lock_guard<std::mutex> lock(rtgo::g_mu);
+    for (auto& b : rtgo::g_host_free) host_blocks.push_back(b.second);
+    rtgo::g_host_free.clear();
+    rtgo::g_host_cached = 0;
+  }
+  for (void* b : host_blocks) (void)hipHostFree(b);
   std::vector<std::pair<int, hipStream_t>> streams;
   std::vector<std::pair<int, hipEvent_t>> events;
   {

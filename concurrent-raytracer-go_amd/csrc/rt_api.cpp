@@ -105,6 +105,8 @@ struct rt_context {
   FlatScene flat;
   void* d_scene = nullptr;  // one allocation: spheres | tris | mats | lights | jump table | bvh
   size_t d_scene_bytes = 0;
+  void* h_stage = nullptr;  // pinned host image of the scene buffer (its upload), made by the constructor
+  size_t h_stage_cap = 0;
   const DSphere* d_spheres = nullptr;
   const DTri* d_tris = nullptr;
   const DBox* d_boxes = nullptr;
@@ -141,6 +143,10 @@ struct rt_context {
   char* d_sched = nullptr;  // scheduler scratch (sched_layout) + the per-tile inputs
   size_t sched_cap = 0;
   int32_t h_totals[4] = {0, 0, 0, 0};  // block and split counts of the last schedule (12 bytes read back)
+  // pinned staging of the schedule's small copies (the counts read back, the
+  // per-tile masks and costs uploaded), made by the constructor
+  char* h_small = nullptr;
+  size_t h_small_cap = 0;
   std::vector<unsigned long long> masks_host;  // per local tile primary-ray masks
   unsigned long long* d_masks = nullptr;       // (inside d_sched)
   int32_t stage_bytes = 0;  // scene prefix staged into LDS per workgroup (0 = none)
@@ -285,6 +291,12 @@ int rt_validate(const rt_scene* scene, int32_t w, int32_t h, const rt_settings* 
 
 const char* rt_last_error(void) { return g_last_error.c_str(); }
 
+// pinned scene staging made by rt_context_create (grown when a scene needs more)
+constexpr size_t kStageDefault = 256 * 1024;
+// pinned schedule staging: [0, 256) the counts read back, then the masks and
+// costs uploaded (grown when a frame has more tiles)
+constexpr size_t kSmallDefault = 64 * 1024;
+
 int rt_context_create(int32_t device, rt_context** out) {
   if (!out) {
     set_error("out is NULL");
@@ -330,14 +342,29 @@ int rt_context_create(int32_t device, rt_context** out) {
     std::lock_guard<std::mutex> lock(mu);
     if ((int)warmed.size() < n) warmed.resize(n, false);
     if (e == hipSuccess && !warmed[device]) {
-      void* d4 = nullptr;
-      e = (hipError_t)dev_alloc(&d4, 4096);
-      if (e == hipSuccess) e = (hipError_t)warm_device(c->stream, d4);
-      dev_free(d4);
+      constexpr size_t kWarmBytes = size_t(4) << 20;  // a large copy each way (the copy engines)
+      void* dbuf = nullptr;
+      void* hbuf = nullptr;
+      e = (hipError_t)dev_alloc(&dbuf, kWarmBytes);
+      if (e == hipSuccess) e = (hipError_t)host_alloc(&hbuf, kWarmBytes);
+      if (e == hipSuccess) e = (hipError_t)warm_device(c->stream, dbuf, hbuf, kWarmBytes);
+      host_free(hbuf);
+      dev_free(dbuf);
       if (e == hipSuccess) warmed[device] = true;
     }
   }
 
+  // pinned staging of the scene upload (a copy from pageable memory makes the
+  // runtime set up its own staging on first use: 9.6 ms of a fresh process's
+  // first Render, profiles/r04_cli_trace.json)
+  if (e == hipSuccess) {
+    e = (hipError_t)host_alloc(&c->h_stage, kStageDefault);
+    if (e == hipSuccess) c->h_stage_cap = kStageDefault;
+  }
+  if (e == hipSuccess) {
+    e = (hipError_t)host_alloc((void**)&c->h_small, kSmallDefault);
+    if (e == hipSuccess) c->h_small_cap = kSmallDefault;
+  }
   if (e != hipSuccess) {
     set_error(std::string("context init failed: ") + hipGetErrorString(e));
     rt_context_destroy(c);
@@ -358,6 +385,8 @@ void rt_context_destroy(rt_context* c) {
                   (void*)c->d_meas, (void*)c->d_split, (void*)c->d_sched, (void*)c->d_part, c->wf_mem, c->wf_rad,
                   (void*)c->wf_ctl})
     dev_free(p);
+  host_free(c->h_stage);
+  host_free(c->h_small);
   if (c->wf_host) (void)hipHostFree(c->wf_host);
   for (hipEvent_t& e : c->wf_ev)
     if (e) (void)hipEventDestroy(e);
@@ -420,14 +449,22 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
     c->d_scene_bytes = total;
   }
   char* base = (char*)c->d_scene;
-  std::vector<char> host(total, 0);
-  memcpy(host.data() + off_s, f.spheres.data(), f.spheres.size() * sizeof(DSphere));
-  memcpy(host.data() + off_t, f.tris.data(), f.tris.size() * sizeof(DTri));
-  memcpy(host.data() + off_x, f.boxes.data(), f.boxes.size() * sizeof(DBox));
-  memcpy(host.data() + off_m, f.mats.data(), f.mats.size() * sizeof(DMat));
-  memcpy(host.data() + off_l, f.lights.data(), f.lights.size() * sizeof(DLight));
+  if (total > c->h_stage_cap) {  // (the last upload was synchronized: the buffer is free)
+    host_free(c->h_stage);
+    c->h_stage = nullptr;
+    c->h_stage_cap = 0;
+    HIP_TRY((hipError_t)host_alloc(&c->h_stage, total));
+    c->h_stage_cap = total;
+  }
+  char* host = (char*)c->h_stage;
+  memset(host, 0, total);
+  memcpy(host + off_s, f.spheres.data(), f.spheres.size() * sizeof(DSphere));
+  memcpy(host + off_t, f.tris.data(), f.tris.size() * sizeof(DTri));
+  memcpy(host + off_x, f.boxes.data(), f.boxes.size() * sizeof(DBox));
+  memcpy(host + off_m, f.mats.data(), f.mats.size() * sizeof(DMat));
+  memcpy(host + off_l, f.lights.data(), f.lights.size() * sizeof(DLight));
   {
-    uint64_t* jt = reinterpret_cast<uint64_t*>(host.data() + off_j);
+    uint64_t* jt = reinterpret_cast<uint64_t*>(host + off_j);
     uint64_t a = 1, cc = 0;  // x_{i+j} = A_j x_i + C_j, built incrementally (rt_pcg_jump_coeffs)
     for (int j = 0; j < 3 * kJump; ++j) {
       if (j % 3 == 0) {  // entry h = j / 3: the jump by 3h draws
@@ -438,10 +475,11 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
       a = a * RT_PCG_MULT;
     }
   }
-  memcpy(host.data() + off_b, f.bvh.data(), f.bvh.size() * sizeof(DBVHNode));
-  memcpy(host.data() + off_q, f.qbvh.data(), f.qbvh.size() * sizeof(DQNode));
-  sky_presets(reinterpret_cast<DSky*>(host.data() + off_sky));
-  HIP_TRY(hipMemcpy(base, host.data(), total, hipMemcpyHostToDevice));
+  memcpy(host + off_b, f.bvh.data(), f.bvh.size() * sizeof(DBVHNode));
+  memcpy(host + off_q, f.qbvh.data(), f.qbvh.size() * sizeof(DQNode));
+  sky_presets(reinterpret_cast<DSky*>(host + off_sky));
+  HIP_TRY(hipMemcpyAsync(base, host, total, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
   c->d_spheres = (const DSphere*)(base + off_s);
   c->d_tris = (const DTri*)(base + off_t);
   c->d_boxes = (const DBox*)(base + off_x);
@@ -668,17 +706,26 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
       std::vector<float> cost;
       tile_cost(f, w, h, tiles, &cost);
       const size_t scratch = sched_scratch_bytes(local);
-      const size_t inputs = c->masks_host.size() * sizeof(unsigned long long) + cost.size() * sizeof(float);
+      const size_t mbytes = c->masks_host.size() * sizeof(unsigned long long), cbytes = cost.size() * sizeof(float);
+      const size_t inputs = mbytes + cbytes;
       rc = grow(c, &c->d_sched, &c->sched_cap, scratch + inputs + 256);
       if (rc) return rc;
+      if (256 + inputs > c->h_small_cap) {  // (its last use was synchronized below)
+        host_free(c->h_small);
+        c->h_small = nullptr;
+        c->h_small_cap = 0;
+        HIP_TRY((hipError_t)host_alloc((void**)&c->h_small, 256 + inputs));
+        c->h_small_cap = 256 + inputs;
+      }
       char* in = (char*)c->d_sched + ((scratch + 255) & ~size_t(255));
       c->d_masks = masks ? (unsigned long long*)in : nullptr;
-      float* d_cost = (float*)(in + c->masks_host.size() * sizeof(unsigned long long));
-      if (!c->masks_host.empty())
-        HIP_TRY(hipMemcpyAsync(c->d_masks, c->masks_host.data(), c->masks_host.size() * sizeof(unsigned long long),
-                               hipMemcpyHostToDevice, s));
-      if (!cost.empty())
-        HIP_TRY(hipMemcpyAsync(d_cost, cost.data(), cost.size() * sizeof(float), hipMemcpyHostToDevice, s));
+      float* d_cost = (float*)(in + mbytes);
+      // (through pinned staging: a pageable copy sets up the runtime's own
+      // staging on first use, milliseconds of a fresh process's first frame)
+      memcpy(c->h_small + 256, c->masks_host.data(), mbytes);
+      memcpy(c->h_small + 256 + mbytes, cost.data(), cbytes);
+      if (mbytes) HIP_TRY(hipMemcpyAsync(c->d_masks, c->h_small + 256, mbytes, hipMemcpyHostToDevice, s));
+      if (cbytes) HIP_TRY(hipMemcpyAsync(d_cost, c->h_small + 256 + mbytes, cbytes, hipMemcpyHostToDevice, s));
       SchedParams sp = sched_params(c, *p, st, tiles, dev_tiles(c, w, h, rank, world), masks, frustum, block_work,
                                     bigP, c->d_sched, c->d_masks, d_cost);
       int e = sched_launch_pixels(sp, s);
@@ -701,8 +748,9 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
         set_error(std::string("schedule launch failed: ") + hipGetErrorString((hipError_t)e));
         return RT_E_DEVICE;
       }
-      HIP_TRY(hipMemcpyAsync(c->h_totals, sp.totals, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(c->h_small, sp.totals, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
+      memcpy(c->h_totals, c->h_small, 3 * sizeof(int32_t));
       const int nblocks = c->h_totals[0], nsplit = c->h_totals[1];
       rc = grow(c, &c->d_blocks, &c->d_blocks_cap, (size_t)std::max(nblocks, 1) * kBlockInts * sizeof(int32_t));
       if (rc) return rc;

@@ -21,6 +21,9 @@ void set_error(const std::string& msg);
 // be in use by any stream when it is freed.
 int dev_alloc(void** p, size_t n);
 void dev_free(void* p);
+// pinned host staging buffers, cached per process (dev_pool.cpp)
+int host_alloc(void** p, size_t n);
+void host_free(void* p);
 // non-blocking streams and timing events, reused the same way (current device)
 int dev_stream_get(hipStream_t* s);
 void dev_stream_put(hipStream_t s);
@@ -289,7 +292,7 @@ int wf_launch_bounce(const WfParams& p, bool first, bool count, void* stream, co
 int preload_render_kernels();
 // An empty launch and a 4-KB copy each way on the stream (dev4k: 4 KB of
 // device memory): the runtime's first-launch and first-copy set-up.
-int warm_device(void* stream, void* dev4k);
+int warm_device(void* stream, void* dev_buf, void* host_pinned, size_t bytes);
 int preload_sched_kernels();
 int preload_wf_kernels();
 // RT_CHECK_XLANE builds: inactive-lane __shfl reads per file (-1: not such a build)

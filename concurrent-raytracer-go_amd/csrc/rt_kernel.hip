@@ -1781,19 +1781,35 @@ int preload_render_kernels() {
   return (int)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(render_kernel<false, true, false, false>));
 }
 
-// An empty launch and a small copy each way on `stream`: the runtime's
-// first-launch and first-copy set-up (kernel argument pool, staging
-// buffers) happens here instead of inside the first render.
+// The runtime's first-use set-up, on `stream`, so that it happens in the
+// constructor (NewParallelRenderer, main.go:46-47) instead of inside the
+// first Render (profiles/r04_cli_trace.json, a fresh `raytracer` process):
+//   - an empty launch (kernel argument pool);
+//   - a launch with private (scratch) memory: the first kernel that needs
+//     scratch makes the runtime allocate the device's scratch pool (the
+//     first render launch started 1.26 ms after it was enqueued); 512 B per
+//     lane covers every render kernel variant (<= 328 B);
+//   - a small copy each way through pageable memory and a large one each
+//     way through pinned memory (the first large device->host copy waited
+//     4.7 ms for the runtime's copy-engine set-up).
 __global__ void warm_kernel(int* p) {
   if (p && threadIdx.x == 0 && blockIdx.x == 0) p[0] = 0;
 }
-int warm_device(void* stream, void* dev4k) {
+__global__ void warm_scratch(int* p, int n) {
+  volatile int a[128];  // (volatile: kept in private memory)
+  for (int i = 0; i < 128; ++i) a[i] = i * n + (int)threadIdx.x;
+  if (p && n < 0) p[threadIdx.x] = a[(threadIdx.x * 7) & 127];
+}
+int warm_device(void* stream, void* dev_buf, void* host_pinned, size_t bytes) {
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(warm_kernel, dim3(1), dim3(64), 0, st, (int*)dev4k);
+  hipLaunchKernelGGL(warm_kernel, dim3(1), dim3(64), 0, st, (int*)dev_buf);
+  hipLaunchKernelGGL(warm_scratch, dim3(1), dim3(64), 0, st, (int*)dev_buf, 1);
   static thread_local unsigned char host[4096];
   hipError_t e = hipGetLastError();
-  if (e == hipSuccess) e = hipMemcpyAsync(dev4k, host, sizeof host, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(host, dev4k, sizeof host, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(dev_buf, host, sizeof host, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(host, dev_buf, sizeof host, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && host_pinned) e = hipMemcpyAsync(dev_buf, host_pinned, bytes, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && host_pinned) e = hipMemcpyAsync(host_pinned, dev_buf, bytes, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   return (int)e;
 }

@@ -80,6 +80,8 @@ def lib():
                                  ctypes.POINTER(i32)]
     L.oracle_rng_draws.restype = None
     L.oracle_rng_draws.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, i32, vp, vp]
+    L.oracle_path_lengths.restype = ctypes.c_int
+    L.oracle_path_lengths.argtypes = [ctypes.POINTER(rt.SceneView), i32, i32, ctypes.POINTER(rt.Settings), i32, vp]
     L.oracle_cube_triangles.restype = None
     L.oracle_cube_triangles.argtypes = [d3, d3, ctypes.c_double * 108]
     _lib = L
@@ -116,6 +118,18 @@ def render(scene, width, height, settings, rank=0, world=1, nthreads=None, max_t
     if rc != 0:
         raise RuntimeError(f"oracle_render failed: {rc}")
     return lin, rgba, (c.as_dict() if counts else None)
+
+
+def path_lengths(scene, width, height, settings, nthreads=None):
+    """Bounces of every sample's path, uint8 (H, W, spp) (clamped at 255):
+    scheduling analysis (scripts/path_stats.py), no image."""
+    nthreads = nthreads or len(os.sched_getaffinity(0))
+    out = np.zeros((height, width, settings.samples), np.uint8)
+    rc = lib().oracle_path_lengths(ctypes.byref(scene.view), width, height, ctypes.byref(settings), nthreads,
+                                   out.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"oracle_path_lengths failed: {rc}")
+    return out
 
 
 def go_pow(x, y):

@@ -237,6 +237,9 @@ typedef struct {
   /* CPU-baseline variant only (oracle_render_ex use_bvh): a sphere BVH */
   struct obvh_node* bvh;
   int* bvh_prims; /* hittable index per leaf slot */
+  /* oracle_path_lengths only: bounces (traceRay calls) of every sample's
+   * path, [pixel y*W+x][sample], clamped at 255; NULL otherwise */
+  uint8_t* path_len;
 } oscene;
 
 /* ------------------------------------------------------------ sky (opt-in)
@@ -870,7 +873,12 @@ static vec3 trace_pixel(const oscene* sc, int x, int y, ocounts* c) {
     double u = ((double)x + rnd(&st)) / (double)sc->W;
     double v = ((double)y + rnd(&st)) / (double)sc->H;
     oray r = get_ray(sc, u, v);
+    const uint64_t b0 = c->bounce_rays;
     color = vadd(color, trace_ray(sc, r, 0, &st));
+    if (sc->path_len) {
+      const uint64_t n = c->bounce_rays - b0;
+      sc->path_len[(size_t)pixel * (size_t)sc->samples + (size_t)smp] = (uint8_t)(n > 255 ? 255 : n);
+    }
   }
   return vdivs(color, (double)sc->samples);
 }
@@ -977,9 +985,26 @@ int oracle_render(const rt_scene* scene, int32_t width, int32_t height, const rt
                           0);
 }
 
+static int render_impl(const rt_scene* scene, int32_t width, int32_t height, const rt_settings* st, int32_t rank,
+                       int32_t world, int32_t nthreads, int32_t max_tiles, double* out_linear, uint8_t* out_rgba,
+                       rt_counts* counts, int32_t use_bvh, uint8_t* path_len);
+
 int oracle_render_ex(const rt_scene* scene, int32_t width, int32_t height, const rt_settings* st, int32_t rank,
                      int32_t world, int32_t nthreads, int32_t max_tiles, double* out_linear, uint8_t* out_rgba,
                      rt_counts* counts, int32_t use_bvh) {
+  return render_impl(scene, width, height, st, rank, world, nthreads, max_tiles, out_linear, out_rgba, counts, use_bvh,
+                     NULL);
+}
+
+int oracle_path_lengths(const rt_scene* scene, int32_t width, int32_t height, const rt_settings* st,
+                        int32_t nthreads, uint8_t* out) {
+  if (!out) return RT_E_INVALID;
+  return render_impl(scene, width, height, st, 0, 1, nthreads, -1, NULL, NULL, NULL, 0, out);
+}
+
+static int render_impl(const rt_scene* scene, int32_t width, int32_t height, const rt_settings* st, int32_t rank,
+                       int32_t world, int32_t nthreads, int32_t max_tiles, double* out_linear, uint8_t* out_rgba,
+                       rt_counts* counts, int32_t use_bvh, uint8_t* path_len) {
   if (!scene || !st || width <= 0 || height <= 0 || world < 1 || rank < 0 || rank >= world) return RT_E_INVALID;
   if (scene->num_objects < 0 || scene->num_lights < 0) return RT_E_INVALID;
   if (nthreads < 1) nthreads = 1;
@@ -1020,6 +1045,7 @@ int oracle_render_ex(const rt_scene* scene, int32_t width, int32_t height, const
   sc.seed_key = rt_rng_seed_key(st->seed);
   sc.W = width;
   sc.H = height;
+  sc.path_len = path_len;
   if (use_bvh) bvh_make(&sc);
 
   ojob job;

@@ -43,6 +43,12 @@ int oracle_render_ex(const rt_scene* scene, int32_t width, int32_t height, const
                      int32_t rank, int32_t world, int32_t nthreads, int32_t max_tiles, double* out_linear,
                      uint8_t* out_rgba, rt_counts* counts, int32_t use_bvh);
 
+/* Scheduling analysis (dev tool, scripts/path_stats.py): the bounces of every
+ * sample's path (traceRay calls, clamped at 255) of the whole frame,
+ * out[(y*W + x)*samples + s]; no image. */
+int oracle_path_lengths(const rt_scene* scene, int32_t width, int32_t height, const rt_settings* settings,
+                        int32_t nthreads, uint8_t* out);
+
 /* Building blocks exposed for known-answer tests. */
 double oracle_go_pow(double x, double y);            /* math.Pow */
 double oracle_go_max(double x, double y);            /* math.Max */

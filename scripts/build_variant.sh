@@ -4,6 +4,8 @@
 # build.  usage: scripts/build_variant.sh NAME "-DFOO -DBAR=2"
 # -> concurrent-raytracer-go_amd/build/var_NAME/librtgo.so (time it with
 #    scripts/ab_bench.py or RTGO_LIB=... python bench.py)
+# VARIANT_SRC=DIR compiles the .hip files from DIR (a patched copy of csrc/)
+# instead, so the in-tree sources and build stay untouched.
 set -eu
 NAME=$1
 DEFS=${2:-}
@@ -12,8 +14,9 @@ make -s -j8 >/dev/null
 OUT=build/var_$NAME
 mkdir -p "$OUT"
 HIPFLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -Wall -Wno-unused-function -munsafe-fp-atomics"
+SRC=${VARIANT_SRC:-csrc}
 for k in rt_kernel rt_wavefront rt_schedule; do
-  /opt/rocm/bin/hipcc $HIPFLAGS $DEFS -x hip -c csrc/$k.hip -o "$OUT/$k.o" &
+  /opt/rocm/bin/hipcc $HIPFLAGS $DEFS -I"$(pwd)/csrc" -x hip -c $SRC/$k.hip -o "$OUT/$k.o" &
 done
 wait
 OBJS="$OUT/rt_kernel.o $OUT/rt_wavefront.o $OUT/rt_schedule.o"
