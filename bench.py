@@ -353,8 +353,9 @@ def render_e2e(rtgo, scene, W, H, args, local):
         "oneshot_value": round(rays / statistics.median(one) / 1e6, 3),
         "note": "rt_renderer_render (NewParallelRenderer once, Render per frame): rt_stats.render_seconds, "
                 "median of 7 calls with distinct seeds; includes the scene check and the device->host copy "
-                "of the float3 + RGBA8 image (pageable host memory). first_call_ms: the first Render of a new "
-                "renderer (device context, scene upload, schedule + pilot). oneshot: rt_render, which "
+                "of the float3 + RGBA8 image into the caller's (pageable) buffers, through the renderer's pinned "
+                "staging. first_call_ms: the first Render of a new renderer, its creation included (device "
+                "context, scene upload, schedule + pilot). oneshot: rt_render, which "
                 "creates and destroys the device context every call (median of 5).",
     }
 

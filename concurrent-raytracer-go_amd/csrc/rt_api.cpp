@@ -347,7 +347,8 @@ int rt_context_create(int32_t device, rt_context** out) {
       void* hbuf = nullptr;
       e = (hipError_t)dev_alloc(&dbuf, kWarmBytes);
       if (e == hipSuccess) e = (hipError_t)host_alloc(&hbuf, kWarmBytes);
-      if (e == hipSuccess) e = (hipError_t)warm_device(c->stream, dbuf, hbuf, kWarmBytes);
+      std::vector<char> pageable(kWarmBytes);
+      if (e == hipSuccess) e = (hipError_t)warm_device(c->stream, dbuf, hbuf, pageable.data(), kWarmBytes);
       host_free(hbuf);
       dev_free(dbuf);
       if (e == hipSuccess) warmed[device] = true;

@@ -292,7 +292,7 @@ int wf_launch_bounce(const WfParams& p, bool first, bool count, void* stream, co
 int preload_render_kernels();
 // An empty launch and a 4-KB copy each way on the stream (dev4k: 4 KB of
 // device memory): the runtime's first-launch and first-copy set-up.
-int warm_device(void* stream, void* dev_buf, void* host_pinned, size_t bytes);
+int warm_device(void* stream, void* dev_buf, void* host_pinned, void* host_pageable, size_t bytes);
 int preload_sched_kernels();
 int preload_wf_kernels();
 // RT_CHECK_XLANE builds: inactive-lane __shfl reads per file (-1: not such a build)

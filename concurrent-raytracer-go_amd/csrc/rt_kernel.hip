@@ -1783,15 +1783,19 @@ int preload_render_kernels() {
 
 // The runtime's first-use set-up, on `stream`, so that it happens in the
 // constructor (NewParallelRenderer, main.go:46-47) instead of inside the
-// first Render (profiles/r04_cli_trace.json, a fresh `raytracer` process):
+// first Render (profiles/r04_cli_trace.json, a fresh `raytracer` process;
+// scripts/copy_probe.hip):
 //   - an empty launch (kernel argument pool);
 //   - a launch with private (scratch) memory: the first kernel that needs
 //     scratch makes the runtime allocate the device's scratch pool (the
 //     first render launch started 1.26 ms after it was enqueued); 512 B per
 //     lane covers every render kernel variant (<= 328 B);
-//   - a small copy each way through pageable memory and a large one each
-//     way through pinned memory (the first large device->host copy waited
-//     4.7 ms for the runtime's copy-engine set-up).
+//   - copies each way through pageable and pinned memory, and device->host
+//     copies queued behind a kernel that is still running: the first time a
+//     process's copy has to wait for a running kernel it starts ~8-9 ms after
+//     the kernel ends (the CLI's image download; scripts/copy_probe.hip:
+//     later ones start at once, 0.16 ms for 8 MB).  warm_busy runs ~0.2 ms
+//     so the copies are queued while it still runs.
 __global__ void warm_kernel(int* p) {
   if (p && threadIdx.x == 0 && blockIdx.x == 0) p[0] = 0;
 }
@@ -1800,7 +1804,12 @@ __global__ void warm_scratch(int* p, int n) {
   for (int i = 0; i < 128; ++i) a[i] = i * n + (int)threadIdx.x;
   if (p && n < 0) p[threadIdx.x] = a[(threadIdx.x * 7) & 127];
 }
-int warm_device(void* stream, void* dev_buf, void* host_pinned, size_t bytes) {
+__global__ void warm_busy(float* p, int iters) {
+  float v = (float)threadIdx.x;
+  for (int k = 0; k < iters; ++k) v = v * 0.999f + 1.0f;  // a dependent chain: ~4 clocks per step
+  if (p && v < 0.f) p[threadIdx.x] = v;
+}
+int warm_device(void* stream, void* dev_buf, void* host_pinned, void* host_pageable, size_t bytes) {
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(warm_kernel, dim3(1), dim3(64), 0, st, (int*)dev_buf);
   hipLaunchKernelGGL(warm_scratch, dim3(1), dim3(64), 0, st, (int*)dev_buf, 1);
@@ -1808,8 +1817,13 @@ int warm_device(void* stream, void* dev_buf, void* host_pinned, size_t bytes) {
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipMemcpyAsync(dev_buf, host, sizeof host, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(host, dev_buf, sizeof host, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess && host_pinned) e = hipMemcpyAsync(dev_buf, host_pinned, bytes, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess && host_pinned) e = hipMemcpyAsync(host_pinned, dev_buf, bytes, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(dev_buf, host_pinned, bytes, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(dev_buf, host_pageable, bytes, hipMemcpyHostToDevice, st);
+  for (int k = 0; k < 2 && e == hipSuccess; ++k) {  // behind a kernel: into pageable, then pinned memory
+    hipLaunchKernelGGL(warm_busy, dim3(1), dim3(64), 0, st, (float*)dev_buf, 120000);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(k ? host_pinned : host_pageable, dev_buf, bytes, hipMemcpyDeviceToHost, st);
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   return (int)e;
 }

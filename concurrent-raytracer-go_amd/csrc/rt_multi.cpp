@@ -167,11 +167,6 @@ struct rt_renderer {
   rt_partition* part = nullptr;
   std::vector<int64_t> part_key;
   std::vector<double> rank_secs;   // device seconds of each rank's last render
-  // pinned staging of the image's device->host copy, made by the constructor
-  // (a copy into pageable memory makes the runtime set up its own staging on
-  // first use: 8 ms of a fresh process's first Render, profiles/r04_cli_trace.json)
-  void* h_img = nullptr;
-  size_t h_img_cap = 0;
 };
 
 struct rt_comm {
@@ -318,15 +313,6 @@ int rt_renderer_create(const int32_t* devices, int32_t n, rt_renderer** out) {
     Rank& q = r->ranks[k];
     if ((int)r->comm_streams.size() <= q.comm_idx) r->comm_streams.push_back(q.stream);
   }
-  {
-    // 16 MB: an 800x600 frame's float3 + RGBA8 twice over (grown on demand)
-    const size_t cap = size_t(16) << 20;
-    if (hipSetDevice(r->ranks[0].device) != hipSuccess || host_alloc(&r->h_img, cap) != hipSuccess) {
-      set_error("rt_renderer_create: pinned staging allocation failed");
-      return renderer_fail_cleanup(r, RT_E_NOMEM);
-    }
-    r->h_img_cap = cap;
-  }
   if (r->devices.size() > 1) {
     r->comms.resize(r->devices.size());
     ncclResult_t e = ncclCommInitAll(r->comms.data(), (int)r->devices.size(), r->devices.data());
@@ -349,7 +335,6 @@ void rt_renderer_destroy(rt_renderer* r) {
     }
   }
   for (ncclComm_t c : r->comms) (void)ncclCommDestroy(c);
-  host_free(r->h_img);
   rt_partition_destroy(r->part);
   const int root = r->ranks.empty() ? 0 : r->ranks[0].device;
   r->gathered.release(root);
@@ -481,18 +466,12 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
   }
   HIP_TRY(hipSetDevice(root));
   const double t_launch = now_s();
-  // the image through the pinned staging (grown when the frame is larger;
-  // its last copy was synchronized by the previous call)
-  const size_t lin_b = out_linear ? npix * 3 * sizeof(float) : 0, rgba_b = out_rgba ? npix * 4 : 0;
-  if (lin_b + rgba_b > r->h_img_cap) {
-    host_free(r->h_img);
-    r->h_img = nullptr;
-    r->h_img_cap = 0;
-    HIP_TRY((hipError_t)host_alloc(&r->h_img, lin_b + rgba_b));
-    r->h_img_cap = lin_b + rgba_b;
-  }
-  if (lin_b) HIP_TRY(hipMemcpyAsync(r->h_img, r->img_lin.p, lin_b, hipMemcpyDeviceToHost, root_s));
-  if (rgba_b) HIP_TRY(hipMemcpyAsync((char*)r->h_img + lin_b, r->img_rgba.p, rgba_b, hipMemcpyDeviceToHost, root_s));
+  // straight into the caller's buffers (the runtime's first-use set-up of a
+  // device->host copy queued behind a kernel, ~9 ms, is done by the
+  // constructor: warm_device)
+  if (out_linear)
+    HIP_TRY(hipMemcpyAsync(out_linear, r->img_lin.p, npix * 3 * sizeof(float), hipMemcpyDeviceToHost, root_s));
+  if (out_rgba) HIP_TRY(hipMemcpyAsync(out_rgba, r->img_rgba.p, npix * 4, hipMemcpyDeviceToHost, root_s));
   double ks = 0;
   r->rank_secs.assign(n, 0.0);
   for (int k = 0; k < n; ++k) {
@@ -505,8 +484,6 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
     r->rank_secs[k] = s;
     ks = std::max(ks, s);
   }
-  if (lin_b) memcpy(out_linear, r->h_img, lin_b);
-  if (rgba_b) memcpy(out_rgba, (char*)r->h_img + lin_b, rgba_b);
   const double t_end = now_s();
   const double secs = t_end - t0;
   if (stats) {
