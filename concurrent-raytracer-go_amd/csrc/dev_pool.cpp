@@ -168,8 +168,9 @@ size_t g_host_cached = 0;
 constexpr size_t kHostCacheCap = size_t(256) << 20;
 }  // namespace
 
-int host_alloc(void** p, size_t n) {
+int host_alloc(void** p, size_t n, bool* fresh) {
   *p = nullptr;
+  if (fresh) *fresh = false;
   const size_t sz = round_up(n == 0 ? 1 : n);
   {
     std::lock_guard<std::mutex> lock(g_mu);
@@ -187,6 +188,7 @@ int host_alloc(void** p, size_t n) {
     *p = nullptr;
     return (int)e;
   }
+  if (fresh) *fresh = true;
   std::lock_guard<std::mutex> lock(g_mu);
   g_host_live[*p] = sz;
   return hipSuccess;

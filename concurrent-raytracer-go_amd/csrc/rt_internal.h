@@ -22,7 +22,7 @@ void set_error(const std::string& msg);
 int dev_alloc(void** p, size_t n);
 void dev_free(void* p);
 // pinned host staging buffers, cached per process (dev_pool.cpp)
-int host_alloc(void** p, size_t n);
+int host_alloc(void** p, size_t n, bool* fresh = nullptr);  // fresh: newly pinned (not from the cache)
 void host_free(void* p);
 // non-blocking streams and timing events, reused the same way (current device)
 int dev_stream_get(hipStream_t* s);
@@ -191,6 +191,8 @@ struct KParams {
 // Enqueue the render kernel; returns hipError_t as int.
 int launch_render(const KParams& p, bool count, void* stream);
 size_t render_shmem(const KParams& p);
+// device -> mapped pinned host memory by a kernel (16-byte aligned, a multiple of 16 bytes)
+int launch_download(const void* d_src, void* h_dst_mapped, size_t bytes, void* stream);
 int launch_unpack(int32_t W, int32_t H, int32_t world, const void* gathered, size_t share_bytes, size_t rgba_off,
                   float* ol, uint8_t* orgba, void* stream);
 // The same for a partition: slot[t] = {owner rank, local tile} of global tile t;

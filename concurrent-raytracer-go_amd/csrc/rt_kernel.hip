@@ -1796,6 +1796,7 @@ int preload_render_kernels() {
 //     the kernel ends (the CLI's image download; scripts/copy_probe.hip:
 //     later ones start at once, 0.16 ms for 8 MB).  warm_busy runs ~0.2 ms
 //     so the copies are queued while it still runs.
+//     (Render itself copies only from an idle stream, rt_renderer_render.)
 __global__ void warm_kernel(int* p) {
   if (p && threadIdx.x == 0 && blockIdx.x == 0) p[0] = 0;
 }
@@ -1820,7 +1821,7 @@ int warm_device(void* stream, void* dev_buf, void* host_pinned, void* host_pagea
   if (e == hipSuccess) e = hipMemcpyAsync(dev_buf, host_pinned, bytes, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(dev_buf, host_pageable, bytes, hipMemcpyHostToDevice, st);
   for (int k = 0; k < 2 && e == hipSuccess; ++k) {  // behind a kernel: into pageable, then pinned memory
-    hipLaunchKernelGGL(warm_busy, dim3(1), dim3(64), 0, st, (float*)dev_buf, 120000);
+    hipLaunchKernelGGL(warm_busy, dim3(1), dim3(64), 0, st, (float*)dev_buf, 10000);
     e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpyAsync(k ? host_pinned : host_pageable, dev_buf, bytes, hipMemcpyDeviceToHost, st);
   }
@@ -1879,6 +1880,23 @@ int launch_render(const KParams& pin, bool count, void* stream) {
   } else {
     hipLaunchKernelGGL((render_kernel<false, false, false, false>), g, b, shmem, st, p);
   }
+  return (int)hipGetLastError();
+}
+
+// The image to pinned host memory, written by the GPU itself (16 B per lane,
+// coalesced): the first Render of a renderer, where a copy-engine transfer
+// started 7-15 ms late in a fresh process (rt_renderer_render).
+__global__ __launch_bounds__(256) void download_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+int launch_download(const void* d_src, void* h_dst_mapped, size_t bytes, void* stream) {
+  if (bytes == 0) return hipSuccess;
+  if ((bytes & 15) || ((uintptr_t)d_src & 15) || ((uintptr_t)h_dst_mapped & 15)) return hipErrorInvalidValue;
+  const size_t n16 = bytes / 16;
+  const unsigned grid = (unsigned)((n16 + 255) / 256 < 2048 ? (n16 + 255) / 256 : 2048);
+  hipLaunchKernelGGL(download_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint4*)d_src,
+                     (uint4*)h_dst_mapped, n16);
   return (int)hipGetLastError();
 }
 

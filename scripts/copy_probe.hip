@@ -56,5 +56,30 @@ int main() {
     hipStreamSynchronize(s);
     printf("idle stream %-8s: copy %.3f ms\n", names[kind], (now() - t1) * 1e3);
   }
+  // copies after the copy engine sat idle for a while (host sleep)
+  for (int idle_ms : {0, 1, 2, 5, 10, 20, 50}) {
+    for (int kind = 0; kind < 2; ++kind) {
+      float* h = kind ? pinned : pageable.data();
+      hipMemcpyAsync(h, d, n * 4, hipMemcpyDeviceToHost, s);
+      hipStreamSynchronize(s);
+      const double ts = now();
+      while (now() - ts < idle_ms * 1e-3) {
+      }
+      double t1 = now();
+      hipMemcpyAsync(h, d, n * 4, hipMemcpyDeviceToHost, s);
+      hipStreamSynchronize(s);
+      printf("after %2d ms idle %-8s: copy %.3f ms\n", idle_ms, names[kind], (now() - t1) * 1e3);
+    }
+  }
+  // small copies (1.92 MB, the CLI's RGBA image) after idling
+  for (int idle_ms : {2, 10}) {
+    const double ts = now();
+    while (now() - ts < idle_ms * 1e-3) {
+    }
+    double t1 = now();
+    hipMemcpyAsync(pageable.data(), d, 1920000, hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    printf("after %2d ms idle pageable 1.92 MB: copy %.3f ms\n", idle_ms, (now() - t1) * 1e3);
+  }
   return 0;
 }
