@@ -86,6 +86,9 @@ FLOPS_PER_BOX = 12          # 6 fma + 6 min/max/compare
 # a ray the soft-shadow traversal kernel sets up: light vector (12), the
 # jittered direction (15), inverse direction (3), the binary64 root box (12)
 SOFT_RAY_SETUP_FLOPS = 42
+# a ray the closest-hit / hard-ray traversal sets up: |d|^2 and its
+# reciprocal (6), the inverse direction (3), the binary64 root box (12)
+TRAV_RAY_SETUP_FLOPS = 21
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) peak: 256 CU x 2.4 GHz x 128 FLOP/clk
 PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
@@ -697,7 +700,23 @@ def main():
         kern_s, launches_per_frame = per_frame_s, k_n / frames_timed
         flops_unit = "per frame (%.0f launches)" % launches_per_frame
         frame64, frame32 = fp_split(ex)
-        whole = {"fp64_flops": frame64, "fp32_flops": frame32,
+        # the two largest kernels since r03 on their own counts and HIP-event
+        # time (rt_counts.extend / hard_occlusion)
+        per_kernel = {}
+        for name, cd, rays_key in (("extend", counts.extend_dict(), "bounce_rays"),
+                                   ("occlude_hard", counts.hard_occlusion_dict(), "shadow_rays")):
+            ks_k = kernel_prof[name][0] / frames_timed
+            k64 = cd[rays_key] * TRAV_RAY_SETUP_FLOPS + cd["sphere_tests"] * FLOPS_PER_EVENT["sphere_tests"]
+            k32 = max(0, cd["box_tests"] - cd[rays_key]) * FLOPS_PER_BOX  # (the root box: binary64, in the set-up)
+            per_kernel[name] = {
+                "kernel_ms_per_frame": round(ks_k * 1e3, 3), "rays": cd[rays_key],
+                "sphere_tests": cd["sphere_tests"], "box_tests": cd["box_tests"],
+                "fp64_flops": k64, "fp32_flops": k32,
+                "achieved_tflops": round((k64 + k32) / ks_k / 1e12, 4) if ks_k > 0 else None,
+                "frac": round(k64 / ks_k / 1e12 / PEAK_FP64_TFLOPS + k32 / ks_k / 1e12 / PEAK_FP32_TFLOPS, 5)
+                if ks_k > 0 else None,
+            }
+        whole = {"fp64_flops": frame64, "fp32_flops": frame32, "kernels": per_kernel,
                  "frame_kernel_ms": round(kernel1_s * 1e3, 3),
                  "frac_fp64": round(frame64 / kernel1_s / 1e12 / PEAK_FP64_TFLOPS, 5),
                  "frac_fp32": round(frame32 / kernel1_s / 1e12 / PEAK_FP32_TFLOPS, 5),

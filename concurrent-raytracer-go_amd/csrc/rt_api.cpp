@@ -1112,7 +1112,9 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
     counts->rng_draws = h_c[8];
     for (int i = 0; i < kCounters; ++i) {
       counts->culled[i] = h_c[kCounters + i];
-      counts->soft_occlusion[i] = h_c[2 * kCounters + i];
+      counts->soft_occlusion[i] = h_c[kGroupSoft * kCounters + i];
+      counts->extend[i] = h_c[kGroupExtend * kCounters + i];
+      counts->hard_occlusion[i] = h_c[kGroupHard * kCounters + i];
     }
   }
   return RT_OK;

@@ -123,7 +123,10 @@ constexpr int kDbgStride = 48;  // RT_WG_TIMING: 64-bit words per workgroup in t
 // reference's counts (camera samples of culled pixels, rt_counts.culled),
 // then the soft-shadow traversal kernel's share (rt_counts.soft_occlusion).
 constexpr int kCounters = 9;
-constexpr int kCountSlots = 3 * kCounters;
+constexpr int kCountSlots = 5 * kCounters;
+// count groups after the totals (rt_counts): culled, then the wavefront
+// kernels' own shares -- soft-shadow stage, closest hit, hard occlusion
+constexpr int kGroupSoft = 2, kGroupExtend = 3, kGroupHard = 4;
 // Deepest BVH the kernels accept (per-lane LDS stack entries; bvh.cpp keeps
 // the linear scan for deeper trees).  The stacks are allocated per launch for
 // the scene's actual depth (10k spheres: 15 levels).

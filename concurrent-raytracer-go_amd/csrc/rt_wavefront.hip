@@ -169,20 +169,23 @@ __device__ __forceinline__ size_t dense_at(const Dense& d, int j, size_t cap) {
   return (size_t)s * cap + (size_t)(j - off);
 }
 
-// (soft: the soft-shadow traversal kernel also adds its counts to the
-// rt_counts.soft_occlusion slots, for its own roofline; there the shadow-ray
-// slot counts the rays it traced, kept in c.v[kSoftJobs] -- softgen counts
-// them for the totals)
+// (group: the kernel also adds its counts to its own slots of rt_counts --
+// kGroupSoft: the soft-shadow stage (rt_counts.soft_occlusion); kGroupHard:
+// the hard-ray traversal (rt_counts.hard_occlusion) -- in both the
+// shadow-ray slot counts the rays the kernel traced, kept in c.v[kSoftJobs]
+// and left out of the totals (softgen and shade1 count them there);
+// kGroupExtend: the closest-hit traversal (rt_counts.extend) -- for each
+// kernel's own roofline)
 constexpr int kSoftJobs = C_SHADOW;
 template <bool kCount>
-__device__ __forceinline__ void flush_counts(const WfParams& p, Counters& c, bool soft = false) {
+__device__ __forceinline__ void flush_counts(const WfParams& p, Counters& c, int group = 0) {
   if constexpr (kCount) {
     for (int i = 0; i < kCounters; ++i) {
       unsigned long long v = c.v[i];
       for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
       if ((threadIdx.x & 63) == 0 && v) {
-        if (!(soft && i == kSoftJobs)) atomicAdd(&p.counts[i], v);
-        if (soft) atomicAdd(&p.counts[2 * kCounters + i], v);
+        if (!((group == kGroupSoft || group == kGroupHard) && i == kSoftJobs)) atomicAdd(&p.counts[i], v);
+        if (group) atomicAdd(&p.counts[group * kCounters + i], v);
       }
     }
   }
@@ -494,7 +497,7 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
       }
     }
   }
-  flush_counts<kCount>(p, c);
+  flush_counts<kCount>(p, c, kGroupExtend);
 }
 
 // ---------------------------------------------------------------- shade1
@@ -614,7 +617,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
         else
           e = make_uint4(p.hardq[at], 0, 0, 0);
         key = e.x;
-        if constexpr (kCount && kSoft) ++c.v[kSoftJobs];  // (flushed to the soft-occlusion slots only)
+        if constexpr (kCount) ++c.v[kSoftJobs];  // (the rays traced: flushed to the kernel's own slots only)
         const uint32_t slot = key / (uint32_t)p.nl, li = key - slot * (uint32_t)p.nl;
         o = mk(p.px[slot], p.py[slot], p.pz[slot]);
         d3 ldir;
@@ -667,7 +670,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
       if (blocked || cur == -1) busy = false;
     }
   }
-  flush_counts<kCount>(p, c, kSoft);
+  flush_counts<kCount>(p, c, kSoft ? kGroupSoft : kGroupHard);
 }
 
 // ---------------------------------------------------------------- cones
@@ -915,7 +918,7 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
       }
     }
   }
-  flush_counts<kCount>(p, c, true);
+  flush_counts<kCount>(p, c, kGroupSoft);
 }
 
 // ---------------------------------------------------------------- softgen
@@ -1105,7 +1108,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
     }
     p.lstate[key] = (uint32_t)__popc(blocked);
   }
-  flush_counts<kCount>(p, c, true);
+  flush_counts<kCount>(p, c, kGroupSoft);
 }
 
 // ---------------------------------------------------------------- shade

@@ -180,7 +180,9 @@ COUNT_FIELDS = [
 
 class Counts(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in COUNT_FIELDS] + [("culled", ctypes.c_uint64 * 9),
-                                                               ("soft_occlusion", ctypes.c_uint64 * 9)]
+                                                               ("soft_occlusion", ctypes.c_uint64 * 9),
+                                                               ("extend", ctypes.c_uint64 * 9),
+                                                               ("hard_occlusion", ctypes.c_uint64 * 9)]
 
     def as_dict(self):
         """The nine counts (the reference's: every camera sample walked)."""
@@ -193,6 +195,14 @@ class Counts(ctypes.Structure):
     def soft_occlusion_dict(self):
         """The wavefront soft-shadow traversal kernel's share of the counts."""
         return {n: int(self.soft_occlusion[i]) for i, n in enumerate(COUNT_FIELDS)}
+
+    def extend_dict(self):
+        """The wavefront closest-hit traversal kernel's share of the counts."""
+        return {n: int(self.extend[i]) for i, n in enumerate(COUNT_FIELDS)}
+
+    def hard_occlusion_dict(self):
+        """The wavefront hard-ray traversal kernel's share of the counts."""
+        return {n: int(self.hard_occlusion[i]) for i, n in enumerate(COUNT_FIELDS)}
 
     def executed_dict(self):
         """Executed work: count - culled."""

@@ -188,6 +188,13 @@ typedef struct {
    * of the counts, for that kernel's own roofline (shadow_rays: the rays it
    * traced).  Zero on the megakernel. */
   uint64_t soft_occlusion[9];
+  /* The wavefront path's closest-hit traversal (wf_extend, hitWorld
+   * renderer.go:333-346) and hard-ray traversal (wf_occlude<hard>,
+   * renderer.go:305) alone: their shares of the counts (box and sphere tests;
+   * bounce_rays / shadow_rays: the rays each traversed), for each kernel's own
+   * roofline.  Zero on the megakernel. */
+  uint64_t extend[9];
+  uint64_t hard_occlusion[9];
 } rt_counts;
 
 void rt_settings_default(rt_settings* s);

@@ -198,7 +198,14 @@ def test_cone_routes_match_megakernel_and_oracle():
     lin = torch.zeros(w * h * 3, dtype=torch.float32, device="cuda")
     c = ctx.count(w, h, st, lin.data_ptr(), 0, full=True)
     soft = c.soft_occlusion_dict()
+    ext, hard = c.extend_dict(), c.hard_occlusion_dict()
     ctx.close()
+    # the closest-hit and hard-ray traversals' own counts (bench.py per-kernel
+    # roofline): every closest-hit query runs in wf_extend; the hard rays not
+    # settled by their own sphere (wf_shade1) run in wf_occlude<hard>
+    assert ext["bounce_rays"] == c.bounce_rays and ext["box_tests"] > 0 and ext["sphere_tests"] > 0, ext
+    assert 0 < hard["shadow_rays"] < c.shadow_rays and hard["box_tests"] > 0, hard
+    assert ext["sphere_tests"] + hard["sphere_tests"] + soft["sphere_tests"] <= c.sphere_tests
     assert soft["shadow_rays"] > 0, soft                     # traced (overflowing cones)
     assert soft["shadow_rays"] < c.shadow_rays, (soft, c.shadow_rays)  # not all: lists and empty cones
     assert soft["sphere_tests"] > 0 and soft["box_tests"] > 0
