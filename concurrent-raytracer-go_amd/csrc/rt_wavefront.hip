@@ -736,19 +736,18 @@ __device__ __forceinline__ void cone_q_axis(double q0, double qd, double P, doub
   ok = ok && fabs(A) > 1e-6 && fabs(B) > 1e-6 && fabs(a1) < 1e30 && fabs(a2) < 1e30 && fabs(b1) < 1e37 &&
        fabs(b2) < 1e37;
 }
-__device__ __forceinline__ ConeQ cone_q(const WfParams& p, d3 P, d3 u, double ldist) {
+// ok = false: a coefficient is not finite or too large for binary32; the
+// caller then does not walk the cone (its rays are traced, exact).  (Round 3
+// kept every node instead, by selects on all of ConeQ's fields; that form
+// made the cone kernel 4.7x slower, 249 vs 53 ms per C4 frame, though the
+// fallback never runs on C4: it changed how the kernel's code came out.)
+__device__ __forceinline__ ConeQ cone_q(const WfParams& p, d3 P, d3 u, double ldist, bool& ok) {
   ConeQ k;
-  bool ok = __builtin_isfinite(ldist);
+  ok = __builtin_isfinite(ldist);
   cone_q_axis(p.q0[0], p.qd[0], P.x, u.x, k.ax, k.bx, k.px, k.sx, ok);
   cone_q_axis(p.q0[1], p.qd[1], P.y, u.y, k.ay, k.by, k.py, k.sy, ok);
   cone_q_axis(p.q0[2], p.qd[2], P.z, u.z, k.az, k.bz, k.pz, k.sz, ok);
   k.len = (float)(ldist * (1.0 + 1e-6));
-  if (!ok) {  // every node is kept (exact, slower)
-    k.ax = k.ay = k.az = f2{0.f, 0.f};
-    k.bx = k.by = k.bz = f2{-1e30f, 1e30f};
-    k.px = k.py = k.pz = f2{-3e38f, 0.f};
-    k.len = 3e38f;
-  }
   return k;
 }
 __device__ __forceinline__ bool cone_node(const uint4 n, const ConeQ& k) {
@@ -878,9 +877,12 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
         const d3 outward = divs(P - ld3(S0.c), S0.r);
         const bool self_out = dot(ld_d(p.cur, slot), outward) < 0 && dot(outward, u) >= 0.1015;
         excl = self_out ? S0.obj : -1;
-        k = cone_q(p, P, u, ldist);
-        found = 0;
-        cur = bvh_code(p.g.bvh[0]);
+        bool ok;
+        k = cone_q(p, P, u, ldist, ok);
+        // (a cone whose bounds cannot be evaluated is not walked: "too many
+        // candidates", so its rays are traced)
+        found = ok ? 0 : kWfConeK + 1;
+        cur = ok ? bvh_code(p.g.bvh[0]) : -1;
         sp = 0;
         busy = true;
       }
