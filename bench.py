@@ -92,7 +92,7 @@ TRAV_RAY_SETUP_FLOPS = 21
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) peak: 256 CU x 2.4 GHz x 128 FLOP/clk
 PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r04_pmc_traffic.json")
 
 CONFIGS = {
     # name: (scene, W, H, spp, label, default steps, default frames in flight at one GPU)
@@ -795,7 +795,7 @@ def main():
                         "need at peak rate.  kernel_ms: the dominant kernel's average launch one frame at a time "
                         "(HIP events on the render stream; for c4/c5 the soft-shadow traversal kernel's time per "
                         "frame from rt_context_profile's events in the timed frames).  traffic = HBM bytes per "
-                        "launch from rocprofv3 FETCH_SIZE + WRITE_SIZE passes (profiles/r03_pmc_traffic.json).",
+                        "launch from rocprofv3 FETCH_SIZE + WRITE_SIZE passes (profiles/r04_pmc_traffic.json).",
             },
             "roofline_frame": whole,
             "roofline_hbm": {
