@@ -503,7 +503,7 @@ def cpu_baseline_bvh(args, rtgo, scene, W, H, st):
 
 def pmc_traffic(workload):
     """HBM bytes per launch of the dominant kernel from the committed
-    rocprofv3 PMC passes (profiles/r03_pmc_traffic.json, scripts/pmc_traffic.py,
+    rocprofv3 PMC passes (profiles/r04_pmc_traffic.json, scripts/pmc_traffic.py,
     with the gfx950 corrections of MI355X_MICROARCH.md §HBM), if it holds this
     workload."""
     try:
