@@ -139,6 +139,9 @@ def parse():
                          "so N ranks can share one GPU (RCCL refuses two ranks on one device); --check compares "
                          "rank 0's last image with a 1-rank render")
     ap.add_argument("--check", action="store_true", help="(default at N > 1; kept for old command lines)")
+    ap.add_argument("--tuning", default="",
+                    help="rt_tuning overrides KEY=VAL[,KEY=VAL] for every context (work partition only: never "
+                         "changes an image; sweeps)")
     ap.add_argument("--no-check", action="store_true",
                     help="N > 1: skip the post-run check of the last frame against a 1-rank render")
     return ap.parse_args()
@@ -163,6 +166,8 @@ class Slot:
     def __init__(self, rtgo, torch, scene, w, h, rank, world, device, part, B):
         self.rtgo, self.w, self.h, self.rank, self.world, self.part, self.B = rtgo, w, h, rank, world, part, B
         self.ctx = rtgo.Context(device)
+        if TUNING:
+            self.ctx.set_tuning(rtgo.default_tuning(**TUNING))
         self.ctx.set_scene(scene)
         self.stream = torch.cuda.Stream(device)
         self.rendered = torch.cuda.Event()
@@ -533,8 +538,14 @@ def plan_partition(rtgo, torch, dist, scene, W, H, st, rank, world, local, strid
     return part, "balanced (pilot-estimated work, heaviest tile first to the least loaded rank)"
 
 
+TUNING = {}  # --tuning overrides (Slot contexts)
+
+
 def main():
     args = parse()
+    for kv in filter(None, args.tuning.split(",")):
+        k, _, v = kv.partition("=")
+        TUNING[k] = float(v) if "." in v else int(v)
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         # a rank keeps several launches and its gather stream in flight: more
         # hardware queues than HIP's default 4 let them run side by side
@@ -599,7 +610,7 @@ def main():
     elif world > 1:
         F, B = 3, 16
     else:
-        F, B = fif_default, 8
+        F, B = fif_default, 16
     F = args.frames_in_flight or F
     B = max(1, min(16, args.frames_per_launch or B))
     scene = load_scene(rtgo, spec)

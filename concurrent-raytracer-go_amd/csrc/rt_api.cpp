@@ -659,9 +659,19 @@ static int run_pilot(const rt_context* c, const KParams& p, SchedParams* sp, cha
 // fewer bounces make a block: silver C3 0.56 -> 0.46 ms; sphere scenes:
 // 384 since solo paths (r02, headline 0.785 -> 0.745 ms; 320: 0.755,
 // 448: 0.79, 512 was the r01 optimum)
-static double default_block_work(const rt_context* c) {
+// Blocks' estimated work (bounce-samples).  A launch of ONE frame ends when
+// its slowest block does, so its blocks are small: a long path shares its
+// wave with few others (the latency schedule).  A launch of several frames
+// (rt_context_render_frames_async) is rendered for throughput: its tail is
+// paid once for all of them and overlaps the next launch, and larger blocks
+// cost less per sample (fewer visibility passes, splits and block starts).
+// Measured (bench.py --tuning block_work=..., 2 launches of 8 frames in
+// flight, one MI355X): C2 384 -> 128.7 k, 512 135.5 k, 768 141.3 k, 1024
+// 144.8 k, 1536 143.0 k, 2048 139.9 k Mrays/s; C3 256 -> 393.9 k, 512
+// 419.8 k, 768 461.8 k, 1024 474.9 k, 2048 480.1 k.
+static double default_block_work(const rt_context* c, int frames = 1) {
   const FlatScene& f = c->flat;
-  double block_work = !f.bvh.empty() ? 8192.0 : (f.tris.empty() ? 384.0 : 256.0);
+  double block_work = !f.bvh.empty() ? 8192.0 : (frames > 1 ? 1024.0 : (f.tris.empty() ? 384.0 : 256.0));
   if (c->tun.block_work > 0) block_work = std::max(1.0, c->tun.block_work);
   return block_work;
 }
@@ -674,7 +684,7 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
   const int w = p->W, h = p->H, rank = p->rank, world = p->world;
   const rt_tuning& tn = c->tun;
   int bigP = big_block_pixels(st->samples, tn);
-  const double block_work = default_block_work(c);
+  const double block_work = default_block_work(c, frames);
   const bool pilot = tn.pilot != 0;
   // a sky makes every camera sample count (a miss returns the sky, not +0):
   // no primary-ray culling, no black tiles

@@ -211,7 +211,10 @@ def test_frames_of_one_launch_equal_single_renders(tuning):
     frame in one launch, each bit-identical to its own single render (split
     pixels included: a copy of their rows per frame); then the packed shares
     of 3 ranks of a balanced partition, 4 frames per launch, gathered as
-    [rank][frame][share] and unpacked in one launch."""
+    [rank][frame][share] and unpacked in one launch.  With the default tuning
+    the launch of 6 frames is cut into larger blocks than a single render's
+    (1024 vs 384 bounce-samples, rt_api.cpp default_block_work), so this also
+    checks that the image does not depend on the schedule."""
     import torch
 
     scene = load_case(rtgo, FACING)
