@@ -17,7 +17,7 @@ step    : one render of a whole frame with the scene and output buffers
           resident in HBM; every step renders a DIFFERENT image (seed + i).
           B consecutive steps (frames that differ only in their seed) form one
           launch (rt_context_render_frames_async; --frames-per-launch, default
-          8 for c2/c3 at one GPU, 16 per rank at N > 1), and F launches are in
+          16 for c2/c3), and F launches are in
           flight (--frames-in-flight; default 2 at one GPU, 3 at N > 1): launch
           j runs on slot j % F (own context, stream and buffers), so a frame's
           low-occupancy tail (its last 50-bounce paths) is

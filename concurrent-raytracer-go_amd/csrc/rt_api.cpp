@@ -668,10 +668,14 @@ static int run_pilot(const rt_context* c, const KParams& p, SchedParams* sp, cha
 // Measured (bench.py --tuning block_work=..., 2 launches of 8 frames in
 // flight, one MI355X): C2 384 -> 128.7 k, 512 135.5 k, 768 141.3 k, 1024
 // 144.8 k, 1536 143.0 k, 2048 139.9 k Mrays/s; C3 256 -> 393.9 k, 512
-// 419.8 k, 768 461.8 k, 1024 474.9 k, 2048 480.1 k.
+// 419.8 k, 768 461.8 k, 1024 474.9 k, 2048 480.1 k (16 frames per launch:
+// C2 896 144.4 k, 1024 146.2 k, 1280 145.4 k; C3 1024 463.7 k, 1536 476.1 k,
+// 2048 479.1 k).
 static double default_block_work(const rt_context* c, int frames = 1) {
   const FlatScene& f = c->flat;
-  double block_work = !f.bvh.empty() ? 8192.0 : (frames > 1 ? 1024.0 : (f.tris.empty() ? 384.0 : 256.0));
+  double block_work = !f.bvh.empty() ? 8192.0
+                      : frames > 1    ? (f.tris.empty() ? 1024.0 : 2048.0)
+                                      : (f.tris.empty() ? 384.0 : 256.0);
   if (c->tun.block_work > 0) block_work = std::max(1.0, c->tun.block_work);
   return block_work;
 }
@@ -1157,6 +1161,74 @@ int rt_context_set_partition(rt_context* c, const rt_partition* p) {
 // each tile's estimated work (spp x the sum of its pixels' estimates,
 // sched_tile_work), then longest-processing-time-first: tiles by decreasing
 // work (ties: lower tile first) to the least loaded rank (ties: lower rank).
+// The measured work of every tile of the frame (r04): the frame rendered
+// once at its full sample count through the context's own (one-rank)
+// schedule, with the measuring instantiation recording every sample's path
+// length; a tile weighs the sum of its pixels' mean path lengths x spp.  The
+// one-sample pilot's estimate (the neighbourhood's longest path, which the
+// block cutting wants) misjudges whole tiles: with it the slowest of 8 ranks
+// of the headline frame took 1.22x the mean share.  Path lengths are
+// integers of an exact render, so every rank that measures the same frame on
+// its own device derives the same partition.
+static int measured_tile_work(rt_context* c, int w, int h, const rt_settings* st, std::vector<float>* work) {
+  hipStream_t s = c->stream;
+  KParams p;
+  base_params(c, w, h, st, 0, 1, RT_LAYOUT_PACKED_TILES, &p);
+  p.spp = st->samples;
+  p.spp_total = st->samples;
+  p.sample_base = 0;
+  p.acc_mode = 0;
+  p.acc = nullptr;
+  p.counts = nullptr;
+  int rc = prepare_schedule(c, &p, st, s);
+  if (rc) return rc;
+  p.num_wgs = p.num_blocks;
+  const int ntiles = rt_num_tiles(w, h);
+  const size_t npx = (size_t)ntiles * 1024;
+  std::vector<int32_t> tiles;
+  strided_tiles(w, h, 0, 1, &tiles);
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t o_meas = al(npx * 16);  // [linear | rgba] image, packed tiles
+  const size_t o_sched = o_meas + al(npx * 8);
+  const size_t o_tw = o_sched + al(sched_scratch_bytes(ntiles));
+  const size_t total = o_tw + al((size_t)ntiles * sizeof(float));
+  char* buf = nullptr;
+  HIP_TRY((hipError_t)dev_alloc((void**)&buf, total));
+  auto done = [&](int code) {
+    (void)hipStreamSynchronize(s);
+    dev_free(buf);
+    return code;
+  };
+  p.out_linear = (float*)buf;
+  p.out_rgba = (uint8_t*)(buf + npx * 12);
+  unsigned int* meas = (unsigned int*)(buf + o_meas);
+  p.work_max = meas;
+  p.work_sum = meas + npx;
+  if (hipMemsetAsync(meas, 0, npx * 8, s) != hipSuccess) return done(RT_E_DEVICE);
+  if (p.num_blocks > 0) {
+    const int e = launch_render(p, false, s);
+    if (e != hipSuccess) {
+      set_error(std::string("partition measuring launch failed: ") + hipGetErrorString((hipError_t)e));
+      return done(RT_E_DEVICE);
+    }
+  }
+  SchedParams sp = sched_params(c, p, st, tiles, nullptr, false, false, default_block_work(c),
+                                big_block_pixels(st->samples, c->tun), buf + o_sched, nullptr, nullptr);
+  sp.work_max = meas;
+  sp.work_sum = meas + npx;
+  sp.work_n = st->samples;
+  sp.split_depth = 1 << 30;  // (weights only: no pixel is marked heavy)
+  float* d_tw = (float*)(buf + o_tw);
+  int e = sched_launch_tile_work(sp, d_tw, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(work->data(), d_tw, (size_t)ntiles * sizeof(float), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    set_error(std::string("partition measurement failed: ") + hipGetErrorString((hipError_t)e));
+    return done(RT_E_DEVICE);
+  }
+  return done(RT_OK);
+}
+
 int rt_partition_balanced(rt_context* c, int32_t w, int32_t h, const rt_settings* st, int32_t world,
                           rt_partition** out) {
   if (!c || !c->have_scene || !out) {
@@ -1175,6 +1247,20 @@ int rt_partition_balanced(rt_context* c, int32_t w, int32_t h, const rt_settings
   const rt_tuning& tn = c->tun;
   hipStream_t s = c->stream;
   const int ntiles = rt_num_tiles(w, h);
+  if (tn.pilot != 0 && !use_wavefront(c) && st->sky == RT_SKY_NONE && st->samples > 0 &&
+      st->samples <= kMaxBlockSamples && st->max_depth > 0) {
+    std::vector<float> work(ntiles, 0.0f);
+    rc = measured_tile_work(c, w, h, st, &work);
+    if (rc) return rc;
+    PartitionData d;
+    d.w = w;
+    d.h = h;
+    d.world = world;
+    lpt_partition(work, &d);
+    finish_partition(&d);
+    *out = make_partition(std::move(d));
+    return RT_OK;
+  }
   std::vector<int32_t> tiles;
   strided_tiles(w, h, 0, 1, &tiles);
   KParams p;

@@ -298,7 +298,7 @@ typedef struct {
   int32_t frustum;        /* 1: primary-ray candidate masks (cull, black tiles) */
   int32_t stage;          /* 1: small scenes staged into LDS */
   double block_work;      /* path bounces x samples per block; 0: default (one frame per launch: 384, 256 with
-                             triangles; several frames per launch: 1024; BVH scenes 8192) */
+                             triangles; several frames per launch: 1024, 2048 with triangles; BVH scenes 8192) */
   int32_t block_samples;  /* pixels x samples of a large block at most; 0: 1024 */
   int32_t bvh_bins;       /* SAH bins per axis; 0: 32 */
   int32_t bvh_leaf;       /* spheres per BVH leaf at most (1..7); 0: 4 */

@@ -9,8 +9,9 @@ The N-GPU step cannot finish before its slowest rank, so
 (the RCCL gather of ~1/N of 7.7 MB per frame and the unpack kernel come on
 top; they run on a separate stream, overlapped with the next frames).
 
-usage: rank_share_probe.py [N ...] [--fif F ...] [--batch B ...] [--steps K] [--strided]
-(--batch: B frames per launch, rt_context_render_frames_async; F launches in flight)
+usage: rank_share_probe.py [N ...] [--fif F ...] [--batch B ...] [--block-work X ...] [--steps K] [--strided]
+(--batch: B frames per launch, rt_context_render_frames_async; F launches in flight;
+--block-work: rt_tuning.block_work, 0 = the library's default)
 """
 import argparse
 import json
@@ -28,6 +29,7 @@ def main():
     ap.add_argument("worlds", type=int, nargs="*", default=[2, 4, 8])
     ap.add_argument("--fif", type=int, nargs="*", default=[1, 2, 4, 8])
     ap.add_argument("--batch", type=int, nargs="*", default=[1])
+    ap.add_argument("--block-work", type=float, nargs="*", default=[0.0])
     ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--strided", action="store_true")
     ap.add_argument("--scene", default="sphere_reflections_light_facing.json")
@@ -52,8 +54,8 @@ def main():
         ctx.set_scene(scene)
         part = rtgo.Partition(W, H, world) if args.strided else ctx.balanced_partition(W, H, settings(1), world)
         ctx.close()
-        for F in args.fif:
-            for B in args.batch:
+        for F, B, bw in [(F, B, bw) for F in args.fif for B in args.batch for bw in args.block_work]:
+            if True:
                 per_rank = []
                 nb = part.packed_bytes
                 launches = max(1, args.steps // B)
@@ -61,6 +63,7 @@ def main():
                     slots = []
                     for _ in range(F):
                         c = rtgo.Context(0)
+                        c.set_tuning(rtgo.default_tuning(block_work=bw))
                         c.set_scene(scene)
                         c.set_partition(part)
                         buf = torch.zeros(B * nb, dtype=torch.uint8, device="cuda")
@@ -86,6 +89,7 @@ def main():
                         c.close()
                 worst = max(r["ms_per_frame"] for r in per_rank)
                 res = {"world": world, "partition": "strided" if args.strided else "balanced", "fif": F, "batch": B,
+                       "block_work": bw or "default",
                        "worst_ms": worst, "predicted_mrays": round(W * H * args.spp / worst / 1e3, 1),
                        "ranks": per_rank}
                 out["results"].append(res)
