@@ -798,6 +798,11 @@ def main():
                 "kernel": KERNELS[cfg],
                 "kernel_ms": round(kern_s * 1e3, 4),
                 "kernel_ms_frames_in_flight": round(kernelF_s * 1e3, 4) if cfg not in WAVEFRONT else None,
+                # the same frame's executed flops over the bench's own time per frame
+                # (value's frames in flight: launches overlap, so no single launch shows it)
+                "frac_in_flight": (round(f64 / (elapsed / steps) / 1e12 / PEAK_FP64_TFLOPS
+                                         + f32 / (elapsed / steps) / 1e12 / PEAK_FP32_TFLOPS, 5)
+                                   if cfg not in WAVEFRONT and world == 1 else None),
                 "note": "FP64 VALU-bound branchy path (binary64 like the Go reference; no matrix shape, no MFMA). "
                         "EXECUTED work only: the counting variant's counts minus rt_counts.culled (the camera "
                         "samples of culled pixels it walks only to report the reference's counts), x DESIGN.md "
@@ -805,7 +810,8 @@ def main():
                         "(157.3 TF): frac = frac_fp64 + frac_fp32, the share of the kernel's time the VALU would "
                         "need at peak rate.  kernel_ms: the dominant kernel's average launch one frame at a time "
                         "(HIP events on the render stream; for c4/c5 the soft-shadow traversal kernel's time per "
-                        "frame from rt_context_profile's events in the timed frames).  traffic = HBM bytes per "
+                        "frame from rt_context_profile's events in the timed frames); frac_in_flight: the frame's flops over "
+                        "ms_per_step (the throughput line's time per frame).  traffic = HBM bytes per "
                         "launch from rocprofv3 FETCH_SIZE + WRITE_SIZE passes (profiles/r04_pmc_traffic.json).",
             },
             "roofline_frame": whole,
