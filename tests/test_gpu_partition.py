@@ -1,8 +1,9 @@
 """GPU: tile partitions across ranks, the counting variant's culled share,
 per-kernel timing, and the advisor's round-2 edge cases.
 
-* A work-balanced partition (rt_partition_balanced: a whole-frame pilot,
-  tiles dealt heaviest first to the least loaded rank) of the headline frame
+* A work-balanced partition (rt_partition_balanced: every tile's work
+  measured by one whole-frame render, tiles dealt heaviest first to the
+  least loaded rank) of the headline frame
   (BASELINE configs[1]: sphere_reflections_light facing, 800x600x100, depth 50)
   over 8 ranks, rendered rank by rank on device 0 and unpacked, equals the
   1-rank image bit for bit; so does rt_renderer with 8 ranks on device 0
@@ -257,3 +258,30 @@ def test_frames_of_one_launch_equal_single_renders(tuning):
     part.unpack_frames_async(nf, g.data_ptr(), img_lin.data_ptr(), img_rgba.data_ptr())
     torch.cuda.synchronize()
     assert torch.equal(img_lin.view(nf, -1), lin[:nf]) and torch.equal(img_rgba.view(nf, -1), rgba[:nf])
+
+
+def test_batched_triangle_frames_equal_single_renders():
+    """The silver prism / purple cube scene (BASELINE C3: triangles, the
+    batched schedule cuts 2048 bounce-samples per block against 256 for one
+    frame, rt_api.cpp default_block_work): 3 frames of one launch, each
+    bit-identical to its own single render, whose parity with the oracle the
+    full-size tests pin."""
+    import torch
+
+    scene = load_case(rtgo, ("file", "final_silver_prism_purple_cube_facing.json"))
+    w, h, spp = 600, 450, 32
+    st = make_settings(rtgo, {"samples": spp, "max_depth": 50}, seed=1)
+    seeds = [21, 22, 23]
+    ctx = rtgo.Context(0)
+    ctx.set_scene(scene)
+    lin = torch.zeros((len(seeds), w * h * 3), dtype=torch.float32, device="cuda")
+    rgba = torch.zeros((len(seeds), w * h * 4), dtype=torch.uint8, device="cuda")
+    ctx.render_frames_async(w, h, st, seeds, [lin[f].data_ptr() for f in range(len(seeds))],
+                            [rgba[f].data_ptr() for f in range(len(seeds))])
+    torch.cuda.synchronize()
+    ctx.close()
+    for f, sd in enumerate(seeds):
+        ref_lin, ref_rgba, _, _ = render_dev(scene, w, h, make_settings(rtgo, {"samples": spp, "max_depth": 50},
+                                                                        seed=sd))
+        assert lin[f].cpu().numpy().tobytes() == ref_lin.tobytes(), f
+        assert rgba[f].cpu().numpy().tobytes() == ref_rgba.tobytes(), f
