@@ -368,18 +368,29 @@ __device__ __forceinline__ const DSphere& leaf_sphere(const DSphere* sp, const D
 struct JobSrc {
   int next, hi;  // the current chunk
   int tried;     // ranges found empty
+  int chunk;     // jobs per atomic (job_chunk)
 };
+// Jobs a wave takes per atomic: kChunk while the launch has plenty (a
+// persistent launch drains faster when no wave holds many unstarted jobs,
+// but every atomic costs), fewer when it has fewer jobs than waves x kChunk
+// -- the frame's last bounce iterations, where a few thousand long paths
+// would otherwise queue on a few dozen waves -- down to kMinChunk.
+constexpr int kMinChunk = 16;
+__device__ __forceinline__ JobSrc job_src(int n) {
+  const int waves = (int)(gridDim.x * (blockDim.x >> 6));
+  return JobSrc{0, 0, 0, min(kChunk, max(kMinChunk, n / max(1, waves)))};
+}
 __device__ __forceinline__ bool job_refill(JobSrc& js, int32_t* heads, int n) {
   const int home = blockIdx.x % kWfShards;
   while (js.tried < kWfShards) {
     const int s = (home + js.tried) % kWfShards;
     const int lo_s = (int)((long long)n * s / kWfShards), hi_s = (int)((long long)n * (s + 1) / kWfShards);
     int got = 0;
-    if ((threadIdx.x & 63) == 0) got = atomicAdd(&heads[s * 32], kChunk);
+    if ((threadIdx.x & 63) == 0) got = atomicAdd(&heads[s * 32], js.chunk);
     got = __builtin_amdgcn_readfirstlane(got);
     if (lo_s + got < hi_s) {
       js.next = lo_s + got;
-      js.hi = min(hi_s, js.next + kChunk);
+      js.hi = min(hi_s, js.next + js.chunk);
       return true;
     }
     ++js.tried;
@@ -399,7 +410,7 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
   const int n = dn.start[kWfShards];
   if (n == 0) return;
   lds_node* lt = stage_tree(p);
-  JobSrc js{0, 0, 0};
+  JobSrc js = job_src(n);
   bool more = true;  // wave-uniform: jobs may remain
   Counters c;
   if constexpr (kCount)
@@ -586,7 +597,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
   const int n = dn.start[kWfShards];
   if (n == 0) return;
   lds_node* lt = stage_tree(p);
-  JobSrc js{0, 0, 0};
+  JobSrc js = job_src(n);
   bool more = true;  // wave-uniform: jobs may remain
   Counters c;
   if constexpr (kCount)
@@ -847,7 +858,7 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
   const int n = dn.start[kWfShards];
   if (n == 0) return;
   lds_node* lt = stage_tree(p);
-  JobSrc js{0, 0, 0};
+  JobSrc js = job_src(n);
   bool more = true;  // wave-uniform: jobs may remain
   Counters c;
   if constexpr (kCount)
