@@ -583,14 +583,15 @@ class ParallelRenderer:
             "depthOfField": bool(s.depth_of_field),
         }
 
-    def render(self, scene: Scene, width: int, height: int) -> np.ndarray:
+    def render(self, scene: Scene, width: int, height: int, keep_linear: bool = True) -> np.ndarray:
         """Render (renderer.go:67-126): returns an (H, W, 4) uint8 RGBA image.
 
         The mean linear radiance (before tone mapping) is kept in
-        ``self.last_linear`` as an (H, W, 3) float32 array.
+        ``self.last_linear`` as an (H, W, 3) float32 array; keep_linear=False
+        skips it (None), as Go's Render returns the RGBA image only.
         """
         _check(lib().rt_validate(ctypes.byref(scene.view), width, height, ctypes.byref(self.settings)))
-        lin = np.zeros((height, width, 3), np.float32)
+        lin = np.zeros((height, width, 3), np.float32) if keep_linear else None
         rgba = np.zeros((height, width, 4), np.uint8)
         st = Stats()
         _check(
@@ -600,7 +601,7 @@ class ParallelRenderer:
                 width,
                 height,
                 ctypes.byref(self.settings),
-                lin.ctypes.data,
+                lin.ctypes.data if lin is not None else None,
                 rgba.ctypes.data,
                 ctypes.byref(st),
             )

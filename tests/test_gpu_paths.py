@@ -90,6 +90,26 @@ def test_renderer_multi_rank_equals_one_rank(devices):
     r.close()
 
 
+@pytest.mark.parametrize("size", [(80, 48), (75, 50)], ids=["16B_multiple", "ragged"])
+def test_renderer_rgba_only_equals_full_render(size):
+    """Render without the float3 image (out_linear_rgb NULL: Go's Render
+    returns the RGBA image only, renderer.go:67), on a new renderer's first
+    call (its image goes down through the download kernel when the sizes are
+    multiples of 16 B) and on a later call (a copy from the idle stream):
+    the same RGBA bytes as the full render."""
+    scene = load_case(rtgo, ("json", None))
+    w, h = size
+    r = rtgo.ParallelRenderer()
+    for seed in (3, 4):
+        st = make_settings(rtgo, {"samples": 3}, seed=seed)
+        _, ref_rgba = _gpu(scene, w, h, st)
+        r.settings = make_settings(rtgo, {"samples": 3}, seed=seed)
+        rgba = r.render(scene, w, h, keep_linear=False)
+        assert r.last_linear is None
+        assert rgba.tobytes() == ref_rgba.tobytes()
+    r.close()
+
+
 def test_renderer_ranks_drive_bvh_frames_concurrently():
     """A BVH scene runs the wavefront path, whose host loop returns only when
     the frame is done; rt_renderer_render drives each rank from its own
