@@ -527,8 +527,8 @@ def pmc_traffic(workload):
 
 def plan_partition(rtgo, torch, dist, scene, W, H, st, rank, world, local, strided):
     """The frame's tile partition, and the same on every rank: balanced
-    (planned by every rank from the same deterministic pilot, checked by
-    comparing digests) or strided."""
+    (planned by every rank from the same deterministic measuring render,
+    rt_partition_balanced; checked by comparing digests) or strided."""
     if strided:
         return rtgo.Partition(W, H, world), "strided t % N"
     ctx = rtgo.Context(local)
@@ -540,7 +540,7 @@ def plan_partition(rtgo, torch, dist, scene, W, H, st, rank, world, local, strid
     dist.all_gather_object(allg, digest)
     if len(set(allg)) != 1:
         raise SystemExit(f"rank {rank}: balanced partitions differ across ranks: {allg}")
-    return part, "balanced (pilot-estimated work, heaviest tile first to the least loaded rank)"
+    return part, "balanced (measured work per tile, heaviest tile first to the least loaded rank)"
 
 
 TUNING = {}  # --tuning overrides (Slot contexts)

@@ -395,11 +395,13 @@ int rt_comm_gather_tiles_async(rt_comm* comm, int32_t width, int32_t height, con
  * separate GPUs share no queue: each renders a fixed set of tiles.  The
  * default set is strided (t % world == rank).  A frame whose work sits in a
  * few tiles (the headline scene: 23 of its 475 tiles hold all the shading)
- * is better dealt by estimated work: rt_partition_balanced renders a
- * one-sample pilot of the whole frame on ctx's device (the schedule's pilot,
- * DESIGN.md §4.1), sums each tile's estimated path work and deals the tiles
- * heaviest first to the least loaded rank.  The pilot is deterministic, so
- * every rank that plans the same frame derives the same partition.  Every
+ * is better dealt by work: rt_partition_balanced renders the whole frame
+ * once on ctx's device with every sample's path length recorded (DESIGN.md
+ * §5; frames with more than 1024 samples, a sky or a BVH: the schedule's
+ * one-sample pilot estimate instead), sums each tile's path work and deals
+ * the tiles heaviest first to the least loaded rank.  Both are
+ * deterministic, so every rank that plans the same frame derives the same
+ * partition.  Every
  * pixel stays on one rank and the random stream is keyed by global pixel and
  * sample: the image is the same for every partition.
  * A rank's packed share holds its tiles in ascending order (local tile lt =
@@ -418,7 +420,7 @@ int32_t rt_partition_tile(const rt_partition* p, int32_t rank, int32_t local); /
 int32_t rt_partition_max_local(const rt_partition* p);
 size_t rt_partition_packed_bytes(const rt_partition* p);  /* one share: max_local * 1024 * 16 */
 size_t rt_partition_rgba_offset(const rt_partition* p);   /* max_local * 1024 * 12 */
-/* Estimated work of rank's tiles (pilot path bounces x samples; balanced partitions, else 0). */
+/* Work of rank's tiles (path bounces summed over samples; balanced partitions, else 0). */
 double rt_partition_work(const rt_partition* p, int32_t rank);
 /* Later renders of ctx with the partition's (W, H, world) render rank's tiles
  * of it (packed: in its order); NULL (or other sizes): strided.  The
