@@ -142,6 +142,12 @@ def parse():
     ap.add_argument("--tuning", default="",
                     help="rt_tuning overrides KEY=VAL[,KEY=VAL] for every context (work partition only: never "
                          "changes an image; sweeps)")
+    ap.add_argument("--watchdog", type=float, default=120.0,
+                    help="N > 1: a rank's blocking wait (a launch, a gather, a barrier) that has not completed in "
+                         "this many seconds prints the rank, step and partition and exits with status 3 "
+                         "(rtgo/watchdog.py; <= 0: unbounded)")
+    ap.add_argument("--withhold-rank", type=int, default=-1,
+                    help="TEST MODE with --host-gather: this rank never joins the gathers (the watchdog must fire)")
     ap.add_argument("--no-check", action="store_true",
                     help="N > 1: skip the post-run check of the last frame against a 1-rank render")
     return ap.parse_args()
@@ -248,10 +254,13 @@ class HostGather:
         self.dist, self.rank, self.world = dist, rank, world
 
     def gather(self, torch, slot, gstream, nbytes):
+        from rtgo.watchdog import host_gather
+
         with torch.cuda.stream(gstream):
             host = slot.share[:nbytes].cpu()
-        parts = [torch.empty_like(host) for _ in range(self.world)] if self.rank == 0 else None
-        self.dist.gather(host, parts, dst=0)
+        if self.rank == WITHHOLD:  # test mode: this rank never sends (the others' watchdogs must fire)
+            return
+        parts = host_gather(self.dist, host, self.rank, self.world)
         if self.rank == 0:
             with torch.cuda.stream(gstream):
                 for r in range(1, self.world):
@@ -261,24 +270,51 @@ class HostGather:
         pass
 
 
-def barrier_sync(torch, dist, world):
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+def barrier_sync(torch, dist, world, phase="barrier", **info):
+    with WD.guard(phase, **info):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
 
 
 def max_over_ranks(torch, dist, world, x):
     if world == 1:
         return x
     t = torch.tensor([x], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)  # gloo (host): the device data path is RCCL's only
+    with WD.guard("max over ranks", step="report", partition=PART_INFO):
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # gloo (host): the device data path is RCCL's only
     return float(t.item())
 
 
 def launches(sts, B):
-    """The K steps as launches of up to B consecutive frames."""
-    return [sts[i:i + B] for i in range(0, len(sts), B)]
+    """The K steps as ceil(K / B) launches of consecutive frames, of near-equal
+    size (20 steps at B = 16: 10 + 10, not 16 + 4), so a launch's tail is
+    spread evenly and the line does not depend on K mod B."""
+    n = len(sts)
+    k = -(-n // B) if n else 0
+    out, i = [], 0
+    for j in range(k):
+        m = -(-(n - i) // (k - j))
+        out.append(sts[i:i + m])
+        i += m
+    return out
+
+
+def busy_ms(spans):
+    """Union length (ms) of [start, end) intervals: the time at least one
+    launch of the timed region was running (launches in flight overlap)."""
+    tot, cur_s, cur_e = 0.0, None, None
+    for a, b in sorted(spans):
+        if cur_e is None or a > cur_e:
+            if cur_e is not None:
+                tot += cur_e - cur_s
+            cur_s, cur_e = a, b
+        else:
+            cur_e = max(cur_e, b)
+    if cur_e is not None:
+        tot += cur_e - cur_s
+    return tot
 
 
 def time_steps(slots, torch, dist, world, sts, warmup, comm, gstream, B):
@@ -290,11 +326,14 @@ def time_steps(slots, torch, dist, world, sts, warmup, comm, gstream, B):
     F = len(slots)
     for j, batch in enumerate(launches([sts[i % len(sts)] for i in range(warmup)], B)):
         sl = slots[j % F]
-        sl.render(batch)
-        sl.gather(torch, comm, gstream)
-    barrier_sync(torch, dist, world)
+        with WD.guard("warm-up launch", step=f"warm-up launch {j}", partition=PART_INFO):
+            sl.render(batch)
+            sl.gather(torch, comm, gstream)
+    barrier_sync(torch, dist, world, "warm-up barrier", step="after warm-up", partition=PART_INFO)
     evs = []
+    ref = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ref.record()
     for j, batch in enumerate(launches(sts, B)):
         sl = slots[j % F]
         e0 = torch.cuda.Event(enable_timing=True)
@@ -302,13 +341,21 @@ def time_steps(slots, torch, dist, world, sts, warmup, comm, gstream, B):
         if sl.gathered is not None:
             sl.stream.wait_event(sl.gathered)
         e0.record(sl.stream)
-        sl.render(batch)
-        e1.record(sl.stream)
-        evs.append((e0, e1, len(batch)))
-        sl.gather(torch, comm, gstream)
-    barrier_sync(torch, dist, world)
+        with WD.guard("timed launch", step=f"launch {j}: steps of seeds {batch[0].seed}..{batch[-1].seed}",
+                      partition=PART_INFO):
+            sl.render(batch)
+            e1.record(sl.stream)
+            evs.append((e0, e1, len(batch)))
+            sl.gather(torch, comm, gstream)
+    barrier_sync(torch, dist, world, "timed-region barrier (every launch and gather enqueued)",
+                 step=f"after {len(evs)} timed launches", partition=PART_INFO)
     elapsed = max_over_ranks(torch, dist, world, time.perf_counter() - t0)
-    return elapsed, [a.elapsed_time(b) / n for a, b, n in evs]
+    # per-frame kernel time of each launch, and the union of the launches'
+    # spans (ms) over the frames: launches in flight overlap, so a launch's
+    # own span over its frames over-states the GPU time per frame
+    spans = [(ref.elapsed_time(a), ref.elapsed_time(b)) for a, b, _ in evs]
+    busy = busy_ms(spans) / max(1, sum(n for _, _, n in evs))
+    return elapsed, [a.elapsed_time(b) / n for a, b, n in evs], busy
 
 
 def first_frame_ms(rtgo, torch, scene, W, H, st, local):
@@ -413,13 +460,36 @@ def cpu_count_info():
 
 
 def cpu_time(oracle, scene, W, H, st, threads, runs=3):
+    """Median seconds of `runs` oracle renders (after a short warm-up), and
+    the last render's (linear, rgba) image."""
     oracle.render(scene, W, H, st, nthreads=threads, max_tiles=min(16, 2 * threads))  # warm-up
-    times = []
+    times, img = [], None
     for _ in range(runs):
         t0 = time.perf_counter()
-        oracle.render(scene, W, H, st, nthreads=threads)
+        img = oracle.render(scene, W, H, st, nthreads=threads)[:2]
         times.append(time.perf_counter() - t0)
-    return sorted(times)[len(times) // 2]
+    return sorted(times)[len(times) // 2], img
+
+
+def oracle_check(cf, ref, W, H):
+    """The GPU frame cf (bench's check frame) against the oracle's render of
+    the same settings, bit for bit: float3 linear (the oracle's binary64
+    rounded to binary32, as the kernel writes it) and RGBA8, over the pixels
+    the oracle rendered (a tile sample leaves the others NaN)."""
+    import numpy as np
+
+    ref_lin, ref_rgba = ref
+    g = cf["lin"].reshape(H, W, 3)
+    m = ~np.isnan(ref_lin).any(axis=2)
+    r32 = ref_lin.astype(np.float32)
+    same_lin = np.array_equal(g[m].view(np.uint32), r32[m].view(np.uint32))
+    same_rgba = np.array_equal(cf["rgba"].reshape(H, W, 4)[m], ref_rgba[m])
+    d = g[m].astype(np.float64) - r32[m].astype(np.float64)
+    return bool(same_lin and same_rgba), {
+        "pixels_compared": int(m.sum()),
+        "rmse_max_channel": float(np.sqrt(np.mean(d ** 2, axis=0)).max()) if d.size else 0.0,
+        "max_abs_diff": float(np.abs(d).max()) if d.size else 0.0,
+    }
 
 
 def cpu_baseline(args, rtgo, scene, W, H, st, cfg):
@@ -445,38 +515,55 @@ def cpu_baseline(args, rtgo, scene, W, H, st, cfg):
         rays = ntl * 1024 * spp
         sample = (f"{ntl} tiles (every {world}th tile from tile 0) of the {W}x{H} frame at {spp} spp, depth "
                   f"{st.max_depth}, one run ({secs:.1f} s), scaled per primary sample")
+        img = None
+        other = None
     else:
-        secs = cpu_time(oracle, scene, W, H, st, threads)
+        # the frame bench.py checks (its seed), timed on NumCPU() threads and
+        # on the box's per-GPU CPU share (16 threads, the cgroup's quota): the
+        # faster of the two is the baseline, the other is reported beside it
+        secs, img = cpu_time(oracle, scene, W, H, st, threads)
         rays = W * H * st.samples
-        sample = f"full {W}x{H}x{st.samples}spp frame, median of 3 runs ({secs:.3f} s) after 1 warm-up"
-    return {
+        sample = f"full {W}x{H}x{st.samples}spp frame (seed {st.seed}), median of 3 runs ({secs:.3f} s) after 1 warm-up"
+        other = None
+        if threads != 16:
+            secs16, _ = cpu_time(oracle, scene, W, H, st, 16)
+            other = {"value": round(rays / secs16 / 1e6, 3), "unit": "Mrays/s", "cores": 16,
+                     "sample": f"the same frame on 16 threads, median of 3 ({secs16:.3f} s)"}
+            if secs16 < secs:
+                other, secs, threads = ({"value": round(rays / secs / 1e6, 3), "unit": "Mrays/s", "cores": threads,
+                                         "sample": f"the same frame on {threads} threads = runtime.NumCPU(), median "
+                                                   f"of 3 ({secs:.3f} s)"}, secs16, 16)
+                sample = (f"full {W}x{H}x{st.samples}spp frame (seed {st.seed}), median of 3 runs ({secs:.3f} s) "
+                          f"after 1 warm-up")
+    out = {
         "value": round(rays / secs / 1e6, 3),
         "unit": "Mrays/s",
         "cores": threads,
         "host_cpus": {"affinity": aff, "os_cpu_count": os.cpu_count(), "cgroup_cpu_quota": quota},
         "kind": "port",
-        "sample": sample + f"; oracle/oracle.c on {threads} threads = runtime.NumCPU() (the affinity count, "
-                           f"cmd/raytracer/main.go:46) on the tile queue of renderer.go:67-148; the Go toolchain "
-                           f"is absent (SURVEY.md §8c)" + (f"; the cgroup grants {quota} CPUs of time" if quota else ""),
+        "sample": sample + f"; oracle/oracle.c on {threads} threads on the tile queue of renderer.go:67-148 "
+                           + (f"(the faster of runtime.NumCPU() = {aff} threads, cmd/raytracer/main.go:46, and 16 "
+                              f"threads; every ratio in this line divides by this value)" if other else
+                              "(runtime.NumCPU(), cmd/raytracer/main.go:46)")
+                           + "; the Go toolchain is absent (SURVEY.md §8c)"
+                           + (f"; the cgroup grants {quota} CPUs of time" if quota else ""),
     }
+    if other:
+        out["other_thread_count"] = other
+    return out, img
 
 
 def cpu_secondary(args, rtgo, scene, W, H, st, cfg):
-    """Labelled secondary CPU figures: the same frame on 16 threads (the
-    box's per-GPU CPU share), and the as-committed C1 scene (BASELINE
+    """Labelled secondary CPU figure: the as-committed C1 scene (BASELINE
     configs[0]) on NumCPU threads."""
     import oracle
 
     aff, _ = cpu_count_info()
     out = {}
-    if cfg not in WAVEFRONT and aff != 16:
-        secs = cpu_time(oracle, scene, W, H, st, 16)
-        out["cpu_16_threads"] = {"value": round(W * H * st.samples / secs / 1e6, 3), "unit": "Mrays/s",
-                                 "cores": 16, "sample": f"the same frame on 16 threads, median of 3 ({secs:.3f} s)"}
     if cfg == "c2":
         c1 = rtgo.Scene.load_from_file(os.path.join(ROOT, "scenes", "sphere_reflections_light.json"))
         threads = args.cpu_threads or aff
-        secs = cpu_time(oracle, c1, W, H, st, threads)
+        secs, _ = cpu_time(oracle, c1, W, H, st, threads)
         out["cpu_c1_as_committed"] = {
             "value": round(W * H * st.samples / secs / 1e6, 3), "unit": "Mrays/s", "cores": threads,
             "sample": f"BASELINE configs[0]: sphere_reflections_light.json as committed (every camera ray misses, "
@@ -497,10 +584,10 @@ def cpu_baseline_bvh(args, rtgo, scene, W, H, st):
     ntl = min(n_tiles, 32)
     world = max(1, n_tiles // ntl)
     t0 = time.perf_counter()
-    oracle.render(scene, W, H, st, rank=0, world=world, nthreads=threads, max_tiles=ntl, bvh=True)
+    img = oracle.render(scene, W, H, st, rank=0, world=world, nthreads=threads, max_tiles=ntl, bvh=True)[:2]
     secs = time.perf_counter() - t0
     rays = ntl * 1024 * st.samples
-    return {
+    return img, {
         "value": round(rays / secs / 1e6, 3),
         "unit": "Mrays/s",
         "cores": threads,
@@ -544,6 +631,9 @@ def plan_partition(rtgo, torch, dist, scene, W, H, st, rank, world, local, strid
 
 
 TUNING = {}  # --tuning overrides (Slot contexts)
+WD = None  # the rank's Watchdog (rtgo/watchdog.py; unbounded at N = 1)
+PART_INFO = None  # this rank's partition, for the watchdog's report
+WITHHOLD = -1  # --withhold-rank (test mode)
 
 
 def main():
@@ -561,9 +651,16 @@ def main():
 
     import rtgo
 
+    from rtgo.watchdog import Watchdog
+
+    global WD, PART_INFO, WITHHOLD
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    WD = Watchdog(args.watchdog if world > 1 else 0, rank)
+    if args.withhold_rank >= 0 and not args.host_gather:
+        raise SystemExit("--withhold-rank is a --host-gather test mode")
+    WITHHOLD = args.withhold_rank
     if world != args.gpus:
         print(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes (WORLD_SIZE={world})",
               file=sys.stderr)
@@ -583,7 +680,8 @@ def main():
         os.dup2(2, 1)
         try:
             dist.init_process_group("gloo")
-            dist.barrier()
+            with WD.guard("process-group start", step="init"):
+                dist.barrier()
         finally:
             sys.stdout.flush()
             os.dup2(saved, 1)
@@ -617,7 +715,7 @@ def main():
     else:
         F, B = fif_default, 16
     F = args.frames_in_flight or F
-    B = max(1, min(16, args.frames_per_launch or B))
+    B = max(1, min(rtgo.RT_MAX_FRAMES, args.frames_per_launch or B))
     scene = load_scene(rtgo, spec)
 
     comm = gstream = part = None
@@ -630,29 +728,46 @@ def main():
             dist.broadcast_object_list(uid, src=0)
             comm = rtgo.Comm(uid[0], world, rank, local)
         gstream = torch.cuda.Stream(local)
-        part, part_kind = plan_partition(rtgo, torch, dist, scene, W, H, sts[0], rank, world, local,
-                                         args.strided or cfg in WAVEFRONT)
+        with WD.guard("partition planning", step="set-up"):
+            part, part_kind = plan_partition(rtgo, torch, dist, scene, W, H, sts[0], rank, world, local,
+                                             args.strided or cfg in WAVEFRONT)
+        PART_INFO = f"{part_kind.split(' (')[0]}, {part.local_tiles(rank)} of {rtgo.num_tiles(W, H)} tiles on rank {rank}"
 
     slots = []
-    for _ in range(F):  # F launches in flight: own context (schedule), stream and buffers each
+    for i in range(F):  # F launches in flight: own context (schedule), stream and buffers each
         sl = Slot(rtgo, torch, scene, W, H, rank, world, local, part, B)
-        sl.render(sts[:B])  # set-up: builds this context's schedule (like the scene upload)
-        sl.gather(torch, comm, gstream)
+        with WD.guard("set-up launch", step=f"slot {i} set-up", partition=PART_INFO):
+            sl.render(sts[:B])  # set-up: builds this context's schedule (like the scene upload)
+            sl.gather(torch, comm, gstream)
         slots.append(sl)
-    barrier_sync(torch, dist, world)
-    counts = slots[0].counts(sts[0])  # algorithmic work of this rank's launch (counting variant, untimed)
-    barrier_sync(torch, dist, world)
+    barrier_sync(torch, dist, world, "set-up barrier", step="set-up", partition=PART_INFO)
+    with WD.guard("counting launch", step="counts", partition=PART_INFO):
+        counts = slots[0].counts(sts[0])  # algorithmic work of this rank's launch (counting variant, untimed)
+    barrier_sync(torch, dist, world, "counting barrier", step="counts", partition=PART_INFO)
     prof_ctx = slots[0].ctx if cfg in WAVEFRONT else None
     if prof_ctx is not None:
         prof_ctx.profile(True)  # per-kernel HIP events in the timed frames (F = 1: every frame on slot 0)
-    elapsed, kms = time_steps(slots, torch, dist, world, sts, args.warmup, comm, gstream, B)
+    elapsed, kms, busy_frame_ms = time_steps(slots, torch, dist, world, sts, args.warmup, comm, gstream, B)
+    plan = launches(sts, B)
+    check_frame = None
+    if world == 1:
+        # the frame the oracle checks (check_equals_oracle): one from the last
+        # launch that ran on the second slot (the first when F = 1), from the
+        # middle of that launch, copied now (later timings reuse slot 0)
+        want = min(1, len(slots) - 1)
+        j = max(i for i in range(len(plan)) if i % len(slots) == want)
+        f = len(plan[j]) // 2
+        lin_d, rgba_d = slots[j % len(slots)].image(f)
+        check_frame = {"seed": plan[j][f].seed, "launch": j, "slot": j % len(slots), "frame_in_launch": f,
+                       "frames_in_launch": len(plan[j]), "st": plan[j][f],
+                       "lin": lin_d.cpu().numpy(), "rgba": rgba_d.cpu().numpy()}
     kernel_prof = None
     if prof_ctx is not None:
         kernel_prof = prof_ctx.kernel_seconds()
         prof_ctx.profile(False)
     # the same frames one at a time (the reference's synchronous Render)
-    elapsed1, kms1 = (time_steps(slots[:1], torch, dist, world, sts, args.warmup, comm, gstream, 1)
-                      if F * B > 1 else (elapsed, kms))
+    elapsed1, kms1, _ = (time_steps(slots[:1], torch, dist, world, sts, args.warmup, comm, gstream, 1)
+                         if F * B > 1 else (elapsed, kms, busy_frame_ms))
     first_ms = first_frame_ms(rtgo, torch, scene, W, H, sts[0], local) if world == 1 else None
     check = share_sums = gathered_ok = None
     if world > 1 and not args.no_check:
@@ -662,6 +777,9 @@ def main():
         # gather buffer the RCCL group filled (the transport check), then
         # compares its unpacked image with a 1-rank render of the same settings
         # on its own device (createRenderTasks' frame, renderer.go:398-436).
+        wd_check = WD.guard("post-run check (share hashes, 1-rank render)", step="after the timed region",
+                            partition=PART_INFO)
+        wd_check.__enter__()
         torch.cuda.synchronize()
         sl = slots[0]
         nb = sl.share_bytes
@@ -683,6 +801,7 @@ def main():
         ok = [None] * world
         dist.all_gather_object(ok, (check, gathered_ok))
         check, gathered_ok = ok[0]
+        wd_check.__exit__(None, None, None)
     e2e = None
     if world == 1 and not args.no_e2e and cfg in ("c2", "c2_committed", "c3"):
         e2e = render_e2e(rtgo, scene, W, H, args, local)
@@ -694,7 +813,8 @@ def main():
     rank_kernel_ms = [kernel1_s * 1e3]
     if world > 1:
         allk = [None] * world
-        dist.all_gather_object(allk, kernel1_s * 1e3)
+        with WD.guard("kernel-time exchange", step="report", partition=PART_INFO):
+            dist.all_gather_object(allk, kernel1_s * 1e3)
         rank_kernel_ms = allk
     ex = executed(counts)
     npix_local = (part.local_tiles(rank) * 1024) if world > 1 else W * H
@@ -747,10 +867,23 @@ def main():
     achieved_gbs = hbm_bytes / kernel1_s / 1e9
 
     cpu = cpu_bvh = cpu2 = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, rtgo, scene, W, H, sts[0], cfg)
-        cpu2 = cpu_secondary(args, rtgo, scene, W, H, sts[0], cfg)
-        cpu_bvh = cpu_baseline_bvh(args, rtgo, scene, W, H, sts[0]) if cfg in WAVEFRONT else None
+    check_oracle = check_info = None
+    if rank == 0 and world == 1:
+        # the oracle renders the check frame's settings: the CPU baseline
+        # (full frame, c2/c3) or its BVH tile sample (c4/c5) doubles as the check
+        ref_img = None
+        cst = check_frame["st"]
+        if not args.no_cpu_baseline:
+            cpu, ref_img = cpu_baseline(args, rtgo, scene, W, H, cst, cfg)
+            cpu2 = cpu_secondary(args, rtgo, scene, W, H, sts[0], cfg)
+            if cfg in WAVEFRONT:
+                ref_img, cpu_bvh = cpu_baseline_bvh(args, rtgo, scene, W, H, cst)
+        elif cfg not in WAVEFRONT:
+            import oracle
+
+            ref_img = oracle.render(scene, W, H, cst)[:2]
+        if ref_img is not None:
+            check_oracle, check_info = oracle_check(check_frame, ref_img, W, H)
 
     if rank == 0:
         parallelism = "1 GPU" if world == 1 else "%d ranks: tiles %s, one %s gather per frame" % (
@@ -768,6 +901,7 @@ def main():
             "frames_in_flight": F * B,
             "launches_in_flight": F,
             "frames_per_launch": B,
+            "launch_frames": [len(b) for b in plan],
             "one_frame_in_flight": {
                 "value": round(rays * steps / elapsed1 / 1e6, 3),
                 "ms_per_step": round(elapsed1 / steps * 1e3, 4),
@@ -803,6 +937,13 @@ def main():
                 "kernel": KERNELS[cfg],
                 "kernel_ms": round(kern_s * 1e3, 4),
                 "kernel_ms_frames_in_flight": round(kernelF_s * 1e3, 4) if cfg not in WAVEFRONT else None,
+                # the timed launches' HIP-event spans, their union over the
+                # frames: GPU time per frame with the launches as the bench
+                # runs them (overlapping launches counted once)
+                "busy_ms_per_frame": round(busy_frame_ms, 4) if cfg not in WAVEFRONT else None,
+                "frac_busy": (round(f64 / (busy_frame_ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS
+                                    + f32 / (busy_frame_ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 5)
+                              if cfg not in WAVEFRONT and busy_frame_ms > 0 else None),
                 # the same frame's executed flops over the bench's own time per frame
                 # (value's frames in flight: launches overlap, so no single launch shows it)
                 "frac_in_flight": (round(f64 / (elapsed / steps) / 1e12 / PEAK_FP64_TFLOPS
@@ -829,6 +970,14 @@ def main():
                 "algorithmic_bytes_per_launch": hbm_bytes,
             },
             "rank_kernel_ms": [round(x, 4) for x in rank_kernel_ms],
+            # N = 1: a frame of the timed region (a batched launch on the second
+            # slot) against the oracle's render of its settings, bit for bit
+            "check_equals_oracle": check_oracle,
+            "check_frame": ({k: v for k, v in check_frame.items() if k not in ("st", "lin", "rgba")}
+                            | (check_info or {})
+                            | {"oracle": ("full frame (the cpu_baseline leg's last render)" if cfg not in WAVEFRONT
+                                          else "the cpu_baseline_bvh leg's tile sample (same image as the linear "
+                                               "scan)")}) if check_frame else None,
             "check_equals_one_rank": check,
             "check_gathered_equals_rank_shares": gathered_ok,
             "rank_share_sha256_16": share_sums,
@@ -840,6 +989,7 @@ def main():
             "cpu_baseline": cpu,
         }
         if cpu:
+            # (all ratios over cpu_baseline.value: the faster CPU figure)
             out["gpu_over_cpu"] = round(value / cpu["value"], 1)
             out["gpu_over_cpu_one_frame"] = round(out["one_frame_in_flight"]["value"] / cpu["value"], 1)
             out.update(cpu2 or {})
@@ -855,7 +1005,8 @@ def main():
     if comm is not None:
         comm.close()
     if world > 1:
-        dist.barrier()
+        with WD.guard("final barrier", step="exit", partition=PART_INFO):
+            dist.barrier()
         dist.destroy_process_group()
 
 

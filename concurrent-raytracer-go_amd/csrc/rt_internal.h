@@ -196,6 +196,9 @@ int launch_render(const KParams& p, bool count, void* stream);
 size_t render_shmem(const KParams& p);
 // device -> mapped pinned host memory by a kernel (16-byte aligned, a multiple of 16 bytes)
 int launch_download(const void* d_src, void* h_dst_mapped, size_t bytes, void* stream);
+// one workgroup that sleeps for `ms` of device time, then exits (the
+// renderer watchdog's test hook, rt_multi.cpp test_stall)
+int launch_spin(double ms, void* stream);
 int launch_unpack(int32_t W, int32_t H, int32_t world, const void* gathered, size_t share_bytes, size_t rgba_off,
                   float* ol, uint8_t* orgba, void* stream);
 // The same for a partition: slot[t] = {owner rank, local tile} of global tile t;

@@ -526,8 +526,7 @@ struct Hot {
 };
 extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
 template <bool kStage>
-__device__ __forceinline__ Hot hot() {
-  KArg k = fresh();
+__device__ __forceinline__ Hot hot(KArg k) {
   Hot h;
   h.g = Geo{k->spheres, k->tris, k->boxes, k->bvh, k->ns, k->nt, k->use_bvh, k->nb};
   h.mats = k->mats;
@@ -552,6 +551,10 @@ __device__ __forceinline__ Hot hot() {
   h.soft = k->soft != 0;
   h.masks = !h.g.use_bvh && h.g.ns <= 64 && h.g.nt <= 64;  // shadow-cone culling available
   return h;
+}
+template <bool kStage>
+__device__ __forceinline__ Hot hot() {
+  return hot<kStage>(fresh());
 }
 
 // Camera ray of sample s of pixel (x, y): tracePixel's jitter
@@ -741,8 +744,32 @@ __shared__ unsigned long long solo_clk[16];
 #endif
 
 // The path of lane `ow`, run to its end by the whole wave: its radiance.
+// A real call (RT_SOLO_CALL, the default): its registers then do not add to
+// the shade loop's, whose per-iteration scratch spills they caused when it
+// was inlined.  A callee has no kernarg segment pointer of
+// its own -- __builtin_amdgcn_kernarg_segment_ptr() lowers to a null pointer
+// outside a kernel entry point, which is what made round 4's non-inlined
+// variant fault on its first parameter load -- so the kernel passes it in
+// (`karg`) and every per-bounce read launders that copy (launder()).
+#ifndef RT_SOLO_CALL
+#define RT_SOLO_CALL 1
+#endif
+#if RT_SOLO_CALL
+#define RT_SOLO_ATTR __noinline__
+#else
+#define RT_SOLO_ATTR __forceinline__
+#endif
+__device__ __forceinline__ KArg launder(KArg k) {
+  // (a call's arguments arrive in VGPRs: made wave-uniform first)
+  const uint64_t v = (uint64_t)(uintptr_t)k;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  KArg r = (KArg)(uintptr_t)(((uint64_t)hi << 32) | lo);
+  asm volatile("" : "+s"(r));
+  return r;
+}
 template <bool kSky>
-__device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t rx, int depth, int* stack) {
+__device__ RT_SOLO_ATTR d3 solo_path(KArg karg, int ow, d3 o, d3 d, d3 T, d3 L, uint64_t rx, int depth,
+                                     int* stack) {
   const int lane = (int)(threadIdx.x & 63);
   o = rl3(o, ow);
   d = rl3(d, ow);
@@ -762,7 +789,7 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
   // stream is then a readlane away: no memory access per bounce)
   uint64_t jA, jC, jA64, jC64;
   {
-    const Hot h0 = hot<true>();
+    const Hot h0 = hot<true>(launder(karg));
     par = h0.g.nt == 0 && h0.nl >= 1 && h0.nl <= 2 && h0.nl * h0.g.ns <= 64;
     jA = h0.jump[2 * lane];
     jC = h0.jump[2 * lane + 1];
@@ -774,7 +801,7 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
   solo_clk[7] += 1;
 #endif
   for (;;) {
-    const Hot h = hot<true>();
+    const Hot h = hot<true>(launder(karg));
     const Geo& g = h.g;
     if (depth >= h.max_depth) return L;  // traceRay depth cut-off: contributes 0
 #ifdef RT_WG_TIMING
@@ -785,7 +812,7 @@ __device__ __forceinline__ d3 solo_path(int ow, d3 o, d3 d, d3 T, d3 L, uint64_t
     const bool found = solo_closest(g, o, d, hs);
     SOLO_T(0);
     if (!found) {  // miss -> black (or the opted-in sky)
-      if constexpr (kSky) L = L + mul(T, sky_color(fresh()->sky, d));
+      if constexpr (kSky) L = L + mul(T, sky_color(launder(karg)->sky, d));
       return L;
     }
     d3 P, N;
@@ -1368,7 +1395,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
         // (two or three paths run one after the other this way measured
         // slower: 0.79 / 0.93 vs 0.78 ms)
         if (__popcll(am) == 1 && hot<kStage>().masks) {
-          const d3 Lr = solo_path<kSky>(__builtin_ctzll(am), o, d, T, path_L(), rng.x, depth, stack);
+          const d3 Lr = solo_path<kSky>(fresh(), __builtin_ctzll(am), o, d, T, path_L(), rng.x, depth, stack);
           if (lane == __builtin_ctzll(am)) {
             const int q = entry & (kRound - 1);
             slot[q][0] = Lr.x;
@@ -1897,6 +1924,18 @@ int launch_download(const void* d_src, void* h_dst_mapped, size_t bytes, void* s
   const unsigned grid = (unsigned)((n16 + 255) / 256 < 2048 ? (n16 + 255) / 256 : 2048);
   hipLaunchKernelGGL(download_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint4*)d_src,
                      (uint4*)h_dst_mapped, n16);
+  return (int)hipGetLastError();
+}
+
+// s_memrealtime counts at 100 MHz: the wave sleeps until `ticks` have passed
+// since it started (a bounded wait: it always ends)
+__global__ void spin_kernel(unsigned long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+int launch_spin(double ms, void* stream) {
+  const double t = ms < 60000.0 ? ms : 60000.0;  // at most a minute
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (unsigned long long)(t * 1e5));
   return (int)hipGetLastError();
 }
 

@@ -172,6 +172,10 @@ struct rt_renderer {
   void* h_img = nullptr;
   size_t h_img_cap = 0;
   int64_t frames = 0;              // Render calls so far
+  double watchdog_s = 120.0;       // bound on a multi-rank frame's wait (rt_renderer_set_watchdog)
+  std::string stalled;             // set when the watchdog fired: the renderer is unusable
+  int stall_rank = -1;             // test hook (rt_renderer_test_stall)
+  double stall_ms = 0;
 };
 
 struct rt_comm {
@@ -180,6 +184,44 @@ struct rt_comm {
 };
 
 namespace {
+
+// Waits until stream s (of `device`) is idle or `deadline` (now_s() clock,
+// <= 0: none) passes: RT_OK, RT_E_TIMEOUT, or RT_E_DEVICE.  Polls the
+// stream (yield, then 20 us sleeps), so a collective that never completes
+// leaves the caller in control instead of in hipStreamSynchronize forever.
+int bounded_sync(int device, hipStream_t s, double deadline) {
+  HIP_TRY(hipSetDevice(device));
+  if (deadline <= 0) {
+    HIP_TRY(hipStreamSynchronize(s));
+    return RT_OK;
+  }
+  for (unsigned spin = 0;; ++spin) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return RT_OK;
+    if (e != hipErrorNotReady) {
+      set_error(std::string("hipStreamQuery failed: ") + hipGetErrorString(e));
+      return RT_E_DEVICE;
+    }
+    if (now_s() > deadline) return RT_E_TIMEOUT;
+    if (spin < 256)
+      std::this_thread::yield();
+    else
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+// Test hook (rt_renderer_test_stall): the next frame's rank k stream first
+// runs a kernel that sleeps for ms milliseconds of device time and then
+// exits, so a short watchdog fires while every wave still ends on its own
+// (tests/test_gpu_watchdog.py).  Armed for one frame.
+void test_stall(rt_renderer* r, int n) {
+  const int k = r->stall_rank;
+  const double ms = r->stall_ms;
+  r->stall_rank = -1;
+  if (k < 0 || k >= n || ms <= 0) return;
+  const Rank& q = r->ranks[k];
+  if (hipSetDevice(q.device) == hipSuccess) (void)launch_spin(ms, q.stream);
+}
 
 int renderer_fail_cleanup(rt_renderer* r, int rc) {
   rt_renderer_destroy(r);
@@ -357,10 +399,16 @@ int rt_renderer_create(const int32_t* devices, int32_t n, rt_renderer** out) {
 void rt_renderer_destroy(rt_renderer* r) {
   if (!r) return;
   for (Rank& q : r->ranks) {
-    if (q.stream) {
+    if (q.stream && r->stalled.empty()) {
       (void)hipSetDevice(q.device);
       (void)hipStreamSynchronize(q.stream);
     }
+  }
+  if (!r->stalled.empty()) {
+    // the watchdog fired: the communicators are aborted and the stalled
+    // work may never end -- nothing that waits on it is released
+    delete r;
+    return;
   }
   for (ncclComm_t c : r->comms) (void)ncclCommDestroy(c);
   host_free(r->h_img);
@@ -392,11 +440,34 @@ int rt_renderer_set_tuning(rt_renderer* r, const rt_tuning* t) {
   return RT_OK;
 }
 
+int rt_renderer_set_watchdog(rt_renderer* r, double seconds) {
+  if (!r) {
+    set_error("renderer is NULL");
+    return RT_E_INVALID;
+  }
+  r->watchdog_s = seconds;
+  return RT_OK;
+}
+
+int rt_renderer_test_stall(rt_renderer* r, int32_t rank, double ms) {
+  if (!r || rank < 0 || rank >= (int32_t)r->ranks.size() || !(ms >= 0 && ms <= 60000)) {
+    set_error("rt_renderer_test_stall: invalid arguments");
+    return RT_E_INVALID;
+  }
+  r->stall_rank = rank;
+  r->stall_ms = ms;
+  return RT_OK;
+}
+
 int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t h, const rt_settings* st,
                        float* out_linear, uint8_t* out_rgba, rt_stats* stats) {
   if (!r) {
     set_error("renderer is NULL");
     return RT_E_INVALID;
+  }
+  if (!r->stalled.empty()) {
+    set_error(r->stalled);
+    return RT_E_TIMEOUT;
   }
   int rc = rt_validate(scene, w, h, st);
   if (rc) return rc;
@@ -464,6 +535,7 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
                                        bufs[k] + rgba_off, q.stream, nullptr);
       if (rcs[k]) errs[k] = rt_last_error();  // (the error text is per thread)
     };
+    test_stall(r, n);
     std::vector<std::thread> pool;
     try {
       for (int k = 1; k < n; ++k) pool.emplace_back(render_rank, k);
@@ -503,10 +575,29 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
   // stream it starts at once.
   double ks = 0;
   r->rank_secs.assign(n, 0.0);
+  // a multi-rank frame waits at most watchdog_s from here (its launches and
+  // the gather are all enqueued): a stalled rank or collective ends the wait
+  const double deadline = n > 1 && r->watchdog_s > 0 ? t_launch + r->watchdog_s : 0.0;
   for (int k = 0; k < n; ++k) {
     Rank& q = r->ranks[k];
-    HIP_TRY(hipSetDevice(q.device));
-    HIP_TRY(hipStreamSynchronize(q.stream));
+    rc = bounded_sync(q.device, q.stream, deadline);
+    if (rc == RT_E_TIMEOUT) {
+      const std::string part =
+          r->part ? "balanced, " + std::to_string(rt_partition_local_tiles(r->part, k)) + " tiles on this rank"
+                  : "strided t % " + std::to_string(n) + ", " + std::to_string(rt_tiles_for_rank(w, h, k, n)) +
+                        " tiles on this rank";
+      r->stalled = "rt_renderer_render: watchdog: rank " + std::to_string(k) + " (device " +
+                   std::to_string(q.device) + ") did not finish frame " + std::to_string(r->frames) + " (" +
+                   std::to_string(w) + "x" + std::to_string(h) + ", " + std::to_string(st->samples) +
+                   " spp) within " + std::to_string(r->watchdog_s) + " s of its launch: its share render" +
+                   (r->devices.size() > 1 ? ", the RCCL gather" : "") + " or the unpack stalled (partition " + part +
+                   "); communicators aborted, the renderer is unusable";
+      for (ncclComm_t c : r->comms) (void)ncclCommAbort(c);
+      r->comms.clear();
+      set_error(r->stalled);
+      return RT_E_TIMEOUT;
+    }
+    if (rc) return rc;
     double s = 0;
     rc = rt_context_last_kernel_seconds(q.ctx, &s);
     if (rc) return rc;
@@ -568,7 +659,7 @@ int rt_render(const rt_scene* scene, int32_t w, int32_t h, const rt_settings* st
   const double t_created = now_s();
   rc = rt_renderer_render(r, scene, w, h, st, out_linear, out_rgba, stats);
   const double t_rendered = now_s();
-  rt_renderer_destroy(r);
+  rt_renderer_destroy(r);  // (after a watchdog timeout it releases only what does not wait on the stall)
   if (!rc && stats) {  // Go's Render time covers everything (renderer.go:68,101)
     stats->create_seconds = t_created - t0;
     stats->destroy_seconds = now_s() - t_rendered;

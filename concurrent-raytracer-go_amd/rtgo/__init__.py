@@ -28,6 +28,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RTGO_LIB") or os.path.join(os.path.dirname(_HERE), "build", "librtgo.so")
 
 RT_OK = 0
+RT_E_TIMEOUT = -6  # a multi-rank frame did not finish in time (rt_renderer_set_watchdog)
 RT_OBJ_SPHERE, RT_OBJ_CUBE = 0, 1
 MATERIAL_KINDS = {
     "lambertian": 0,
@@ -43,7 +44,7 @@ RT_PATH_AUTO, RT_PATH_MEGAKERNEL = 0, 1
 RT_PARTITION_AUTO, RT_PARTITION_STRIDED, RT_PARTITION_BALANCED = 0, 1, 2
 SKIES = {"none": 0, "default": 1, "white": 2, "sunset": 3, "night": 4}  # RT_SKY_*
 RT_COMM_ID_BYTES = 128
-RT_MAX_FRAMES = 16  # frames per launch (rt_context_render_frames_async)
+RT_MAX_FRAMES = 32  # frames per launch (rt_context_render_frames_async)
 # wavefront kernel classes (RT_WF_*, rt_context_kernel_seconds)
 WF_KERNELS = ["extend", "shade1", "occlude_hard", "cone", "softgen", "cone_rays", "occlude_soft", "shade", "regen", "resolve"]
 
@@ -269,6 +270,8 @@ EXPORTED_SYMBOLS = [
     "rt_context_render_frames_async",
     "rt_unpack_partition_frames_async",
     "rt_release_cached_memory",
+    "rt_renderer_set_watchdog",
+    "rt_renderer_test_stall",
 ]
 
 _lib = None
@@ -366,6 +369,8 @@ def lib():
         ),
         "rt_unpack_partition_frames_async": (ctypes.c_int, [vp, i32, vp, vp, vp, vp]),
         "rt_release_cached_memory": (ctypes.c_int, []),
+        "rt_renderer_set_watchdog": (ctypes.c_int, [vp, ctypes.c_double]),
+        "rt_renderer_test_stall": (ctypes.c_int, [vp, i32, ctypes.c_double]),
         "rt_context_kernel_seconds": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
                                                      ctypes.POINTER(ctypes.c_int64)]),
     }
@@ -544,6 +549,14 @@ class ParallelRenderer:
             self.close()
         except Exception:
             pass
+
+    def set_watchdog(self, seconds: float):
+        """rt_renderer_set_watchdog: bound a multi-rank Render's wait (RT_E_TIMEOUT after `seconds`)."""
+        _check(lib().rt_renderer_set_watchdog(self._renderer(), float(seconds)))
+
+    def test_stall(self, rank: int, ms: float):
+        """rt_renderer_test_stall (test hook): the next multi-rank frame's rank first sleeps `ms` on the GPU."""
+        _check(lib().rt_renderer_test_stall(self._renderer(), rank, float(ms)))
 
     # settings.go:3-25
     def set_samples(self, samples: int):

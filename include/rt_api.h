@@ -39,6 +39,7 @@ extern "C" {
 #define RT_E_PARSE (-3)     /* scene JSON malformed */
 #define RT_E_DEVICE (-4)    /* HIP runtime / device error */
 #define RT_E_NOMEM (-5)
+#define RT_E_TIMEOUT (-6)   /* a multi-device frame did not finish in time (rt_renderer_set_watchdog) */
 
 /* Object kinds — internal/scene/scene.go:69-82 ("sphere", "cube"; any other
  * type string is skipped by the loader with "Unknown object type"). */
@@ -272,6 +273,21 @@ int rt_renderer_create(const int32_t* devices, int32_t num_devices, rt_renderer*
 int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t width, int32_t height,
                        const rt_settings* settings, float* out_linear_rgb, uint8_t* out_rgba, rt_stats* stats);
 void rt_renderer_destroy(rt_renderer* r);
+/* Watchdog of a multi-rank Render (more than one rank): if a rank's share
+ * render, the RCCL gather into the first device (renderer.go:398-436 is the
+ * tile farm-out it replaces) or the unpack has not completed `seconds` after
+ * the frame was enqueued, Render stops waiting, aborts the renderer's RCCL
+ * communicators and returns RT_E_TIMEOUT with the rank, device, frame and
+ * partition in rt_last_error().  The renderer is then unusable: later calls
+ * return RT_E_TIMEOUT, and rt_renderer_destroy releases only what does not
+ * wait on the stalled work (exit the process to reclaim the rest).  Default
+ * 120 s; seconds <= 0 waits without a bound.  One-rank renders have no
+ * collective and are never bounded. */
+int rt_renderer_set_watchdog(rt_renderer* r, double seconds);
+/* Test hook for the watchdog: the renderer's next multi-rank frame first
+ * runs, on `rank`'s stream, one workgroup that sleeps for `ms` (0..60000)
+ * milliseconds of device time and then exits -- a stall that always ends. */
+int rt_renderer_test_stall(rt_renderer* r, int32_t rank, double ms);
 
 /* ------------------------------------------- resident context (bench/MGPU) */
 
@@ -351,7 +367,7 @@ int rt_context_render_async(rt_context* ctx, int32_t width, int32_t height, cons
  * once per frame.  d_linear[f] / d_rgba[f] (d_rgba may
  * be NULL, entries may be NULL) are laid out as in rt_context_render_async.
  * BVH scenes, sample passes and measuring frames render frame by frame. */
-#define RT_MAX_FRAMES 16
+#define RT_MAX_FRAMES 32
 int rt_context_render_frames_async(rt_context* ctx, int32_t width, int32_t height, const rt_settings* settings,
                                    int32_t nframes, const uint64_t* seeds, int32_t rank, int32_t world,
                                    int32_t layout, float* const* d_linear, uint8_t* const* d_rgba, void* hip_stream);

@@ -3,7 +3,10 @@
 dominant kernel, merged into profiles/<round>_pmc_traffic.json under the
 workload label bench.py prints (its roofline.traffic).
 
-usage: pmc_traffic.py CONFIG FETCH_DIR WRITE_DIR OUT.json FRAMES
+usage: pmc_traffic.py CONFIG FETCH_DIR WRITE_DIR OUT.json FRAMES [FRAMES_PER_LAUNCH]
+(FRAMES_PER_LAUNCH > 1, c2/c3: the passes ran PMC_FRAMES launches of that
+many frames; the entry is keyed "<workload> | B frames per launch" and
+carries bytes per launch and per frame)
 Each DIR holds one rocprofv3 --pmc pass (FETCH_SIZE, resp. WRITE_SIZE; they
 cannot share a pass on gfx950) in CSV form over FRAMES frames of the config
 (scripts/pmc_workload.py).  Corrections from
@@ -46,8 +49,11 @@ def per_dispatch(d, counter):
 
 def main():
     cfg, fdir, wdir, out, frames = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5])
+    fpl = int(sys.argv[6]) if len(sys.argv) > 6 else 1
     spec, W, H, SPP, label = CONFIGS[cfg][:5]
     workload = "%s %dx%d %dspp depth 50" % (label, W, H, SPP)
+    if fpl > 1:
+        workload += " | %d frames per launch" % fpl
     kerns = [k.strip() for k in KERNELS[cfg].replace("rtgo::", "").split("+")]  # (c4/c5: the soft-shadow stage)
     fetch = per_dispatch(fdir, "FETCH_SIZE")
     write = per_dispatch(wdir, "WRITE_SIZE")
@@ -73,7 +79,8 @@ def main():
         fb = statistics.median(kf) * 1024 * 2
         wb = statistics.median(kw) * 1024
         res.update({"unit": "per launch (median)", "fetch_bytes_corrected": fb, "write_bytes": wb,
-                    "hbm_bytes_per_launch": fb + wb, "algorithmic_bytes_per_launch": W * H * 16 + 4096})
+                    "hbm_bytes_per_launch": fb + wb, "algorithmic_bytes_per_launch": (W * H * 16 + 4096) * fpl,
+                    "frames_per_launch": fpl, "hbm_bytes_per_frame": (fb + wb) / fpl})
     res["note"] = ("FETCH_SIZE (KiB) x1024 x2 per MI355X_MICROARCH.md §HBM (gfx950 counts half the bytes of wide "
                    "reads); WRITE_SIZE (KiB) x1024, exact for these stores (profiles/r02_pmc_calibration.json)")
     try:

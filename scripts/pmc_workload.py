@@ -4,7 +4,9 @@ of one bench config (PMC_CONFIG: c2 default, c2_committed, c3, c4, c5; the
 scenes and sizes of bench.py CONFIGS) on one GPU, one frame per launch.  Run
 under rocprofv3 --pmc by scripts/profile.sh so each PMC pass sees only the
 config's kernels.  PMC_SIZE=W,H,SPP overrides the size (the instruction-mix
-passes of scripts/profile_instmix.sh use C4's scene at 960x540x16)."""
+passes of scripts/profile_instmix.sh use C4's scene at 960x540x16).
+PMC_FRAMES=B (c2/c3): K launches of B frames each (rt_context_render_frames_async,
+the bench's timed launches) instead of K one-frame launches."""
 import os
 import sys
 
@@ -30,10 +32,15 @@ s = torch.cuda.Stream()
 torch.cuda.set_stream(s)
 ctx = rtgo.Context(0)
 ctx.set_scene(load_scene(rtgo, spec))
-lin = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
-rgba = torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda")
+B = int(os.environ.get("PMC_FRAMES", "1"))
+lin = torch.zeros((B, W * H * 3), dtype=torch.float32, device="cuda")
+rgba = torch.zeros((B, W * H * 4), dtype=torch.uint8, device="cuda")
 for i in range(K):
-    st.seed = 1 + i
-    ctx.render_async(W, H, st, lin.data_ptr(), rgba.data_ptr(), s.cuda_stream)
+    if B == 1:
+        st.seed = 1 + i
+        ctx.render_async(W, H, st, lin[0].data_ptr(), rgba[0].data_ptr(), s.cuda_stream)
+    else:
+        ctx.render_frames_async(W, H, st, [1 + i * B + f for f in range(B)], [lin[f].data_ptr() for f in range(B)],
+                                [rgba[f].data_ptr() for f in range(B)], s.cuda_stream)
 torch.cuda.synchronize()
-print("rendered", K, "frames of", cfg, f"{W}x{H}x{SPP}; linear sum", float(lin.double().sum()))
+print("rendered", K, "launches of", B, "frames of", cfg, f"{W}x{H}x{SPP}; linear sum", float(lin.double().sum()))
