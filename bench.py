@@ -92,7 +92,10 @@ TRAV_RAY_SETUP_FLOPS = 21
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) peak: 256 CU x 2.4 GHz x 128 FLOP/clk
 PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-PMC_FILE = os.path.join(ROOT, "profiles", "r04_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")
+# the driver's own command under rocprofv3 --kernel-trace: its timed launches
+# (scripts/batched_trace.py, scripts/profile.sh "driver")
+TRACE_FILE = os.path.join(ROOT, "profiles", "r05_driver_batched_trace.json")
 
 CONFIGS = {
     # name: (scene, W, H, spp, label, default steps, default frames in flight at one GPU)
@@ -372,6 +375,24 @@ def first_frame_ms(rtgo, torch, scene, W, H, st, local):
     return ms
 
 
+def first_frame_ms_multi(rtgo, torch, dist, scene, W, H, st, rank, world, local, comm, gstream, strided):
+    """N > 1: one frame on fresh contexts, its partition planned anew (a
+    balanced partition measures the frame first, rt_partition_balanced), its
+    schedule built, rendered and gathered to rank 0.  Wall clock, max over
+    ranks."""
+    barrier_sync(torch, dist, world, "first-frame barrier", step="first frame", partition=PART_INFO)
+    t0 = time.perf_counter()
+    with WD.guard("first frame", step="first frame (fresh contexts)", partition=PART_INFO):
+        part, _ = plan_partition(rtgo, torch, dist, scene, W, H, st, rank, world, local, strided)
+        sl = Slot(rtgo, torch, scene, W, H, rank, world, local, part, 1)
+        sl.render([st])
+        sl.gather(torch, comm, gstream)
+        torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3
+    sl.close()
+    return max_over_ranks(torch, dist, world, ms)
+
+
 def render_e2e(rtgo, scene, W, H, args, local):
     """The blocking Render of the C ABI (N = 1): scene check + upload,
     schedule, kernels, image download to the host."""
@@ -600,7 +621,7 @@ def cpu_baseline_bvh(args, rtgo, scene, W, H, st):
 
 def pmc_traffic(workload):
     """HBM bytes per launch of the dominant kernel from the committed
-    rocprofv3 PMC passes (profiles/r04_pmc_traffic.json, scripts/pmc_traffic.py,
+    rocprofv3 PMC passes (profiles/r05_pmc_traffic.json, scripts/pmc_traffic.py,
     with the gfx950 corrections of MI355X_MICROARCH.md §HBM), if it holds this
     workload."""
     try:
@@ -610,6 +631,36 @@ def pmc_traffic(workload):
         return None
     e = d.get(workload) if isinstance(d, dict) else None
     return e.get("hbm_bytes_per_launch") if e else None
+
+
+def pmc_traffic_batched(workload):
+    """HBM bytes per FRAME of the dominant kernel in launches of several
+    frames (the "| B frames per launch" entry of the same PMC file), and B."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    for k, e in (d.items() if isinstance(d, dict) else ()):
+        if k.startswith(workload + " | "):
+            return e.get("hbm_bytes_per_frame"), e.get("frames_per_launch")
+    return None, None
+
+
+def trace_batched(cfg):
+    """The committed kernel trace of the driver's command (c2): its timed
+    launches' per-frame kernel time (union of their spans over the frames)."""
+    if cfg != "c2":
+        return None
+    try:
+        with open(TRACE_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return {"union_ms_per_frame": d.get("union_ms_per_frame"), "avg_launch_ms_per_frame": d.get("avg_launch_ms_per_frame"),
+            "launch_frames": d.get("bench_cmd_line", {}).get("launch_frames"),
+            "ms_per_step_of_that_run": d.get("bench_cmd_line", {}).get("ms_per_step"),
+            "file": os.path.relpath(TRACE_FILE, ROOT)}
 
 
 def plan_partition(rtgo, torch, dist, scene, W, H, st, rank, world, local, strided):
@@ -708,12 +759,18 @@ def main():
     # start.  A rank's share at N > 1 holds ~1/N of the frame's work but the
     # frame's longest paths, so it needs more frames per launch
     # (scripts/rank_share_probe.py).  BVH frames: one at a time.
+    # At one GPU the timed steps fill the F slots: ceil(K / F) frames per
+    # launch up to RT_MAX_FRAMES (K = 20: two launches of 10 side by side;
+    # K = 100: four of 25, two at a time -- 25-frame launches measured 2 %
+    # faster than 16-frame ones at K = 100, and K = 20 the same either way,
+    # DESIGN.md §6).
     if cfg in WAVEFRONT:
         F, B = 1, 1
     elif world > 1:
         F, B = 3, 16
     else:
-        F, B = fif_default, 16
+        F = fif_default
+        B = -(-steps // (args.frames_in_flight or F))
     F = args.frames_in_flight or F
     B = max(1, min(rtgo.RT_MAX_FRAMES, args.frames_per_launch or B))
     scene = load_scene(rtgo, spec)
@@ -754,7 +811,7 @@ def main():
         # the frame the oracle checks (check_equals_oracle): one from the last
         # launch that ran on the second slot (the first when F = 1), from the
         # middle of that launch, copied now (later timings reuse slot 0)
-        want = min(1, len(slots) - 1)
+        want = min(1, len(slots) - 1, len(plan) - 1)
         j = max(i for i in range(len(plan)) if i % len(slots) == want)
         f = len(plan[j]) // 2
         lin_d, rgba_d = slots[j % len(slots)].image(f)
@@ -768,7 +825,11 @@ def main():
     # the same frames one at a time (the reference's synchronous Render)
     elapsed1, kms1, _ = (time_steps(slots[:1], torch, dist, world, sts, args.warmup, comm, gstream, 1)
                          if F * B > 1 else (elapsed, kms, busy_frame_ms))
-    first_ms = first_frame_ms(rtgo, torch, scene, W, H, sts[0], local) if world == 1 else None
+    if world == 1:
+        first_ms = first_frame_ms(rtgo, torch, scene, W, H, sts[0], local)
+    else:
+        first_ms = first_frame_ms_multi(rtgo, torch, dist, scene, W, H, sts[0], rank, world, local, comm, gstream,
+                                        args.strided or cfg in WAVEFRONT)
     check = share_sums = gathered_ok = None
     if world > 1 and not args.no_check:
         # After the timed region, always at N > 1: the last timed frame (slot 0
@@ -934,6 +995,11 @@ def main():
                 "fp32_flops": f32,
                 "flops_unit": flops_unit,
                 "traffic": pmc_traffic(workload),
+                # the same kernel in launches of several frames (the timed ones):
+                # HBM bytes per frame, and the rocprof trace's per-frame time
+                "traffic_batched_per_frame": pmc_traffic_batched(workload)[0],
+                "traffic_batched_frames_per_launch": pmc_traffic_batched(workload)[1],
+                "trace_batched": trace_batched(cfg) if world == 1 else None,
                 "kernel": KERNELS[cfg],
                 "kernel_ms": round(kern_s * 1e3, 4),
                 "kernel_ms_frames_in_flight": round(kernelF_s * 1e3, 4) if cfg not in WAVEFRONT else None,
@@ -958,7 +1024,11 @@ def main():
                         "(HIP events on the render stream; for c4/c5 the soft-shadow traversal kernel's time per "
                         "frame from rt_context_profile's events in the timed frames); frac_in_flight: the frame's flops over "
                         "ms_per_step (the throughput line's time per frame).  traffic = HBM bytes per "
-                        "launch from rocprofv3 FETCH_SIZE + WRITE_SIZE passes (profiles/r04_pmc_traffic.json).",
+                        "launch from rocprofv3 FETCH_SIZE + WRITE_SIZE passes (profiles/r05_pmc_traffic.json; "
+                        "traffic_batched_per_frame: the same passes over launches of several frames, per frame).  "
+                        "busy_ms_per_frame / frac_busy: the timed launches' HIP-event spans (their union: launches in "
+                        "flight overlap) over the frames; trace_batched: the same from the committed rocprofv3 "
+                        "kernel trace of this exact command (profiles/r05_driver_batched_trace.json).",
             },
             "roofline_frame": whole,
             "roofline_hbm": {

@@ -117,16 +117,30 @@ int rt_write_png(const char* path, const uint8_t* rgba, int32_t w, int32_t h) {
     set_error(std::string("mkdir for ") + path + ": " + strerror(errno));
     return RT_E_IO;
   }
-  // raw scanlines, filter type 0, RGB8
+  // image/png encodes an opaque *image.RGBA as RGB8 (every render: alpha 255,
+  // renderer.go:96) and any other as RGBA8 with the colour un-premultiplied
+  // ((c * 0xffff / a) >> 8 on 16-bit values; the CLI's empty frame of a
+  // negative size is all zero)
+  bool opaque = true;
+  for (size_t i = 0; i < (size_t)w * h && opaque; ++i) opaque = rgba[i * 4 + 3] == 255;
+  const int ch = opaque ? 3 : 4;
+  // raw scanlines, filter type 0
   std::vector<uint8_t> raw;
-  raw.reserve((size_t)h * (1 + (size_t)w * 3));
+  raw.reserve((size_t)h * (1 + (size_t)w * ch));
   for (int32_t y = 0; y < h; ++y) {
     raw.push_back(0);
     const uint8_t* row = rgba + (size_t)y * w * 4;
     for (int32_t x = 0; x < w; ++x) {
-      raw.push_back(row[x * 4 + 0]);
-      raw.push_back(row[x * 4 + 1]);
-      raw.push_back(row[x * 4 + 2]);
+      const uint8_t* q = row + x * 4;
+      if (opaque) {
+        raw.push_back(q[0]);
+        raw.push_back(q[1]);
+        raw.push_back(q[2]);
+        continue;
+      }
+      const uint32_t a = q[3] * 0x101u;
+      for (int c = 0; c < 3; ++c) raw.push_back(a == 0 ? 0 : (uint8_t)(((q[c] * 0x101u) * 0xffffu / a) >> 8));
+      raw.push_back(q[3]);
     }
   }
   uLongf zcap = compressBound((uLong)raw.size());
@@ -147,7 +161,7 @@ int rt_write_png(const char* path, const uint8_t* rgba, int32_t w, int32_t h) {
   ihdr[6] = (uint8_t)(h >> 8);
   ihdr[7] = (uint8_t)h;
   ihdr[8] = 8;   // bit depth
-  ihdr[9] = 2;   // truecolour (opaque RGBA is encoded as RGB by image/png)
+  ihdr[9] = opaque ? 2 : 6;  // truecolour, or truecolour with alpha
   ihdr[10] = 0;  // deflate
   ihdr[11] = 0;  // adaptive filtering
   ihdr[12] = 0;  // no interlace

@@ -13,9 +13,11 @@
 // (README.md:60-61), and the optional flags above (the Go CLI never calls
 // the renderer's setters, settings.go:3-25; --sky is the opt-in atmosphere,
 // include/rt_api.h RT_SKY_*).
+#include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
 #include <sys/time.h>
 #include <time.h>
 #include <unistd.h>
@@ -46,6 +48,11 @@ static std::string dir_of(const std::string& path) {  // filepath.Dir
   return path.substr(0, s);
 }
 
+static void mkdir_p(const std::string& dir) {  // os.MkdirAll(dir, 0755)
+  for (size_t i = 1; i <= dir.size(); ++i)
+    if (i == dir.size() || dir[i] == '/') (void)mkdir(dir.substr(0, i).c_str(), 0755);
+}
+
 static std::string ext_of(const std::string& path) {  // filepath.Ext
   for (size_t i = path.size(); i-- > 0;) {
     if (path[i] == '/') break;
@@ -74,6 +81,59 @@ static std::string rfc3339nano_now() {
   else
     snprintf(tz, sizeof tz, "%c%02ld:%02ld", off < 0 ? '-' : '+', labs(off) / 3600, (labs(off) % 3600) / 60);
   return std::string(date) + frac + tz;
+}
+
+static const char* kFeatures[] = {
+    "Improved metallic reflections with Fresnel effect",
+    "Shiny materials with configurable roughness and specular",
+    "Enhanced light source reflections",
+    "Better specular highlights for metallic surfaces",
+};
+
+// Render's closing lines (renderer.go:119-123)
+static void print_complete() {
+  printf("Rendering complete!\n");
+  printf("Enhanced materials features:\n");
+  for (const char* f : kFeatures) printf("- %s\n", f);
+}
+
+// SaveBenchmarkData (renderer.go:473-485): BenchmarkData JSON, 2-space indent,
+// next to the output (main.go:64-69)
+static void save_benchmark(const std::string& out_path, long long w, long long h, const rt_settings& st,
+                           const rt_stats& stats) {
+  std::string bench_path = dir_of(out_path) + "/benchmark_data.json";
+  FILE* f = fopen(bench_path.c_str(), "wb");
+  if (!f) {
+    printf("Error saving benchmark data: open %s failed\n", bench_path.c_str());
+  } else {
+    fprintf(f, "{\n");
+    fprintf(f, "  \"scene_name\": \"demo_scene\",\n");  // GetSceneName, scene.go:100-102
+    fprintf(f, "  \"resolution\": \"%lldx%lld\",\n", w, h);
+    fprintf(f, "  \"render_time_seconds\": %.17g,\n", stats.render_seconds);
+    fprintf(f, "  \"samples\": %d,\n", st.samples);
+    fprintf(f, "  \"max_depth\": %d,\n", st.max_depth);
+    fprintf(f, "  \"num_workers\": %d,\n", st.num_workers);
+    fprintf(f, "  \"objects\": %d,\n", stats.objects);
+    fprintf(f, "  \"lights\": %d,\n", stats.lights);
+    fprintf(f, "  \"timestamp\": \"%s\",\n", rfc3339nano_now().c_str());
+    fprintf(f, "  \"features\": [\n");
+    for (int i = 0; i < 4; ++i) fprintf(f, "    \"%s\"%s\n", kFeatures[i], i < 3 ? "," : "");
+    fprintf(f, "  ],\n");
+    fprintf(f, "  \"kernel_time_seconds\": %.17g,\n", stats.kernel_seconds);
+    // the published benchmark JSON's setup_time / bvh_build_time
+    // (demo-assets/*_benchmark.json; not produced by the snapshot's Go code)
+    fprintf(f, "  \"setup_time\": %.17g,\n", stats.create_seconds + stats.scene_seconds);
+    fprintf(f, "  \"bvh_build_time\": %.17g,\n", stats.bvh_build_seconds);
+    fprintf(f, "  \"render_breakdown_seconds\": {\"create\": %.9g, \"scene\": %.9g, \"launch\": %.9g, "
+               "\"kernels_and_download\": %.9g, \"destroy\": %.9g},\n",
+            stats.create_seconds, stats.scene_seconds, stats.launch_seconds, stats.download_seconds,
+            stats.destroy_seconds);
+    fprintf(f, "  \"pixels_per_second\": %.17g,\n", stats.pixels_per_second);
+    fprintf(f, "  \"rays_per_second\": %.17g\n", stats.rays_per_second);
+    fprintf(f, "}");
+    fclose(f);
+    printf("Benchmark data saved\n");
+  }
 }
 
 int main(int argc, char** argv) {
@@ -144,15 +204,52 @@ int main(int argc, char** argv) {
     printf("Error loading scene: %s\n", rt_last_error());
     return 1;
   }
-  if (w <= 0 || h <= 0) {
-    // image.NewRGBA of an empty rectangle renders nothing; png.Encode then
-    // fails on a zero-sized image.  Decided before any device state exists,
-    // so a machine without a GPU gives the same answer (exit 1).
+  const long long aw = llabs(w), ah = llabs(h);
+  if ((w <= 0 || h <= 0) && aw <= 65536 && ah <= 65536) {
+    // A size with no tile: createRenderTasks makes none (renderer.go:401-403:
+    // (n + 31) / 32 <= 0), so Go renders nothing.  image.Rect canonicalizes
+    // the rectangle (renderer.go:70): the image is |w| x |h|, every pixel
+    // zero (transparent black), which png.Encode writes as RGBA8 (exit 0);
+    // with |w| or |h| zero, SaveImage creates the file and png.Encode fails
+    // ("invalid image size", exit 1).  No GPU is involved either way, so
+    // this is decided before any device state exists.
+    const auto t0 = std::chrono::steady_clock::now();
     printf("Rendering at %lldx%lld resolution...\n", w, h);
     rt_scene_print_hittables(sb);
-    printf("Error saving image: invalid image size %lldx%lld\n", w, h);
+    rt_stats stats;
+    memset(&stats, 0, sizeof stats);
+    stats.objects = rt_scene_view(sb)->num_objects;
+    stats.lights = rt_scene_view(sb)->num_lights;
+    stats.render_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    print_complete();
+    std::string out_path = output_file;
+    if (ext_of(out_path).empty()) out_path += ".png";
+    printf("Saving to: %s\n", out_path.c_str());
+    int rc = RT_OK;
+    if (aw == 0 || ah == 0) {
+      // os.Create succeeded, png.Encode refused the empty image
+      mkdir_p(dir_of(out_path));  // os.MkdirAll (renderer.go:439-442)
+      FILE* f = fopen(out_path.c_str(), "wb");
+      if (!f) {
+        printf("Error saving image: open %s: %s\n", out_path.c_str(), strerror(errno));
+      } else {
+        fclose(f);
+        printf("Error saving image: png: invalid format: invalid image size: %lldx%lld\n", aw, ah);
+      }
+      rt_scene_free(sb);
+      return 1;
+    }
+    std::vector<uint8_t> rgba((size_t)aw * (size_t)ah * 4, 0);
+    rc = ext_of(out_path) == ".ppm" ? rt_write_ppm(out_path.c_str(), rgba.data(), (int32_t)aw, (int32_t)ah)
+                                    : rt_write_png(out_path.c_str(), rgba.data(), (int32_t)aw, (int32_t)ah);
+    if (rc != RT_OK) {
+      printf("Error saving image: %s\n", rt_last_error());
+      rt_scene_free(sb);
+      return 1;
+    }
+    save_benchmark(out_path, w, h, st, stats);
     rt_scene_free(sb);
-    return 1;
+    return 0;
   }
   // renderer := renderer.NewParallelRenderer(numWorkers) (main.go:46-47):
   // the device state (HIP runtime, context, stream, the kernels' code
@@ -184,15 +281,7 @@ int main(int argc, char** argv) {
     return 2;
   }
   stats.create_seconds = new_seconds;  // (reported apart: setup_time, render_breakdown_seconds.create)
-  static const char* features[] = {
-      "Improved metallic reflections with Fresnel effect",
-      "Shiny materials with configurable roughness and specular",
-      "Enhanced light source reflections",
-      "Better specular highlights for metallic surfaces",
-  };
-  printf("Rendering complete!\n");
-  printf("Enhanced materials features:\n");
-  for (const char* f : features) printf("- %s\n", f);
+  print_complete();
 
   std::string out_path = output_file;
   if (ext_of(out_path).empty()) out_path += ".png";
@@ -206,40 +295,7 @@ int main(int argc, char** argv) {
     rt_scene_free(sb);
     return 1;
   }
-  // SaveBenchmarkData (renderer.go:473-485): BenchmarkData JSON, 2-space indent
-  std::string bench_path = dir_of(out_path) + "/benchmark_data.json";
-  FILE* f = fopen(bench_path.c_str(), "wb");
-  if (!f) {
-    printf("Error saving benchmark data: open %s failed\n", bench_path.c_str());
-  } else {
-    fprintf(f, "{\n");
-    fprintf(f, "  \"scene_name\": \"demo_scene\",\n");  // GetSceneName, scene.go:100-102
-    fprintf(f, "  \"resolution\": \"%lldx%lld\",\n", w, h);
-    fprintf(f, "  \"render_time_seconds\": %.17g,\n", stats.render_seconds);
-    fprintf(f, "  \"samples\": %d,\n", st.samples);
-    fprintf(f, "  \"max_depth\": %d,\n", st.max_depth);
-    fprintf(f, "  \"num_workers\": %d,\n", st.num_workers);
-    fprintf(f, "  \"objects\": %d,\n", stats.objects);
-    fprintf(f, "  \"lights\": %d,\n", stats.lights);
-    fprintf(f, "  \"timestamp\": \"%s\",\n", rfc3339nano_now().c_str());
-    fprintf(f, "  \"features\": [\n");
-    for (int i = 0; i < 4; ++i) fprintf(f, "    \"%s\"%s\n", features[i], i < 3 ? "," : "");
-    fprintf(f, "  ],\n");
-    fprintf(f, "  \"kernel_time_seconds\": %.17g,\n", stats.kernel_seconds);
-    // the published benchmark JSON's setup_time / bvh_build_time
-    // (demo-assets/*_benchmark.json; not produced by the snapshot's Go code)
-    fprintf(f, "  \"setup_time\": %.17g,\n", stats.create_seconds + stats.scene_seconds);
-    fprintf(f, "  \"bvh_build_time\": %.17g,\n", stats.bvh_build_seconds);
-    fprintf(f, "  \"render_breakdown_seconds\": {\"create\": %.9g, \"scene\": %.9g, \"launch\": %.9g, "
-               "\"kernels_and_download\": %.9g, \"destroy\": %.9g},\n",
-            stats.create_seconds, stats.scene_seconds, stats.launch_seconds, stats.download_seconds,
-            stats.destroy_seconds);
-    fprintf(f, "  \"pixels_per_second\": %.17g,\n", stats.pixels_per_second);
-    fprintf(f, "  \"rays_per_second\": %.17g\n", stats.rays_per_second);
-    fprintf(f, "}");
-    fclose(f);
-    printf("Benchmark data saved\n");
-  }
+  save_benchmark(out_path, w, h, st, stats);
   rt_renderer_destroy(rr);
   rt_scene_free(sb);
   return 0;

@@ -138,6 +138,7 @@ struct rt_context {
   // every pixel's paths into d_meas (max | sum), 2 measured (the next
   // schedule is re-cut from them), 3 done
   int meas_state = 0;
+  rt_context_stats stats{};  // rt_context_get_stats
   char* d_meas = nullptr;
   size_t meas_cap = 0;
   char* d_sched = nullptr;  // scheduler scratch (sched_layout) + the per-tile inputs
@@ -739,14 +740,31 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
       // staging on first use, milliseconds of a fresh process's first frame)
       memcpy(c->h_small + 256, c->masks_host.data(), mbytes);
       memcpy(c->h_small + 256 + mbytes, cost.data(), cbytes);
-      if (mbytes) HIP_TRY(hipMemcpyAsync(c->d_masks, c->h_small + 256, mbytes, hipMemcpyHostToDevice, s));
-      if (cbytes) HIP_TRY(hipMemcpyAsync(d_cost, c->h_small + 256 + mbytes, cbytes, hipMemcpyHostToDevice, s));
+      // From the first copy on, h_small may be read by a DMA still in flight:
+      // every return before the synchronize below waits for the stream first
+      // (the next schedule writes h_small again; host_free hands it to the
+      // process-wide cache).
+      auto fail_synced = [&](int code) {
+        (void)hipStreamSynchronize(s);
+        return code;
+      };
+      auto hip_ok = [&](hipError_t err, const char* what) {
+        if (err == hipSuccess) return true;
+        set_error(std::string(what) + " failed: " + hipGetErrorString(err));
+        return false;
+      };
+      if (mbytes && !hip_ok(hipMemcpyAsync(c->d_masks, c->h_small + 256, mbytes, hipMemcpyHostToDevice, s),
+                            "schedule mask upload"))
+        return fail_synced(RT_E_DEVICE);
+      if (cbytes && !hip_ok(hipMemcpyAsync(d_cost, c->h_small + 256 + mbytes, cbytes, hipMemcpyHostToDevice, s),
+                            "schedule cost upload"))
+        return fail_synced(RT_E_DEVICE);
       SchedParams sp = sched_params(c, *p, st, tiles, dev_tiles(c, w, h, rank, world), masks, frustum, block_work,
                                     bigP, c->d_sched, c->d_masks, d_cost);
       int e = sched_launch_pixels(sp, s);
       if (e != hipSuccess) {
         set_error(std::string("schedule launch failed: ") + hipGetErrorString((hipError_t)e));
-        return RT_E_DEVICE;
+        return fail_synced(RT_E_DEVICE);
       }
       if (remeasured) {  // every sample's path of the last frame (the measuring render)
         sp.work_max = (const unsigned int*)c->d_meas;
@@ -754,16 +772,18 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
         sp.work_n = st->samples;
       } else if (pilot && st->samples > 0 && st->max_depth > 0) {
         rc = grow(c, &c->d_pilot, &c->pilot_cap, (size_t)local * 1024 * 24 + 256);
-        if (rc) return rc;
+        if (rc) return fail_synced(rc);
         rc = run_pilot(c, *p, &sp, c->d_pilot, s);
-        if (rc) return rc;
+        if (rc) return fail_synced(rc);
       }
       e = sched_launch_blocks(sp, false, s);
       if (e != hipSuccess) {
         set_error(std::string("schedule launch failed: ") + hipGetErrorString((hipError_t)e));
-        return RT_E_DEVICE;
+        return fail_synced(RT_E_DEVICE);
       }
-      HIP_TRY(hipMemcpyAsync(c->h_small, sp.totals, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+      if (!hip_ok(hipMemcpyAsync(c->h_small, sp.totals, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s),
+                  "schedule count read-back"))
+        return fail_synced(RT_E_DEVICE);
       HIP_TRY(hipStreamSynchronize(s));
       memcpy(c->h_totals, c->h_small, 3 * sizeof(int32_t));
       const int nblocks = c->h_totals[0], nsplit = c->h_totals[1];
@@ -781,6 +801,7 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
     // (a rank with no tiles -- more ranks than the frame has tiles -- renders
     // nothing: no scheduler launch, no read-back of counts it never wrote)
     memcpy(c->order_key, key, sizeof key);
+    c->stats.schedules_built += 1;
     // a new key's first frame measures (state 1), the next re-cuts (2 -> 3)
     c->meas_state = remeasured ? 3 : (tn.measure && local > 0 ? 1 : 0);
   }
@@ -1022,9 +1043,24 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   return RT_OK;
 }
 
+// One frame (rt_context_render_async).  key_frames: the frames per launch
+// whose schedule this frame uses -- 1 for a frame of its own; n when it is
+// one of n frames that rt_context_render_frames_async renders one at a time
+// (a measuring frame): the schedule key then stays the batched launch's, so
+// the measured re-cut is the one the next batched launch reuses.
+static int render_one(rt_context* c, int32_t w, int32_t h, const rt_settings* st, int32_t rank, int32_t world,
+                      int32_t layout, float* d_linear, uint8_t* d_rgba, void* stream, rt_counts* counts,
+                      int key_frames);
+
 int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settings* st, int32_t rank,
                             int32_t world, int32_t layout, float* d_linear, uint8_t* d_rgba, void* stream,
                             rt_counts* counts) {
+  return render_one(c, w, h, st, rank, world, layout, d_linear, d_rgba, stream, counts, 1);
+}
+
+static int render_one(rt_context* c, int32_t w, int32_t h, const rt_settings* st, int32_t rank, int32_t world,
+                      int32_t layout, float* d_linear, uint8_t* d_rgba, void* stream, rt_counts* counts,
+                      int key_frames) {
   if (!c || !c->have_scene) {
     set_error("context has no scene");
     return RT_E_INVALID;
@@ -1074,7 +1110,7 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
     p.sample_base = s0;
     p.acc_mode = npass > 1 ? ((pass > 0 ? 1 : 0) | (pass < npass - 1 ? 2 : 0)) : 0;
     if (!wf) {
-      rc = prepare_schedule(c, &p, &ps, s);
+      rc = prepare_schedule(c, &p, &ps, s, key_frames);
       if (rc) return rc;
     }
     p.num_wgs = p.num_blocks;
@@ -1110,7 +1146,12 @@ int rt_context_render_async(rt_context* c, int32_t w, int32_t h, const rt_settin
     }
   }
   HIP_TRY(hipEventRecord(c->ev1, s));
-  if (measuring) c->meas_state = 2;
+  if (measuring) {
+    c->meas_state = 2;
+    c->stats.measuring_frames += 1;
+  }
+  c->stats.frames += 1;
+  c->stats.launches += npass;
   c->last_stream = s;
   c->have_timing = true;
   if (counts) {
@@ -1169,18 +1210,31 @@ int rt_context_set_partition(rt_context* c, const rt_partition* p) {
 // block cutting wants) misjudges whole tiles: with it the slowest of 8 ranks
 // of the headline frame took 1.22x the mean share.  Path lengths are
 // integers of an exact render, so every rank that measures the same frame on
-// its own device derives the same partition.
-static int measured_tile_work(rt_context* c, int w, int h, const rt_settings* st, std::vector<float>* work) {
+// its own device derives the same partition.  (r05) measure_spp < spp: the
+// measuring render takes only the frame's first measure_spp samples of every
+// pixel; a tile weighs its pixels' mean path length over them x spp.  The
+// renderer (rt_renderer_render) plans its partition that way with 16
+// samples, because its first Render -- and every one-shot rt_render with
+// num_devices > 1 -- pays this render before its own frame (at
+// the full 100 samples it cost a whole one-GPU frame); the public
+// rt_partition_balanced, which a caller plans once for many frames, measures
+// every sample (8 ranks of the headline frame, rank shares alone on one GPU:
+// predicted 874 k Mrays/s with all 100 samples, 853 k with 16, 815 k with the
+// one-sample pilot; profiles/r04_rank_share_probe.json, r05_rank_share_probe.json).
+static int measured_tile_work(rt_context* c, int w, int h, const rt_settings* st, int measure_spp,
+                              std::vector<float>* work) {
   hipStream_t s = c->stream;
+  rt_settings sm = *st;
+  sm.samples = std::min(st->samples, measure_spp);
   KParams p;
-  base_params(c, w, h, st, 0, 1, RT_LAYOUT_PACKED_TILES, &p);
-  p.spp = st->samples;
-  p.spp_total = st->samples;
+  base_params(c, w, h, &sm, 0, 1, RT_LAYOUT_PACKED_TILES, &p);
+  p.spp = sm.samples;
+  p.spp_total = sm.samples;
   p.sample_base = 0;
   p.acc_mode = 0;
   p.acc = nullptr;
   p.counts = nullptr;
-  int rc = prepare_schedule(c, &p, st, s);
+  int rc = prepare_schedule(c, &p, &sm, s);
   if (rc) return rc;
   p.num_wgs = p.num_blocks;
   const int ntiles = rt_num_tiles(w, h);
@@ -1216,7 +1270,8 @@ static int measured_tile_work(rt_context* c, int w, int h, const rt_settings* st
                                 big_block_pixels(st->samples, c->tun), buf + o_sched, nullptr, nullptr);
   sp.work_max = meas;
   sp.work_sum = meas + npx;
-  sp.work_n = st->samples;
+  sp.work_n = sm.samples;
+  sp.work_mean = 1;          // (the measured samples' mean, times the frame's spp)
   sp.split_depth = 1 << 30;  // (weights only: no pixel is marked heavy)
   float* d_tw = (float*)(buf + o_tw);
   int e = sched_launch_tile_work(sp, d_tw, s);
@@ -1229,8 +1284,16 @@ static int measured_tile_work(rt_context* c, int w, int h, const rt_settings* st
   return done(RT_OK);
 }
 
+static int partition_balanced_impl(rt_context* c, int32_t w, int32_t h, const rt_settings* st, int32_t world,
+                                   int measure_spp, rt_partition** out);
+
 int rt_partition_balanced(rt_context* c, int32_t w, int32_t h, const rt_settings* st, int32_t world,
                           rt_partition** out) {
+  return partition_balanced_impl(c, w, h, st, world, st ? st->samples : 0, out);
+}
+
+static int partition_balanced_impl(rt_context* c, int32_t w, int32_t h, const rt_settings* st, int32_t world,
+                                   int measure_spp, rt_partition** out) {
   if (!c || !c->have_scene || !out) {
     set_error("rt_partition_balanced: context without a scene, or out is NULL");
     return RT_E_INVALID;
@@ -1250,7 +1313,7 @@ int rt_partition_balanced(rt_context* c, int32_t w, int32_t h, const rt_settings
   if (tn.pilot != 0 && !use_wavefront(c) && st->sky == RT_SKY_NONE && st->samples > 0 &&
       st->samples <= kMaxBlockSamples && st->max_depth > 0) {
     std::vector<float> work(ntiles, 0.0f);
-    rc = measured_tile_work(c, w, h, st, &work);
+    rc = measured_tile_work(c, w, h, st, std::max(1, measure_spp), &work);
     if (rc) return rc;
     PartitionData d;
     d.w = w;
@@ -1384,12 +1447,14 @@ int rt_context_render_frames_async(rt_context* c, int32_t w, int32_t h, const rt
   // one frame at a time where a launch cannot hold several: the wavefront
   // path (host-driven bounce loop), sample passes, a measuring frame
   const int npass = std::max(1, (st->samples + kMaxBlockSamples - 1) / kMaxBlockSamples);
+  // (frame by frame under the batched launch's schedule key: a measuring
+  // frame then measures the schedule the next batched launch uses)
   auto one_by_one = [&]() {
     for (int f = 0; f < nframes; ++f) {
       rt_settings sf = *st;
       sf.seed = seeds[f];
-      int r = rt_context_render_async(c, w, h, &sf, rank, world, layout, d_linear[f], d_rgba ? d_rgba[f] : nullptr,
-                                      stream, nullptr);
+      int r = render_one(c, w, h, &sf, rank, world, layout, d_linear[f], d_rgba ? d_rgba[f] : nullptr, stream,
+                         nullptr, nframes);
       if (r) return r;
     }
     return (int)RT_OK;
@@ -1422,6 +1487,18 @@ int rt_context_render_frames_async(rt_context* c, int32_t w, int32_t h, const rt
   HIP_TRY(hipEventRecord(c->ev1, s));
   c->last_stream = s;
   c->have_timing = true;
+  c->stats.frames += nframes;
+  c->stats.launches += 1;
+  c->stats.batched_launches += 1;
+  return RT_OK;
+}
+
+int rt_context_get_stats(const rt_context* c, rt_context_stats* out) {
+  if (!c || !out) {
+    set_error("context or out is NULL");
+    return RT_E_INVALID;
+  }
+  *out = c->stats;
   return RT_OK;
 }
 
@@ -1448,3 +1525,8 @@ int rt_context_last_kernel_seconds(rt_context* c, double* seconds) {
 }
 
 }  // extern "C"
+
+int rtgo::partition_balanced(rt_context* c, int32_t w, int32_t h, const rt_settings* st, int32_t world,
+                             int measure_spp, rt_partition** out) {
+  return partition_balanced_impl(c, w, h, st, world, measure_spp, out);
+}

@@ -88,6 +88,7 @@ struct SchedParams {
   const unsigned int* work_max;  // measured per local pixel: the longest path (bounces + 1) ...
   const unsigned int* work_sum;  // ... and the sum over the measured samples, or null (no measurement)
   int32_t work_n;              // samples measured per pixel (1..16: a pilot; spp: a whole frame)
+  int32_t work_mean;           // 1: work_n < spp samples of every pixel measured: use their mean (partitions)
   int32_t split_depth;         // a pixel whose longest path has this many bounces is split (measured frames)
   // scratch (sched_layout)
   unsigned long long* pixmask; // per local pixel: 2 u64
@@ -199,6 +200,11 @@ int launch_download(const void* d_src, void* h_dst_mapped, size_t bytes, void* s
 // one workgroup that sleeps for `ms` of device time, then exits (the
 // renderer watchdog's test hook, rt_multi.cpp test_stall)
 int launch_spin(double ms, void* stream);
+// rt_partition_balanced measuring only the first measure_spp samples of every
+// pixel (rt_api.cpp measured_tile_work; the renderer's partitions: 16)
+int partition_balanced(rt_context* c, int32_t w, int32_t h, const rt_settings* st, int32_t world, int measure_spp,
+                       rt_partition** out);
+constexpr int kRendererPartitionSpp = 16;
 int launch_unpack(int32_t W, int32_t H, int32_t world, const void* gathered, size_t share_bytes, size_t rgba_off,
                   float* ol, uint8_t* orgba, void* stream);
 // The same for a partition: slot[t] = {owner rank, local tile} of global tile t;

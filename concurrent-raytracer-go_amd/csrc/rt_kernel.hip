@@ -437,8 +437,14 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
       const Cand co{__shfl(cm.s, ow), p.nt ? __shfl(cm.t, ow) : 0ull};  // (no triangles: cm.t is 0)
       if (lane < n) {
         const d3 pt = mk(rt_bits_to_unit(e.x) * 2 - 1, rt_bits_to_unit(e.y) * 2 - 1, rt_bits_to_unit(e.z) * 2 - 1);
+#if defined(RT_EXP_NO_SOFT_TRACE)  // timing experiments only (scripts/build_variant.sh): wrong images
+        atomicAdd(&sq_unocc[ow], 1);
+#elif defined(RT_EXP_NO_SOFT_NORM)
+        if (!shadow_blocked<kCount>(p, masks, Po, Lo + muls(pt, 0.1), dist, co, stack, c)) atomicAdd(&sq_unocc[ow], 1);
+#else
         if (!shadow_blocked<kCount>(p, masks, Po, normalize(Lo + muls(pt, 0.1)), dist, co, stack, c))
           atomicAdd(&sq_unocc[ow], 1);
+#endif
       }
       head += n;
       __syncthreads();

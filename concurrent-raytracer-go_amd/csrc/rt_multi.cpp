@@ -282,7 +282,7 @@ int renderer_partition(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
                                     st->recursive_reflections, st->soft_shadows, st->sky};
   if (r->part && key == r->part_key) return RT_OK;
   rt_partition* p = nullptr;
-  int rc = rt_partition_balanced(r->ranks[0].ctx, w, h, st, n, &p);
+  int rc = partition_balanced(r->ranks[0].ctx, w, h, st, n, kRendererPartitionSpp, &p);
   if (rc) return rc;
   for (Rank& q : r->ranks) {
     rc = rt_context_set_partition(q.ctx, p);
@@ -578,7 +578,10 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
   // a multi-rank frame waits at most watchdog_s from here (its launches and
   // the gather are all enqueued): a stalled rank or collective ends the wait
   const double deadline = n > 1 && r->watchdog_s > 0 ? t_launch + r->watchdog_s : 0.0;
-  for (int k = 0; k < n; ++k) {
+  // (the other ranks first: the root's stream waits for every rank's share
+  // before its unpack, so a stalled rank is named as itself, not as the root)
+  for (int i = 1; i <= n; ++i) {
+    const int k = i % n;
     Rank& q = r->ranks[k];
     rc = bounded_sync(q.device, q.stream, deadline);
     if (rc == RT_E_TIMEOUT) {

@@ -147,7 +147,7 @@ __global__ __launch_bounds__(256) void sched_est(const SchedParams p) {
   const int lt = (int)(i >> 10), q = (int)(i & 1023);
   float e;
   bool heavy = false;
-  if (p.work_max && p.work_n < p.spp) {
+  if (p.work_max && p.work_n < p.spp && !p.work_mean) {
     // a pilot of a few samples is a noisy estimate of a pixel's mean: take
     // the neighbourhood's longest path
     const unsigned int* L = p.work_max + (size_t)lt * 1024;

@@ -166,6 +166,13 @@ class Stats(ctypes.Structure):
     ]
 
 
+class ContextStats(ctypes.Structure):
+    """rt_context_stats (rt_context_get_stats)."""
+
+    _fields_ = [(n, ctypes.c_int64) for n in ("schedules_built", "measuring_frames", "frames", "launches",
+                                             "batched_launches")]
+
+
 COUNT_FIELDS = [
     "camera_rays",
     "bounce_rays",
@@ -272,6 +279,7 @@ EXPORTED_SYMBOLS = [
     "rt_release_cached_memory",
     "rt_renderer_set_watchdog",
     "rt_renderer_test_stall",
+    "rt_context_get_stats",
 ]
 
 _lib = None
@@ -371,6 +379,7 @@ def lib():
         "rt_release_cached_memory": (ctypes.c_int, []),
         "rt_renderer_set_watchdog": (ctypes.c_int, [vp, ctypes.c_double]),
         "rt_renderer_test_stall": (ctypes.c_int, [vp, i32, ctypes.c_double]),
+        "rt_context_get_stats": (ctypes.c_int, [vp, ctypes.POINTER(ContextStats)]),
         "rt_context_kernel_seconds": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
                                                      ctypes.POINTER(ctypes.c_int64)]),
     }
@@ -734,6 +743,12 @@ class Context:
         n = (ctypes.c_int64 * len(WF_KERNELS))()
         _check(lib().rt_context_kernel_seconds(self._h, s, n))
         return {k: (s[i], int(n[i])) for i, k in enumerate(WF_KERNELS)}
+
+    def stats(self) -> dict:
+        """rt_context_get_stats: schedules built, measuring frames, frames, launches, batched launches."""
+        s = ContextStats()
+        _check(lib().rt_context_get_stats(self._h, ctypes.byref(s)))
+        return {k: getattr(s, k) for k, _ in ContextStats._fields_}
 
     def last_kernel_seconds(self) -> float:
         s = ctypes.c_double()

@@ -372,6 +372,15 @@ int rt_context_render_frames_async(rt_context* ctx, int32_t width, int32_t heigh
                                    int32_t nframes, const uint64_t* seeds, int32_t rank, int32_t world,
                                    int32_t layout, float* const* d_linear, uint8_t* const* d_rgba, void* hip_stream);
 
+/* What a context has done so far (diagnostics): work schedules built (a new
+ * scene, frame, rank or settings key; a measured re-cut counts too),
+ * measuring frames (rt_tuning.measure), frames rendered, render launches,
+ * and the launches that rendered several frames at once. */
+typedef struct {
+  int64_t schedules_built, measuring_frames, frames, launches, batched_launches;
+} rt_context_stats;
+int rt_context_get_stats(const rt_context* ctx, rt_context_stats* out);
+
 /* Packed share of one rank, as rt_comm_gather_tiles_async moves it:
  * [max_local_tiles * 1024 float3][max_local_tiles * 1024 RGBA8] = 16 B per
  * pixel of the largest share (rank 0's).  Render a share with layout

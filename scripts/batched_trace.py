@@ -53,7 +53,7 @@ def main():
     rows = sorted(csv.DictReader(open(paths[0])), key=lambda r: int(r["Start_Timestamp"]))
     names = [r["Kernel_Name"] for r in rows]
     counting = next(i for i, n in enumerate(names) if "render_kernel<true" in n)
-    dom = [r for r in rows[counting + 1:] if r["Kernel_Name"].startswith(kname)]
+    dom = [r for r in rows[counting + 1:] if kname in r["Kernel_Name"]]
     timed = dom[n_warm:n_warm + len(frames)]
     launches = []
     for r, f in zip(timed, frames):

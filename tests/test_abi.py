@@ -3,6 +3,7 @@ every declared symbol, its struct layouts match the Python mirror, the host
 entry points behave as documented, and the render path fails loudly (an
 error code and message, no fallback) when no GPU is present."""
 import ctypes
+import json
 import os
 import re
 import subprocess
@@ -51,6 +52,7 @@ STRUCTS = {
     "rt_stats": (rtgo.Stats, ["render_seconds", "kernel_seconds", "rays_per_second", "pixels_per_second",
                               "objects", "lights"]),
     "rt_counts": (rtgo.Counts, rtgo.COUNT_FIELDS),
+    "rt_context_stats": (rtgo.ContextStats, [n for n, _ in rtgo.ContextStats._fields_]),
 }
 
 
@@ -124,6 +126,7 @@ def test_png_and_ppm_writers(tmp_path):
 
     w, h = 5, 3
     rgba = np.arange(w * h * 4, dtype=np.uint8).reshape(h, w, 4)
+    rgba[:, :, 3] = 255  # every render is opaque (renderer.go:96)
     p = str(tmp_path / "a.png")
     assert rtgo.lib().rt_write_png(p.encode(), rgba.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), w, h) == 0
     data = open(p, "rb").read()
@@ -145,6 +148,17 @@ def test_png_and_ppm_writers(tmp_path):
     assert all(row[0] == 0 for row in rows)
     assert np.array_equal(np.frombuffer(b"".join(row[1:] for row in rows), np.uint8).reshape(h, w, 3),
                           rgba[:, :, :3])
+    # not opaque: RGBA8, the colour un-premultiplied as image/png does
+    q = np.zeros((1, 3, 4), np.uint8)
+    q[0, 1] = (64, 32, 0, 128)
+    q[0, 2] = (10, 20, 30, 255)
+    p2 = str(tmp_path / "b.png")
+    assert rtgo.lib().rt_write_png(p2.encode(), q.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), 3, 1) == 0
+    d2 = open(p2, "rb").read()
+    assert d2[25] == 6
+    j = d2.index(b"IDAT")
+    raw2 = zlib.decompress(d2[j + 4:j + 4 + int.from_bytes(d2[j - 4:j], "big")])
+    assert raw2 == bytes([0, 0, 0, 0, 0, 127, 63, 0, 128, 10, 20, 30, 255])
     q = str(tmp_path / "a.ppm")
     assert rtgo.lib().rt_write_ppm(q.encode(), rgba.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), w, h) == 0
     toks = open(q).read().split()
@@ -181,18 +195,50 @@ def test_cli_fails_loudly_without_gpu(tmp_path):
     assert "device" in (p.stdout + p.stderr).lower()
 
 
-@pytest.mark.parametrize("w,h", [("0", "8"), ("8", "-3")])
-def test_cli_invalid_size_is_decided_before_the_device(tmp_path, w, h):
-    """A zero or negative size fails at SaveImage in the reference (exit 1,
-    'Error saving image'), on any machine: the CLI decides it before it makes
-    device state, so no GPU is needed for that answer."""
+@pytest.mark.parametrize("w,h", [("0", "8"), ("8", "0"), ("-5", "0")])
+def test_cli_zero_size_fails_at_save_image(tmp_path, w, h):
+    """A size with a zero side: image.Rect(0, 0, w, h) is empty, Render makes
+    no tile, SaveImage creates the file (renderer.go:444) and png.Encode
+    refuses the image ("png: invalid format: invalid image size: WxH" with
+    the canonical |w| x |h|), exit 1.  Go prints Render's closing lines and
+    "Saving to:" first.  No device is made (no GPU needed for this answer)."""
+    exe = os.path.join(ROOT, "concurrent-raytracer-go_amd", "build", "raytracer")
+    out = tmp_path / "sub" / "o.png"
+    p = subprocess.run([exe, os.path.join(ROOT, "scenes", "sphere_reflections_light_facing.json"), str(out), w, h],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 1, p.stdout + p.stderr
+    assert "Rendering complete!" in p.stdout and f"Saving to: {out}" in p.stdout
+    aw, ah = abs(int(w)), abs(int(h))
+    assert f"Error saving image: png: invalid format: invalid image size: {aw}x{ah}" in p.stdout
+    assert out.exists() and out.stat().st_size == 0
+
+
+@pytest.mark.parametrize("w,h", [("8", "-3"), ("-5", "-7")])
+def test_cli_negative_size_writes_the_empty_canonical_image(tmp_path, w, h):
+    """A negative side: image.Rect canonicalizes to a |w| x |h| image that no
+    tile touches (createRenderTasks: (n + 31) / 32 <= 0), so every pixel is
+    transparent black; png.Encode writes it as RGBA8 and the CLI exits 0 with
+    benchmark_data.json ("resolution": "WxH" as given).  No device is made."""
+    import struct
+    import zlib
+
     exe = os.path.join(ROOT, "concurrent-raytracer-go_amd", "build", "raytracer")
     out = tmp_path / "o.png"
     p = subprocess.run([exe, os.path.join(ROOT, "scenes", "sphere_reflections_light_facing.json"), str(out), w, h],
                        capture_output=True, text=True, timeout=120)
-    assert p.returncode == 1, p.stdout + p.stderr
-    assert "Error saving image" in p.stdout
-    assert not out.exists()
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "Rendering complete!" in p.stdout and "Benchmark data saved" in p.stdout
+    b = out.read_bytes()
+    aw, ah = abs(int(w)), abs(int(h))
+    assert b[:8] == b"\x89PNG\r\n\x1a\n"
+    iw, ih, depth, ctype = struct.unpack(">IIBB", b[16:26])
+    assert (iw, ih, depth, ctype) == (aw, ah, 8, 6)  # RGBA8: the image is not opaque
+    i = b.index(b"IDAT")
+    n = struct.unpack(">I", b[i - 4:i])[0]
+    raw = zlib.decompress(b[i + 4:i + 4 + n])
+    assert raw == bytes(ah * (1 + aw * 4))  # filter 0, every pixel (0, 0, 0, 0)
+    bd = json.loads((tmp_path / "benchmark_data.json").read_text())
+    assert bd["resolution"] == f"{w}x{h}" and bd["objects"] == 5 and bd["lights"] == 2
 
 
 def test_invalid_arguments_are_rejected_without_a_device():

@@ -78,3 +78,46 @@ def test_split_pixels_across_frames_of_one_renderer():
         ref, ref_rgba, _ = oracle.render(scene, w, h, st)
         assert r.last_linear.tobytes() == ref.astype(np.float32).tobytes(), seed
         assert rgba.tobytes() == ref_rgba.tobytes(), seed
+
+
+@pytest.mark.parametrize("measure", [1, 0], ids=["measure", "pilot_only"])
+def test_measured_schedule_reaches_batched_launches(measure):
+    """rt_tuning.measure with batched frames (rt_context_render_frames_async):
+    the first call renders frame by frame (its first frame measures, the next
+    re-cuts) under the batched launch's own schedule key, so every later call
+    is ONE launch on that schedule with no rebuild (the measuring
+    frames used the one-frame key and the two keys rebuilt each other on
+    every call, so batched launches never happened).  Every frame is the
+    oracle's image."""
+    import torch
+
+    scene = load_case(rtgo, ("json", None))
+    st = make_settings(rtgo, {"samples": 6, "max_depth": 12}, seed=1)
+    w, h, nf = 64, 48, 4
+    ctx = rtgo.Context(0)
+    ctx.set_tuning(rtgo.default_tuning(measure=measure))
+    ctx.set_scene(scene)
+    lin = torch.zeros((nf, w * h * 3), dtype=torch.float32, device="cuda")
+    rgba = torch.zeros((nf, w * h * 4), dtype=torch.uint8, device="cuda")
+    seen = []
+    for call in range(3):
+        seeds = [1 + call * nf + f for f in range(nf)]
+        ctx.render_frames_async(w, h, st, seeds, [lin[f].data_ptr() for f in range(nf)],
+                                [rgba[f].data_ptr() for f in range(nf)], 0)
+        torch.cuda.synchronize()
+        seen.append(ctx.stats())
+        st_f = make_settings(rtgo, {"samples": 6, "max_depth": 12}, seed=seeds[-1])
+        ref, ref_rgba, _ = oracle.render(scene, w, h, st_f)
+        assert lin[nf - 1].cpu().numpy().tobytes() == ref.astype(np.float32).tobytes(), (call, seen[-1])
+        assert rgba[nf - 1].cpu().numpy().tobytes() == ref_rgba.tobytes(), call
+    ctx.close()
+    first, second, third = seen
+    assert second["batched_launches"] == first["batched_launches"] + 1, seen
+    assert third["batched_launches"] == second["batched_launches"] + 1, seen
+    assert third["schedules_built"] == second["schedules_built"] == first["schedules_built"], seen
+    assert third["frames"] == 3 * nf, seen
+    if measure:
+        assert first["measuring_frames"] == 1 and third["measuring_frames"] == 1, seen
+        assert first["batched_launches"] == 0 and first["schedules_built"] == 2, seen  # pilot cut, measured re-cut
+    else:
+        assert first["batched_launches"] == 1 and first["schedules_built"] == 1, seen
