@@ -1089,6 +1089,14 @@ __device__ RT_SOLO_ATTR d3 solo_path(KArg karg, int ow, d3 o, d3 d, d3 T, d3 L, 
 //       spp, tone-mapped (renderer.go:348-367) and written once (float3
 //       linear + RGBA8).
 constexpr int kRound = 128;  // list entries shaded per round (LDS radiance slots)
+// second closest-hit pass of a shade iteration (render_kernel): taken when at
+// least this many lanes are free after the first (0: never).  Measured (r05,
+// K = 100 throughput, two rounds each): never 148.8 k, 4 155.6 k, 8 156.2 k,
+// 16 157.5 k Mrays/s; one frame at a time unchanged (0.74-0.75 ms)
+#ifndef RT_REFILL2_MIN
+#define RT_REFILL2_MIN 16
+#endif
+constexpr int kRefill2Min = RT_REFILL2_MIN;
 
 template <bool kCount, bool kStage, bool kPilot, bool kSky>
 __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KParams pk) {
@@ -1337,148 +1345,176 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     slot[q_][2] = v_.z;                  \
   } while (0)
     for (;;) {
-      const unsigned long long freem = __ballot(!alive);
-      int limit = min(nh, resolved + kRound);
-      if (freem != 0 && next == limit && next < nh) {
-        // the ring is full and lanes are idle: sum every entry before the
-        // earliest one still running (a wave-wide min over the live lanes)
-        // (swizzles within each half-wave, then the two halves' lane 0)
-        int lo = alive ? entry : next;
-        lo = min(lo, __builtin_amdgcn_ds_swizzle(lo, 0x1F | (16 << 10)));
-        lo = min(lo, __builtin_amdgcn_ds_swizzle(lo, 0x1F | (8 << 10)));
-        lo = min(lo, __builtin_amdgcn_ds_swizzle(lo, 0x1F | (4 << 10)));
-        lo = min(lo, __builtin_amdgcn_ds_swizzle(lo, 0x1F | (2 << 10)));
-        lo = min(lo, __builtin_amdgcn_ds_swizzle(lo, 0x1F | (1 << 10)));
-        lo = min(__builtin_amdgcn_readlane(lo, 0), __builtin_amdgcn_readlane(lo, 32));
-        if (lo > resolved) {
-          __syncthreads();
-          resolve_entries(resolved, lo);
-          __syncthreads();
-          resolved = lo;
-          limit = min(nh, resolved + kRound);
-        }
-      }
-      // lanes without a path take the next entries, in lane order
-      const int e = next + lanes_below(freem);
-      if (!alive && e < limit) {
-        KArg k = fresh();
-        const BlockLoc loc = block_loc(k, block_of(k));
-        const int id = entry_id(e), ns = loc.ns;
-        const int p = id / ns, s = k->sample_base + loc.s0 + id - p * ns;
-        const int tp = loc.p0 + p;
-        Counters nc;  // phase 1 counted this camera ray and its draws
-        camera_ray<false>(k, loc.tx * 32 + (tp & 31), loc.ty * 32 + (tp >> 5), s, rng, o, d, nc);
-        entry = e;
-        T = mk(1, 1, 1);
-        set_path_L(mk(0, 0, 0));
-        depth = 0;
-        alive = true;
-      }
-      next = min(limit, next + __popcll(freem));
-      if (__ballot(alive) == 0) {  // wave-uniform
-        if (next >= nh) break;     // every entry done
-        continue;                  // ring full of finished entries: resolve, then refill
-      }
-#ifdef RT_WG_TIMING
-      ++dbg_iter;
-      dbg_alive += __popcll(__ballot(alive));
-      {
-        const unsigned long long now = __builtin_amdgcn_s_memtime();
-        if (dbg_bprev >= 0) dbg_bclk[dbg_bprev] += now - dbg_bts;
-        const int nal = __popcll(__ballot(alive));
-        dbg_bprev = nal == 1 ? 0 : (nal == 2 ? 1 : (nal <= 4 ? 2 : (nal <= 8 ? 3 : 4)));
-        dbg_bcnt[dbg_bprev] += 1;
-        dbg_bts = now;
-      }
-      if (dbg_iter % 4 == 0 && dbg_iter / 4 < 16 && lane == 0 && fresh()->dbg)
-        fresh()->dbg[(size_t)blockIdx.x * kDbgStride + 16 + dbg_iter / 4] = __builtin_amdgcn_s_memrealtime();
-      const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
-#endif
-      if constexpr (kStage && !kCount && !kPilot) {
-        // one path left (no free lane found an entry to start): the whole
-        // wave runs it to its end (solo_path)
-        const unsigned long long am = __ballot(alive);
-        // (two or three paths run one after the other this way measured
-        // slower: 0.79 / 0.93 vs 0.78 ms)
-        if (__popcll(am) == 1 && hot<kStage>().masks) {
-          const d3 Lr = solo_path<kSky>(fresh(), __builtin_ctzll(am), o, d, T, path_L(), rng.x, depth, stack);
-          if (lane == __builtin_ctzll(am)) {
-            const int q = entry & (kRound - 1);
-            slot[q][0] = Lr.x;
-            slot[q][1] = Lr.y;
-            slot[q][2] = Lr.z;
-            alive = false;
-          }
-          continue;
-        }
-      }
-
-      // (1) closest hit (hitWorld, renderer.go:170)
+      // (1) closest hit (hitWorld, renderer.go:170), in up to two passes: a
+      // lane whose ray missed (or reached the depth cut-off) finishes at once
+      // and, while other lanes go on to light their hits, takes the next
+      // entry (its camera ray hits: phase 1 found a hit for it) and runs that
+      // closest hit in a second pass -- so lighting and scatter, the bulk of
+      // an iteration, run on the lanes of both passes' hits instead of
+      // idling every lane whose ray missed (57 % of the headline's traced
+      // rays hit: the lighting used to run on ~60 % of the lanes)
       bool shade = false, front = false, fin = false;
       d3 P = mk(0, 0, 0), N = mk(0, 0, 0);
       int mi = 0, self = -1;
       HitSel hs;
-      bool wide_q = false, wide_found = false, wide_fb = false;
-      if constexpr (kStage) {  // wave-uniform: few paths left -> helpers
-        const Hot h = hot<kStage>();
-        const bool need = alive && depth < h.max_depth;
-        const unsigned long long qm = __ballot(need);
-        const int nq = __popcll(qm);
-        // (from 16 spheres on: below that the group set-up and merge cost more
-        // than the short scan they split; measured on the 5-sphere scene)
-        if (h.g.nt == 0 && h.g.ns >= 16 && nq > 0 && nq <= 16) {
-          // (kCount: helpers count their sphere tests, primary queries included)
-          wide_found = closest_wide<kCount>(h.g, need, qm, nq, o, d, hs, wide_fb, c);
-          wide_q = true;
+      int outer = 0;  // 1: continue the shade loop, 2: leave it
+#ifdef RT_WG_TIMING
+      unsigned long long ts0 = 0;
+#endif
+      for (int pass = 0;; ++pass) {
+        const unsigned long long freem = __ballot(!alive);
+        int limit = min(nh, resolved + kRound);
+        if (freem != 0 && next == limit && next < nh) {
+          // the ring is full and lanes are idle: sum every entry before the
+          // earliest one still running (a wave-wide min over the live lanes)
+          // (swizzles within each half-wave, then the two halves' lane 0)
+          int lo = alive ? entry : next;
+          lo = min(lo, __builtin_amdgcn_ds_swizzle(lo, 0x1F | (16 << 10)));
+          lo = min(lo, __builtin_amdgcn_ds_swizzle(lo, 0x1F | (8 << 10)));
+          lo = min(lo, __builtin_amdgcn_ds_swizzle(lo, 0x1F | (4 << 10)));
+          lo = min(lo, __builtin_amdgcn_ds_swizzle(lo, 0x1F | (2 << 10)));
+          lo = min(lo, __builtin_amdgcn_ds_swizzle(lo, 0x1F | (1 << 10)));
+          lo = min(__builtin_amdgcn_readlane(lo, 0), __builtin_amdgcn_readlane(lo, 32));
+          if (lo > resolved) {
+            __syncthreads();
+            resolve_entries(resolved, lo);
+            __syncthreads();
+            resolved = lo;
+            limit = min(nh, resolved + kRound);
+          }
         }
-      }
-      if (alive) {
-        const Hot h = hot<kStage>();
-        const Geo& gg = h.g;
-        bool done = depth >= h.max_depth;  // traceRay depth cut-off: contributes 0
-        bool missed = false;
-        if (!done) {
-          if (kCount && depth == 0) {  // phase 1 counted the primary query
-            Counters nc;
-            done = (wide_q && !wide_fb) ? !wide_found : !closest_hit<false>(gg, o, d, hs, stack, all, nc);
+        // lanes without a path take the next entries, in lane order
+        const int e = next + lanes_below(freem);
+        if (!alive && e < limit) {
+          KArg k = fresh();
+          const BlockLoc loc = block_loc(k, block_of(k));
+          const int id = entry_id(e), ns = loc.ns;
+          const int p = id / ns, s = k->sample_base + loc.s0 + id - p * ns;
+          const int tp = loc.p0 + p;
+          Counters nc;  // phase 1 counted this camera ray and its draws
+          camera_ray<false>(k, loc.tx * 32 + (tp & 31), loc.ty * 32 + (tp >> 5), s, rng, o, d, nc);
+          entry = e;
+          T = mk(1, 1, 1);
+          set_path_L(mk(0, 0, 0));
+          depth = 0;
+          alive = true;
+        }
+        next = min(limit, next + __popcll(freem));
+        if (pass == 0) {
+          if (__ballot(alive) == 0) {  // wave-uniform
+            outer = next >= nh ? 2 : 1;  // every entry done / ring full of finished entries: resolve, then refill
+            break;
+          }
+#ifdef RT_WG_TIMING
+          ++dbg_iter;
+          dbg_alive += __popcll(__ballot(alive));
+          {
+            const unsigned long long now = __builtin_amdgcn_s_memtime();
+            if (dbg_bprev >= 0) dbg_bclk[dbg_bprev] += now - dbg_bts;
+            const int nal = __popcll(__ballot(alive));
+            dbg_bprev = nal == 1 ? 0 : (nal == 2 ? 1 : (nal <= 4 ? 2 : (nal <= 8 ? 3 : 4)));
+            dbg_bcnt[dbg_bprev] += 1;
+            dbg_bts = now;
+          }
+          if (dbg_iter % 4 == 0 && dbg_iter / 4 < 16 && lane == 0 && fresh()->dbg)
+            fresh()->dbg[(size_t)blockIdx.x * kDbgStride + 16 + dbg_iter / 4] = __builtin_amdgcn_s_memrealtime();
+          ts0 = __builtin_amdgcn_s_memtime();
+#endif
+          if constexpr (kStage && !kCount && !kPilot) {
+            // one path left (no free lane found an entry to start): the whole
+            // wave runs it to its end (solo_path)
+            const unsigned long long am = __ballot(alive);
+            // (two or three paths run one after the other this way measured
+            // slower: 0.79 / 0.93 vs 0.78 ms)
+            if (__popcll(am) == 1 && hot<kStage>().masks) {
+              const d3 Lr = solo_path<kSky>(fresh(), __builtin_ctzll(am), o, d, T, path_L(), rng.x, depth, stack);
+              if (lane == __builtin_ctzll(am)) {
+                const int q = entry & (kRound - 1);
+                slot[q][0] = Lr.x;
+                slot[q][1] = Lr.y;
+                slot[q][2] = Lr.z;
+                alive = false;
+              }
+              outer = 1;
+              break;
+            }
+          }
+        }  // pass 0
+
+        bool wide_q = false, wide_found = false, wide_fb = false;
+        if constexpr (kStage) {  // wave-uniform: few paths left -> helpers
+          const Hot h = hot<kStage>();
+          const bool need = alive && !shade && depth < h.max_depth;
+          const unsigned long long qm = __ballot(need);
+          const int nq = __popcll(qm);
+          // (from 16 spheres on: below that the group set-up and merge cost more
+          // than the short scan they split; measured on the 5-sphere scene)
+          if (h.g.nt == 0 && h.g.ns >= 16 && nq > 0 && nq <= 16) {
+            // (kCount: helpers count their sphere tests, primary queries included)
+            wide_found = closest_wide<kCount>(h.g, need, qm, nq, o, d, hs, wide_fb, c);
+            wide_q = true;
+          }
+        }
+        if (alive && !shade) {
+          const Hot h = hot<kStage>();
+          const Geo& gg = h.g;
+          bool done = depth >= h.max_depth;  // traceRay depth cut-off: contributes 0
+          bool missed = false;
+          if (!done) {
+            if (kCount && depth == 0) {  // phase 1 counted the primary query
+              Counters nc;
+              done = (wide_q && !wide_fb) ? !wide_found : !closest_hit<false>(gg, o, d, hs, stack, all, nc);
+            } else {
+              cnt<kCount>(c, C_BOUNCE);
+              done = (wide_q && !wide_fb) ? !wide_found
+                                          : !closest_hit<kCount>(gg, o, d, hs, stack, all, c);  // miss -> black
+            }
+            missed = done;
+          }
+          if (done) {
+            if constexpr (kSky) {  // an opted-in sky instead of black (rt_settings.sky)
+              if (missed) set_path_L(path_L() + mul(T, sky_color(fresh()->sky, d)));
+            }
+            if constexpr (kPilot) {  // a measuring render: the pixel's longest path and its bounces
+              KArg k = fresh();
+              const BlockLoc loc = block_loc(k, block_of(k));
+              const size_t px = (size_t)loc.lt * 1024 + loc.p0 + entry_id(entry) / loc.ns;
+              atomicMax(k->work_max + px, (unsigned)depth + 1u);
+              atomicAdd(k->work_sum + px, (unsigned)depth + 1u);
+            }
+            alive = false;  // finished: its radiance is in its slot, the lane is free for the second pass
           } else {
-            cnt<kCount>(c, C_BOUNCE);
-            done = (wide_q && !wide_fb) ? !wide_found
-                                        : !closest_hit<kCount>(gg, o, d, hs, stack, all, c);  // miss -> black
-          }
-          missed = done;
-        }
-        if (done) {
-          fin = true;
-          if constexpr (kSky) {  // an opted-in sky instead of black (rt_settings.sky)
-            if (missed) set_path_L(path_L() + mul(T, sky_color(fresh()->sky, d)));
-          }
-        } else {
-          shade = true;
-          cnt<kCount>(c, C_SHADE);
-          // HitRecord of the closest primitive (sphere.go:42-58, triangle.go:68-81)
-          if (!hs.is_tri) {
-            const DSphere& S0 = gg.spheres[hs.idx];
-            const double t = hs.num / len2(d);
-            P = o + muls(d, t);
-            d3 outward = divs(P - ld3(S0.c), S0.r);
-            front = dot(d, outward) < 0;
-            N = front ? outward : neg(outward);
-            mi = S0.mat;
-            self = S0.obj;
-          } else {
-            const DTri& T0 = gg.tris[hs.idx];
-            P = o + muls(d, hs.num);
-            double w = 1.0 - hs.u - hs.v;
-            d3 n = ld3(T0.n);
-            N = normalize((muls(n, w) + muls(n, hs.u)) + muls(n, hs.v));
-            front = dot(d, N) < 0;
-            if (!front) N = neg(N);
-            mi = T0.mat;
-            self = T0.obj;
+            shade = true;
+            cnt<kCount>(c, C_SHADE);
+            // HitRecord of the closest primitive (sphere.go:42-58, triangle.go:68-81)
+            if (!hs.is_tri) {
+              const DSphere& S0 = gg.spheres[hs.idx];
+              const double t = hs.num / len2(d);
+              P = o + muls(d, t);
+              d3 outward = divs(P - ld3(S0.c), S0.r);
+              front = dot(d, outward) < 0;
+              N = front ? outward : neg(outward);
+              mi = S0.mat;
+              self = S0.obj;
+            } else {
+              const DTri& T0 = gg.tris[hs.idx];
+              P = o + muls(d, hs.num);
+              double w = 1.0 - hs.u - hs.v;
+              d3 n = ld3(T0.n);
+              N = normalize((muls(n, w) + muls(n, hs.u)) + muls(n, hs.v));
+              front = dot(d, N) < 0;
+              if (!front) N = neg(N);
+              mi = T0.mat;
+              self = T0.obj;
+            }
           }
         }
-      }
+        // a second pass when enough lanes are free and entries are left
+        if (pass > 0 || kRefill2Min <= 0 || __popcll(__ballot(!alive)) < kRefill2Min || next >= nh) break;
+      }  // passes
+      if (outer == 1) continue;
+      if (outer == 2) break;
+
 #ifdef RT_WG_TIMING
       const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
       dbg_hit += ts1 - ts0;

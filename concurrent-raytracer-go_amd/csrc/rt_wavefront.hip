@@ -1042,6 +1042,9 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
 // (One ray per thread, the cone's 16 lanes sharing its loads and a ballot
 // for the count: 41 vs 31 ms per C4 frame; rays outer, each entry read once
 // and the candidates re-read from L2 per ray: 51 vs 31 ms.)
+#ifndef RT_LISTTEST_REGS
+#define RT_LISTTEST_REGS 1
+#endif
 template <bool kCount>
 __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
   const Dense dn = dense(p.ctl->list_cnt);  // (entries: 16 per cone, so no cone spans two shards)
@@ -1082,7 +1085,26 @@ __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
     const size_t at = dense_at(dn, 16 * j, p.soft_cap);
     const size_t sh = at / (size_t)p.soft_cap, off = at - sh * (size_t)p.soft_cap;
     const uint4* e = reinterpret_cast<const uint4*>(p.softq) + sh * (size_t)p.soft_cap + (p.soft_cap - off - 16);
+    // (r05) the cone's 16 entries (256 contiguous bytes) are read once, all
+    // loads issued together, and kept in registers for every candidate group:
+    // re-reading entry r per group let the lines of a wave's 64 cones (16 KB)
+    // fall out of L2 between the reads -- the soft queue is GBs per frame --
+    // so the kernel fetched 140 GB per C4 frame for ~20 GB of entries
+    // (profiles/r05_pmc_traffic.json)
+#if RT_LISTTEST_REGS
+    uint32_t ux[16], uy[16], uz[16];
+    uint32_t key = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint4 er = e[r];
+      if (r == 0) key = er.x;
+      ux[r] = er.y;
+      uy[r] = er.z;
+      uz[r] = er.w;
+    }
+#else
     const uint32_t key = e[0].x;
+#endif
     const uint32_t slot = key / (uint32_t)p.nl, li = key - slot * (uint32_t)p.nl;
     const d3 o = ld_P(p, (int)slot);
     d3 ldir;
@@ -1101,10 +1123,15 @@ __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
         ls[k] = p.g.spheres[valid[k] ? id[k] : 0];
       }
       if (!valid[0]) break;
+#pragma unroll 1
       for (int r = 0; r < 16; ++r) {
         if (blocked & (1u << r)) continue;
+#if RT_LISTTEST_REGS  // (a wave-uniform index: v_movrels, no scratch)
+        const d3 pt = mk(rt_bits_to_unit(ux[r]) * 2 - 1, rt_bits_to_unit(uy[r]) * 2 - 1, rt_bits_to_unit(uz[r]) * 2 - 1);
+#else
         const uint4 er = e[r];
         const d3 pt = mk(rt_bits_to_unit(er.y) * 2 - 1, rt_bits_to_unit(er.z) * 2 - 1, rt_bits_to_unit(er.w) * 2 - 1);
+#endif
         const d3 d = normalize(ldir + muls(pt, 0.1));
         const double av = len2(d), inv_a = approx_rcp(av);
         bool b = false;

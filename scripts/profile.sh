@@ -3,7 +3,7 @@
 # commands and PMC passes (FETCH_SIZE, WRITE_SIZE) of every config's
 # workload, reduced to HBM bytes of its dominant kernel.
 # usage: scripts/profile.sh r05   (writes gpurun_out/profiles_r05/*; copy them into profiles/)
-#   PROFILE_PARTS="driver onefr c4 pmc"  (default: all four)
+#   PROFILE_PARTS="driver onefr c4 pmc"  (default: all four); PMC_CONFIGS="c2 c2b c3 c4 c5" (default)
 set -eu
 R=${1:-r05}
 PARTS=${PROFILE_PARTS:-driver onefr c4 pmc}
@@ -35,7 +35,7 @@ if has c4; then
   cp "$(find gpurun_out/prof_${R}_c4trace -name '*kernel_stats.csv' | head -1)" $O/${R}_c4_kernel_stats.csv
 fi
 if has pmc; then
-  for cfg in c2 c2b c3 c4 c5; do
+  for cfg in ${PMC_CONFIGS:-c2 c2b c3 c4 c5}; do
     c=$cfg; n=5; fpl=1
     [ $cfg = c2b ] && { c=c2; n=2; fpl=10; }
     [ $cfg = c4 ] && n=2
