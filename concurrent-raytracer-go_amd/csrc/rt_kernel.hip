@@ -48,13 +48,22 @@
 #endif
 // cooperative soft shadows when at most this many lanes need them (measured
 // best of 0/2/4/8 in round 1; 4 and 16 within noise in round 2)
-constexpr int kCoopMax = 8;
+#ifndef RT_COOP_MAX
+#define RT_COOP_MAX 8
+#endif
+constexpr int kCoopMax = RT_COOP_MAX;
 // soft_queue: the owners still drawing finish cooperatively once at most
 // this many are left (measured best of 0/1/2/4, r03)
-constexpr int kSqTail = 2;
+#ifndef RT_SQ_TAIL
+#define RT_SQ_TAIL 2
+#endif
+constexpr int kSqTail = RT_SQ_TAIL;
 // soft_queue: rejection tries per pass of its loop (measured best of 1..6
 // within the LDS budget, r03)
-constexpr int kSqTries = 2;
+#ifndef RT_SQ_TRIES
+#define RT_SQ_TRIES 2
+#endif
+constexpr int kSqTries = RT_SQ_TRIES;
 
 namespace rtgo {
 
@@ -342,6 +351,12 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
   sq_unocc[lane] = 0;
   int need = need_soft ? 16 : 0, free_rays = 0;  // free_rays: points of an owner with nothing to trace
   int head = 0, tail = 0;  // wave-uniform ring positions
+#ifdef RT_EXP_FREE_SKIP  // timing experiment only: an owner with nothing to trace draws no tries (wrong stream)
+  if (need > 0 && !trace) {
+    free_rays = 16;
+    need = 0;
+  }
+#endif
   for (;;) {
     // kSqTries tries per pass: the later tries are drawn ahead and each
     // is consumed only when the owner still needs a point after the ones
@@ -648,26 +663,26 @@ __device__ __forceinline__ bool solo_closest(const Geo& g, d3 o, d3 d, HitSel& h
 }
 
 // ---- parallel direct lighting of a lone path (solo_lights)
-// The tries of a bounce's random stream, evaluated ahead: try k of the
+// The tries of a bounce's soft-shadow streams, evaluated ahead: try k of the
 // stream whose state is x uses draws 3k, 3k+1, 3k+2 (RandomVec3InUnitSphere,
-// vector.go:132-139); lane h holds tries h and 64 + h.  The soft shadows of
-// calculateSmartShadow take their points from this stream in light order
-// (each light whose hard ray is clear: the next 16 accepted tries), so the
-// tries of every light are known once the hard rays are, and all lights'
-// soft rays can be traced at once.  The scatter draws follow them.
+// vector.go:132-139); lane h holds try h of light 0's stream (a) and of light
+// 1's (b) (spec v4, include/rt_rng.h: each (sample, bounce, light) has a
+// stream of its own).  A light whose hard ray is clear takes the first 16
+// accepted tries of its stream, so all lights' soft rays are known once the
+// hard rays are, and can be traced at once.
 struct SoloTries {
-  uint32_t a0, a1, a2, b0, b1, b2;  // the draws of tries h and 64 + h
-  unsigned long long ma, mb;        // accepted tries 0..63 / 64..127 (wave-uniform)
+  uint32_t a0, a1, a2, b0, b1, b2;  // the draws of try h of stream a, of stream b
+  unsigned long long ma, mb;        // accepted tries 0..63 of each (wave-uniform)
 };
-__device__ __forceinline__ SoloTries solo_tries(uint64_t x, uint64_t jA, uint64_t jC, uint64_t jA64, uint64_t jC64) {
+__device__ __forceinline__ SoloTries solo_tries(uint64_t xa, uint64_t xb, uint64_t jA, uint64_t jC) {
   SoloTries t;
-  uint64_t s = jA * x + jC;  // state before draw 3h
+  uint64_t s = jA * xa + jC;  // state before draw 3h of stream a
   t.a0 = rt_pcg_out(s);
   s = s * RT_PCG_MULT + RT_PCG_INC;
   t.a1 = rt_pcg_out(s);
   s = s * RT_PCG_MULT + RT_PCG_INC;
   t.a2 = rt_pcg_out(s);
-  s = jA * (jA64 * x + jC64) + jC;  // state before draw 3(64 + h)
+  s = jA * xb + jC;  // ... of stream b
   t.b0 = rt_pcg_out(s);
   s = s * RT_PCG_MULT + RT_PCG_INC;
   t.b1 = rt_pcg_out(s);
@@ -677,46 +692,16 @@ __device__ __forceinline__ SoloTries solo_tries(uint64_t x, uint64_t jA, uint64_
   t.mb = __ballot(unit_ball_accept(t.b0, t.b1, t.b2));
   return t;
 }
-// The index after the 16th accepted try at or after `from` (< 128), or -1
-// when the 128 evaluated tries do not hold 16 more (wave-uniform).
-// position of the n-th set bit (n >= 1) of m, which has at least n
-__device__ __forceinline__ int nth_set_bit(unsigned long long m, int n) {
-  int pos = 0;
-#pragma unroll
-  for (int w = 32; w >= 1; w >>= 1) {
-    const int c = __popcll(m & ((1ull << w) - 1ull));
-    if (n > c) {
-      n -= c;
-      m >>= w;
-      pos += w;
-    }
-  }
-  return pos;
-}
-__device__ __forceinline__ int solo_take16(const SoloTries& t, int from) {
-  // tries [from, 64) of ma, then [max(from, 64), 128) of mb
-  const unsigned long long a = from < 64 ? t.ma >> from : 0ull;
-  const int ca = __popcll(a);
-  if (ca >= 16) return from + nth_set_bit(a, 16) + 1;
-  const int fb = from > 64 ? from - 64 : 0;
-  const unsigned long long b = t.mb >> fb;
-  if (ca + __popcll(b) < 16) return -1;
-  return 64 + fb + nth_set_bit(b, 16 - ca) + 1;
-}
-// The index after the 16th and after the 32nd accepted try of the 128 (-1:
-// fewer): every lane ranks its two tries among the accepted ones (v_mbcnt)
-// and four ballots find the 16th and the 32nd -- instead of solo_take16's
-// bit-serial search on the critical path (the lights' soft rays take the
-// accepted tries in order: light 0 the first 16, light 1 the next 16, or
-// the first 16 when light 0 takes none).
-__device__ __forceinline__ void solo_take_16_32(const SoloTries& t, int& i16, int& i32) {
+// The index after the 16th accepted try of each stream's 64 (-1: fewer):
+// every lane ranks its tries among the accepted ones (v_mbcnt) and two
+// ballots find the 16th of each
+__device__ __forceinline__ void solo_take16(const SoloTries& t, int& ia, int& ib) {
   const int lane = (int)(threadIdx.x & 63);
   const bool aa = (t.ma >> lane) & 1ull, ab = (t.mb >> lane) & 1ull;
-  const int ra = lanes_below(t.ma) + 1, rb = __popcll(t.ma) + lanes_below(t.mb) + 1;  // ranks, 1-based
-  const unsigned long long a16 = __ballot(aa && ra == 16), b16 = __ballot(ab && rb == 16);
-  const unsigned long long a32 = __ballot(aa && ra == 32), b32 = __ballot(ab && rb == 32);
-  i16 = a16 ? __builtin_ctzll(a16) + 1 : (b16 ? 65 + __builtin_ctzll(b16) : -1);
-  i32 = a32 ? __builtin_ctzll(a32) + 1 : (b32 ? 65 + __builtin_ctzll(b32) : -1);
+  const unsigned long long a16 = __ballot(aa && lanes_below(t.ma) + 1 == 16);
+  const unsigned long long b16 = __ballot(ab && lanes_below(t.mb) + 1 == 16);
+  ia = a16 ? __builtin_ctzll(a16) + 1 : -1;
+  ib = b16 ? __builtin_ctzll(b16) + 1 : -1;
 }
 
 // RT_WG_TIMING builds: s_memtime clocks of a lone path's bounce by section
@@ -775,7 +760,7 @@ __device__ __forceinline__ KArg launder(KArg k) {
 }
 template <bool kSky>
 __device__ RT_SOLO_ATTR d3 solo_path(KArg karg, int ow, d3 o, d3 d, d3 T, d3 L, uint64_t rx, int depth,
-                                     int* stack) {
+                                     uint64_t skey, int* stack) {
   const int lane = (int)(threadIdx.x & 63);
   o = rl3(o, ow);
   d = rl3(d, ow);
@@ -790,18 +775,14 @@ __device__ RT_SOLO_ATTR d3 solo_path(KArg karg, int ow, d3 o, d3 d, d3 T, d3 L, 
   // the parallel lighting form (solo_lights): sphere-only scenes with one or
   // two lights, a (light, sphere) pair per lane
   bool par;
-  // jump coefficients of try `lane` and of try 64 (solo_tries), held in
-  // VGPRs for the lone path's bounces (the state at any try k < 64 of the
-  // stream is then a readlane away: no memory access per bounce)
-  uint64_t jA, jC, jA64, jC64;
+  // jump coefficients of try `lane` (solo_tries), held in VGPRs for the
+  // lone path's bounces: no memory access per bounce
+  uint64_t jA, jC;
   {
     const Hot h0 = hot<true>(launder(karg));
     par = h0.g.nt == 0 && h0.nl >= 1 && h0.nl <= 2 && h0.nl * h0.g.ns <= 64;
     jA = h0.jump[2 * lane];
     jC = h0.jump[2 * lane + 1];
-    jA64 = h0.jump[128];
-    jC64 = h0.jump[129];
-    asm volatile("" : "+v"(jA64), "+v"(jC64));
   }
 #ifdef RT_WG_TIMING
   solo_clk[7] += 1;
@@ -856,7 +837,7 @@ __device__ RT_SOLO_ATTR d3 solo_path(KArg karg, int ow, d3 o, d3 d, d3 T, d3 L, 
       // operations and sums as the loop below, so the same bits)
       const int nl = h.nl, ns = g.ns;
       SoloTries tr{};
-      if (h.soft) tr = solo_tries(rng.x, jA, jC, jA64, jC64);
+      if (h.soft) tr = solo_tries(rt_soft_state(skey, (uint32_t)depth, 0u), rt_soft_state(skey, (uint32_t)depth, 1u), jA, jC);
       SOLO_S(8);
       d3 lvd = mk(0, 0, 0);
       double lvl = 0;
@@ -910,62 +891,50 @@ __device__ RT_SOLO_ATTR d3 solo_path(KArg karg, int ow, d3 o, d3 d, d3 T, d3 L, 
       const bool lit0 = litm & 1ull, lit1 = (litm >> 1) & 1ull;
       const bool occ0 = (blks & sm) != 0, occ1 = ((blks >> ns) & sm) != 0;
       const bool need0 = lit0 && !occ0 && h.soft, need1 = lit1 && !occ1 && h.soft;
-      // soft rays: light 0 takes the 16 accepted tries from try 0, light 1 the
-      // 16 after those (a light without soft rays draws nothing)
-      int i16 = -1, i32 = -1;
-      solo_take_16_32(tr, i16, i32);
-      const int e0 = need0 ? i16 : 0;
-      const int e1 = need1 && e0 >= 0 ? (need0 ? i32 : i16) : e0;
+      // soft rays: each light takes the first 16 accepted tries of its own
+      // stream (spec v4; a light without soft rays draws nothing)
+      int i16a = -1, i16b = -1;
+      solo_take16(tr, i16a, i16b);
+      const int e0 = need0 ? i16a : 0, e1 = need1 ? i16b : 0;
       SOLO_T(2);
       int un0 = 16, un1 = 16;
       if (e0 >= 0 && e1 >= 0) {
         int cnt0 = 0, cnt1 = 0;
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {  // try lane, then try 64 + lane
-          if (half == 1 && e0 <= 64 && e1 <= 64) break;  // (the lights took tries of the first 64 only)
-          const int k = lane + 64 * half;
+        for (int half = 0; half < 2; ++half) {  // light 0 (stream a), then light 1 (stream b)
+          if (half == 1 && !need1) break;
+          if (half == 0 && !need0) continue;
           const bool acc = ((half ? tr.mb : tr.ma) >> lane) & 1ull;
-          const bool in0 = need0 && k < e0, in1 = need1 && k >= e0 && k < e1;
-          const int li = in1 ? 1 : 0;
-          const d3 lD = mk(__shfl(lvd.x, li), __shfl(lvd.y, li), __shfl(lvd.z, li));
-          const double lT = __shfl(lvl, li);
+          const bool in = lane < (half ? e1 : e0);
+          const d3 lD = mk(__shfl(lvd.x, half), __shfl(lvd.y, half), __shfl(lvd.z, half));
+          const double lT = __shfl(lvl, half);
           bool occ = false;
-          if (acc && (in0 || in1)) {
+          if (acc && in) {
             const d3 pt = half ? unit_ball_point(tr.b0, tr.b1, tr.b2) : unit_ball_point(tr.a0, tr.a1, tr.a2);
             const d3 sd = normalize(lD + muls(pt, 0.1));
             const double a = len2(sd);
             const double ia = approx_rcp(a);
             // (every candidate, no early exit: their loads issue together)
-            for (unsigned long long b = in1 ? cm1 : cm0; b; b &= b - 1) {
+            for (unsigned long long b = half ? cm1 : cm0; b; b &= b - 1) {
               double num;
               occ = (sphere_query(g.spheres[__builtin_ctzll(b)], P, sd, a, ia, 0.001, lT, num) != 0) || occ;
             }
           }
-          cnt0 += __popcll(__ballot(acc && in0 && !occ));
-          cnt1 += __popcll(__ballot(acc && in1 && !occ));
+          (half ? cnt1 : cnt0) = __popcll(__ballot(acc && in && !occ));
           if (half == 0) SOLO_S(12);
         }
         SOLO_S(13);
         un0 = cnt0;
         un1 = cnt1;
-        // the stream continues after the last try the lights took
-        const int used = e1;
-        if (used > 0) {  // the state before draw 3 used: jumps by 64 tries, then by used mod 64
-          uint64_t xb = rng.x;
-          for (int k = used; k >= 64; k -= 64) xb = rl64(jA64, 0) * xb + rl64(jC64, 0);
-          const int u = used & 63;
-          rng.x = rl64(jA, u) * xb + rl64(jC, u);
-        }
       } else {
-        // (the 128 tries did not hold them: the lights' soft rays one light
-        // after the other from the stream, as below)
+        // (64 tries of a stream did not hold 16 points: that light's soft
+        // rays cooperatively from its stream, as below)
         for (int li = 0; li < 2; ++li) {
           if (!(li ? need1 : need0)) continue;
           const Cand cl{li ? cm1 : cm0, 0ull};
-          const CoopOut r = soft_coop<false>(g, true, cl.s != 0, P, rl3(lvd, li), rld(lvl, li), cl, rng.x, h.jump,
-                                             stack, c);
+          const CoopOut r = soft_coop<false>(g, true, cl.s != 0, P, rl3(lvd, li), rld(lvl, li), cl,
+                                             rt_soft_state(skey, (uint32_t)depth, (uint32_t)li), h.jump, stack, c);
           (li ? un1 : un0) = r.unocc;
-          rng.x = r.x;
         }
       }
       SOLO_T(3);
@@ -1032,9 +1001,15 @@ __device__ RT_SOLO_ATTR d3 solo_path(KArg karg, int ow, d3 o, d3 d, d3 T, d3 L, 
                            __builtin_isfinite(m->albedo[0] + m->albedo[1] + m->albedo[2]) &&
                            __builtin_isfinite(m->metallic);
         const bool trace = (cm.s | cm.t) != 0 && !quiet;
-        const CoopOut r = soft_coop<false>(g, true, trace, P, ldir, ldist, cm, rng.x, h.jump, stack, c);
-        unocc = r.unocc;
-        rng.x = r.x;
+        // (spec v4: the points come from the light's own stream; rays that
+        // cannot be blocked need none of them)
+        if (trace) {
+          const CoopOut r = soft_coop<false>(g, true, true, P, ldir, ldist, cm,
+                                             rt_soft_state(skey, (uint32_t)depth, (uint32_t)li), h.jump, stack, c);
+          unocc = r.unocc;
+        } else {
+          unocc = 16;
+        }
       }
       const double sf = occl ? 0.0 : (h.soft ? (double)unocc / 16.0 : 1.0);  // shadowSum / 16
       if (sf > 0.0) {
@@ -1105,6 +1080,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   __shared__ double slot[kRound][3];                 // radiance of the round's entries
   __shared__ double psum[64][3];                     // per pixel: running sum over samples
   __shared__ uint8_t lpix[64];                       // phase 1: the block's live pixels
+  __shared__ uint64_t skey[64];                      // per lane: its path's soft-shadow key (rt_soft_key, spec v4)
   // dynamic LDS (dyn_lds): [staged scene prefix (kStage)][BVH stack (stack_depth x 64 ints)]
 
   const int lane = threadIdx.x;
@@ -1392,7 +1368,9 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
           const int p = id / ns, s = k->sample_base + loc.s0 + id - p * ns;
           const int tp = loc.p0 + p;
           Counters nc;  // phase 1 counted this camera ray and its draws
-          camera_ray<false>(k, loc.tx * 32 + (tp & 31), loc.ty * 32 + (tp >> 5), s, rng, o, d, nc);
+          const int px = loc.tx * 32 + (tp & 31), py = loc.ty * 32 + (tp >> 5);
+          camera_ray<false>(k, px, py, s, rng, o, d, nc);
+          skey[lane] = rt_soft_key(k->frame_key[frame_of(k)], (uint32_t)py * (uint32_t)k->W + (uint32_t)px, (uint32_t)s);
           entry = e;
           T = mk(1, 1, 1);
           set_path_L(mk(0, 0, 0));
@@ -1427,7 +1405,8 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
             // (two or three paths run one after the other this way measured
             // slower: 0.79 / 0.93 vs 0.78 ms)
             if (__popcll(am) == 1 && hot<kStage>().masks) {
-              const d3 Lr = solo_path<kSky>(fresh(), __builtin_ctzll(am), o, d, T, path_L(), rng.x, depth, stack);
+              const d3 Lr = solo_path<kSky>(fresh(), __builtin_ctzll(am), o, d, T, path_L(), rng.x, depth,
+                                          skey[__builtin_ctzll(am)], stack);
               if (lane == __builtin_ctzll(am)) {
                 const int q = entry & (kRound - 1);
                 slot[q][0] = Lr.x;
@@ -1580,12 +1559,40 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
                              __builtin_isfinite(m->metallic);
           const bool trace = (!masks || (cm.s | cm.t) != 0) && !quiet;
           int unocc = 0;
+          // Spec v4 (include/rt_rng.h): the 16 points come from the stream of
+          // (sample, depth, light), not from the path's.  A lane whose rays
+          // cannot be blocked (empty shadow cone, or quiet) needs none of them:
+          // all 16 are unoccluded, nothing is drawn.  (The counting variant
+          // still walks their tries, for the reference's draw count, and
+          // books them as culled: executed work is the difference.)
+          const bool free_soft = need_soft && !trace;
+          if (free_soft) {
+            unocc = 16;
+            if constexpr (kCount) {
+              rt_rng fr{rt_soft_state(skey[lane], (uint32_t)depth, (uint32_t)li)};
+              unsigned long long tries = 0;
+              for (int got = 0; got < 16; ++tries) {
+                const uint32_t ux = rt_rng_next(&fr), uy = rt_rng_next(&fr), uz = rt_rng_next(&fr);
+                got += unit_ball_accept(ux, uy, uz) ? 1 : 0;
+              }
+              cnt<kCount>(c, C_SHADOW, 16);
+              cnt<kCount>(c, C_RNG, 3ull * tries);
+              culled.v[C_RNG] += 3ull * tries;
+            }
+          }
+          const bool traced_soft = need_soft && trace;
+          rt_rng srng{traced_soft ? rt_soft_state(skey[lane], (uint32_t)depth, (uint32_t)li) : 0ull};
           // soft shadows: wave-converged decision between the two forms
-          const unsigned long long owners = __ballot(need_soft);
+          const unsigned long long owners = __ballot(traced_soft);
 #ifdef RT_WG_TIMING
           const unsigned long long ts2 = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef RT_EXP_NO_SOFT  // timing experiment only (scripts/build_variant.sh): no soft-shadow draws or rays
+          if (need_soft) unocc = 16;
+          if (false) {
+#else
           if (owners != 0) {
+#endif
 #ifdef RT_WG_TIMING
             if (__popcll(owners) <= kCoopMax) dbg_coop += __popcll(owners); else ++dbg_seq;
 #endif
@@ -1594,17 +1601,17 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
               for (unsigned long long b = owners; b; b &= b - 1) {
                 const int ow = __builtin_ctzll(b);
                 const CoopOut r = soft_coop<kCount>(
-                    gg, masks, rl32(trace ? 1u : 0u, ow) != 0, inv3(rl3(P, ow)), inv3(rl3(ldir, ow)),
-                    inv(rld(ldist, ow)), Cand{rl64(cm.s, ow), rl64(cm.t, ow)}, rl64(rng.x, ow), h.jump, stack, c);
+                    gg, masks, true, inv3(rl3(P, ow)), inv3(rl3(ldir, ow)),
+                    inv(rld(ldist, ow)), Cand{rl64(cm.s, ow), rl64(cm.t, ow)}, rl64(srng.x, ow), h.jump, stack, c);
                 if (lane == ow) {
                   unocc = r.unocc;
-                  rng.x = r.x;
                   cnt<kCount>(c, C_SHADOW, 16);
                   cnt<kCount>(c, C_RNG, 3ull * r.tries);
                 }
               }
             } else {
-              unocc = soft_queue<kCount>(gg, masks, need_soft, trace, P, ldir, ldist, cm, rng, h.jump, stack, c);
+              const int uq = soft_queue<kCount>(gg, masks, traced_soft, true, P, ldir, ldist, cm, srng, h.jump, stack, c);
+              if (traced_soft) unocc = uq;  // (a free lane keeps its 16)
             }
           }
 #ifdef RT_WG_TIMING

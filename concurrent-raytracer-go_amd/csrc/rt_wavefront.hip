@@ -934,6 +934,18 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
   flush_counts<kCount>(p, c, kGroupSoft);
 }
 
+// The image pixel (y W + x) and sample index of sample id `sid` (wf_regen's
+// mapping): the key of its soft-shadow streams (spec v4, include/rt_rng.h)
+__device__ __forceinline__ uint64_t sid_soft_key(const WfParams& p, uint32_t sid) {
+  const uint32_t q = sid / (uint32_t)p.spp;
+  const uint32_t lp = p.lp0 + q;
+  const uint32_t smp = sid - q * (uint32_t)p.spp;
+  const int lt = (int)(lp >> 10), tp = (int)(lp & 1023);
+  const int tile = p.tile_list ? p.tile_list[lt] : p.rank + lt * p.world;
+  const int x = (tile % p.tiles_x) * 32 + (tp & 31), y = (tile / p.tiles_x) * 32 + (tp >> 5);
+  return rt_soft_key(p.seed_key, (uint32_t)y * (uint32_t)p.W + (uint32_t)x, smp);
+}
+
 // ---------------------------------------------------------------- softgen
 // For every light whose hard ray is clear, in light order, the 16 points of
 // calculateSmartShadow's soft rays from the path's stream (rejection
@@ -960,19 +972,25 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
     hit = p.hidx[slot] >= 0;
   }
   const int shard = blockIdx.x % kWfShards;
-  // the 16 points of each light of `own`, in light order: traced rays at
-  // entries q.. of the shard's queue, a listed light's at the 16 entries
-  // ending before soft_cap - ql (ql += 16); an empty cone's are drawn and
-  // dropped (none can be blocked)
-  auto gen = [&](size_t sl, uint32_t own, uint32_t listed, uint32_t empty, int base, int q, int ql,
-                 rt_rng& rng) {
+  // the 16 points of each light of `own`: traced rays at entries q.. of the
+  // shard's queue, a listed light's at the 16 entries ending before
+  // soft_cap - ql (ql += 16).  Each light's points come from its own stream
+  // (spec v4: (sample, depth, light), include/rt_rng.h); an empty cone's rays
+  // cannot be blocked and need none, so nothing is drawn for it (the
+  // counting variant walks its tries for the reference's draw count).
+  auto gen = [&](size_t sl, uint32_t own, uint32_t listed, uint32_t empty, int base, int q, int ql) {
     uint4* sq = reinterpret_cast<uint4*>(p.softq) + (size_t)shard * p.soft_cap;
+    const uint64_t skey = sid_soft_key(p, p.cur.sid[sl]);
+    const uint32_t depth = (uint32_t)p.cur.depth[sl];
     for (uint32_t m = own; m; m &= m - 1) {
-      const uint32_t key = (uint32_t)(sl * p.nl) + (uint32_t)(base + __builtin_ctz(m));
+      const int li = base + __builtin_ctz(m);
+      const uint32_t key = (uint32_t)(sl * p.nl) + (uint32_t)li;
       const uint32_t bit = m & (0u - m);
       cnt<kCount>(c, C_SHADOW, 16);
+      const bool keep = !(empty & bit);
+      if (!keep && !kCount) continue;
       size_t at;  // (an index, not a bumped pointer)
-      if (empty & bit) {
+      if (!keep) {
         at = 0;
       } else if (listed & bit) {
         at = (size_t)(p.soft_cap - ql - 16);
@@ -981,7 +999,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
         at = (size_t)q;
         q += 16;
       }
-      const bool keep = !(empty & bit);
+      rt_rng rng{rt_soft_state(skey, depth, (uint32_t)li)};
       for (int k = 0; k < 16;) {
         const uint32_t ux = rt_rng_next(&rng), uy = rt_rng_next(&rng), uz = rt_rng_next(&rng);
         cnt<kCount>(c, C_RNG, 3);
@@ -1012,24 +1030,18 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
     const uint32_t wl = work ? s_list[threadIdx.x] : 0u, we = work ? s_empty[threadIdx.x] : 0u;
     const int q = block_append(16 * __popc(wo & ~wl), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
     const int ql = block_append(16 * __popc(wl & ~we), &p.ctl->list_cnt[shard * 32], s_wave, &s_base);
-    if (work) {
-      rt_rng rng{p.cur.rng[ws]};
-      gen(ws, wo, wl, we, 0, q, ql, rng);
-      p.cur.rng[ws] = rng.x;
-    }
+    if (work) gen(ws, wo, wl, we, 0, q, ql);
     flush_counts<kCount>(p, c);
     return;
   }
-  rt_rng rng{hit ? p.cur.rng[slot] : 0ull};
   // more than 32 lights: in chunks of 32 (one bit each), in light order
   for (int base = 0; base < p.nl; base += 32) {
     uint32_t listed, empty;
     const uint32_t own = clear_lights(p, slot, hit, base, &listed, &empty);
     const int q = block_append(16 * __popc(own & ~listed), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
     const int ql = block_append(16 * __popc(listed & ~empty), &p.ctl->list_cnt[shard * 32], s_wave, &s_base);
-    if (own) gen(slot, own, listed, empty, base, q, ql, rng);
+    if (own) gen(slot, own, listed, empty, base, q, ql);
   }
-  if (hit) p.cur.rng[slot] = rng.x;
   flush_counts<kCount>(p, c);
 }
 

@@ -10,7 +10,7 @@
  * the same draws as the kernel because both key the stream by
  * (seed, pixel, sample) — never by tile, rank or thread.
  *
- * Spec (v3): one PCG32 stream (O'Neill 2014, PCG-XSH-RR 64/32) per sample.
+ * Spec (v3, kept by v4 below): one PCG32 stream (O'Neill 2014, PCG-XSH-RR 64/32) per sample.
  *   key0    = mix64(seed)                               (once per render)
  *   x_0     = mix64(key0 ^ (pixel << 32 | sample))      pixel = y*W + x
  *   x_{i+1} = x_i * 6364136223846793005 + 1442695040888963407   (mod 2^64)
@@ -27,6 +27,23 @@
  * hard shadow ray is unoccluded, 16 RandomVec3InUnitSphere
  * (renderer.go:315-316, vector.go:132-139: 3 draws per rejection try);
  * then the material's scatter draws.
+ *
+ * Spec v4 (round 5): the 16 soft-shadow points of one (sample, bounce,
+ * light) draw from a stream of their own, not from the sample's stream:
+ *   y_0 = mix64(mix64(key0 ^ RT_SOFT_TAG ^ (pixel << 32 | sample))
+ *               ^ (depth << 32 | light))          depth = traceRay's depth
+ * then the same PCG steps and outputs, 3 draws per rejection try until 16
+ * points are accepted.  The sample's stream carries u, v and the scatter
+ * draws only.  Why: a light whose 16 soft rays cannot be blocked (nothing
+ * in their shadow cone) needs its points only to advance the sample's
+ * stream; with a stream of their own, the kernels skip those ~31 tries per
+ * (hit, light) -- a third of the headline kernel's time --
+ * and a cone's points can be drawn by any lane in any order.  The
+ * reference's draws are a global stream shared by every goroutine
+ * (random.go:8-14), so which generator state feeds which call was never
+ * reproducible; every draw is still an independent uniform draw, and the
+ * rejection sampling, its 3 draws per try and the points are the
+ * reference's.
  */
 #ifndef RT_RNG_H
 #define RT_RNG_H
@@ -57,6 +74,16 @@ RT_RNG_FN uint64_t rt_rng_seed_key(uint64_t seed) { return rt_mix64(seed); }
 
 RT_RNG_FN void rt_rng_init(rt_rng* r, uint64_t seed_key, uint32_t pixel, uint32_t sample) {
   r->x = rt_mix64(seed_key ^ (((uint64_t)pixel << 32) | (uint64_t)sample));
+}
+
+/* v4: the soft-shadow stream of (pixel, sample, depth, light), in two steps:
+ * the sample's soft key (once per sample), then the stream of a bounce's light */
+#define RT_SOFT_TAG 0x5F0F7A11E5EED5A1ULL
+RT_RNG_FN uint64_t rt_soft_key(uint64_t seed_key, uint32_t pixel, uint32_t sample) {
+  return rt_mix64(seed_key ^ RT_SOFT_TAG ^ (((uint64_t)pixel << 32) | (uint64_t)sample));
+}
+RT_RNG_FN uint64_t rt_soft_state(uint64_t soft_key, uint32_t depth, uint32_t light) {
+  return rt_mix64(soft_key ^ (((uint64_t)depth << 32) | (uint64_t)light));
 }
 
 /* PCG-XSH-RR output of a state value */

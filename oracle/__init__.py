@@ -80,6 +80,9 @@ def lib():
                                  ctypes.POINTER(i32)]
     L.oracle_rng_draws.restype = None
     L.oracle_rng_draws.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, i32, vp, vp]
+    L.oracle_soft_points.restype = None
+    L.oracle_soft_points.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                     ctypes.c_uint32, vp, ctypes.POINTER(i32)]
     L.oracle_path_lengths.restype = ctypes.c_int
     L.oracle_path_lengths.argtypes = [ctypes.POINTER(rt.SceneView), i32, i32, ctypes.POINTER(rt.Settings), i32, vp]
     L.oracle_cube_triangles.restype = None
@@ -199,6 +202,14 @@ def rng_draws(seed, pixel, sample, n):
     raw = np.zeros(n, np.uint64)
     lib().oracle_rng_draws(seed, pixel, sample, n, vals.ctypes.data, raw.ctypes.data)
     return vals, raw
+
+
+def soft_points(seed, pixel, sample, depth, light):
+    """(16x3 points, tries) of the soft-shadow stream of (pixel, sample, depth, light), spec v4."""
+    pts = np.zeros((16, 3), np.float64)
+    t = ctypes.c_int32()
+    lib().oracle_soft_points(seed, pixel, sample, depth, light, pts.ctypes.data, ctypes.byref(t))
+    return pts, int(t.value)
 
 
 def cube_triangles(position, size):

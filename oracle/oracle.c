@@ -184,6 +184,7 @@ typedef struct {
 typedef struct {
   rt_rng rng;
   ocounts* c;
+  uint64_t soft_key;  /* rt_soft_key of the sample (spec v4: its soft-shadow streams) */
 } ostream;
 
 static inline double rnd(ostream* s) {
@@ -736,8 +737,10 @@ static int hit_world(const oscene* sc, oray r, double tmin, double tmax, hitrec*
 
 /* ------------------------------------------------------------ renderer */
 
-/* calculateSmartShadow, renderer.go:299-331 */
-static double smart_shadow(const oscene* sc, const hitrec* h, int li, ostream* s) {
+/* calculateSmartShadow, renderer.go:299-331.  Its 16 RandomVec3InUnitSphere
+ * points draw from the (sample, depth, light) soft-shadow stream of spec v4
+ * (include/rt_rng.h), not from the sample's stream. */
+static double smart_shadow(const oscene* sc, const hitrec* h, int li, int depth, ostream* s) {
   vec3 ldir = vnorm(vsub(sc->lpos[li], h->p));
   double ldist = vlen(vsub(sc->lpos[li], h->p));
   oray sr = {h->p, ldir};
@@ -747,8 +750,12 @@ static double smart_shadow(const oscene* sc, const hitrec* h, int li, ostream* s
     return 0.0;
   if (sc->soft) {
     double sum = 0.0;
+    ostream ps;  /* the points' stream (its draws are counted with the sample's) */
+    ps.rng.x = rt_soft_state(s->soft_key, (uint32_t)depth, (uint32_t)li);
+    ps.c = s->c;
+    ps.soft_key = s->soft_key;
     for (int i = 0; i < 16; i++) {
-      vec3 off = vmuls(random_in_unit_sphere(s), 0.1);
+      vec3 off = vmuls(random_in_unit_sphere(&ps), 0.1);
       vec3 sdir = vnorm(vadd(ldir, off));
       oray ss = {h->p, sdir};
       s->c->shadow_rays++;
@@ -761,7 +768,7 @@ static double smart_shadow(const oscene* sc, const hitrec* h, int li, ostream* s
 }
 
 /* calculateDirectLighting, renderer.go:229-297 */
-static vec3 direct_lighting(const oscene* sc, const hitrec* h, ostream* s) {
+static vec3 direct_lighting(const oscene* sc, const hitrec* h, int depth, ostream* s) {
   vec3 total = V(0, 0, 0);
   const omat* m = h->mat;
   vec3 albedo = mat_albedo(m);
@@ -779,7 +786,7 @@ static vec3 direct_lighting(const oscene* sc, const hitrec* h, ostream* s) {
     double ldist = vlen(vsub(sc->lpos[li], h->p));
     if (ldist < 0.001) continue;
     s->c->light_evals++;
-    double sf = smart_shadow(sc, h, li, s);
+    double sf = smart_shadow(sc, h, li, depth, s);
     if (sf > 0.0) {
       double cos_t = oracle_go_max(0, vdot(h->n, ldir));
       double intensity = cos_t * sc->lint[li] / (ldist * ldist);
@@ -821,7 +828,7 @@ static vec3 trace_ray(const oscene* sc, oray r, int depth, ostream* s) {
   const omat* m = h.mat;
   s->c->shade_events++;
   vec3 emitted = mat_emitted(m);
-  vec3 direct = direct_lighting(sc, &h, s);
+  vec3 direct = direct_lighting(sc, &h, depth, s);
   oray scattered;
   vec3 att;
   if (!mat_scatter(m, r, &h, s, &scattered, &att)) return vadd(emitted, direct);
@@ -869,6 +876,7 @@ static vec3 trace_pixel(const oscene* sc, int x, int y, ocounts* c) {
     ostream st;
     st.c = c;
     rt_rng_init(&st.rng, sc->seed_key, pixel, (uint32_t)smp);
+    st.soft_key = rt_soft_key(sc->seed_key, pixel, (uint32_t)smp);
     c->camera_rays++;
     double u = ((double)x + rnd(&st)) / (double)sc->W;
     double v = ((double)y + rnd(&st)) / (double)sc->H;
@@ -1149,6 +1157,7 @@ int oracle_scatter(const rt_material* m, const double ray_o[3], const double ray
   memset(&c, 0, sizeof c);
   ostream st;
   st.c = &c;
+  st.soft_key = 0;
   rt_rng_init(&st.rng, rt_rng_seed_key(seed), pixel, sample);
   for (int i = 0; i < skip; i++) rt_rng_draw(&st.rng);
   hitrec h;
@@ -1179,6 +1188,25 @@ void oracle_rng_draws(uint64_t seed, uint32_t pixel, uint32_t sample, int32_t n,
     if (raw) raw[i] = x;
     if (out) out[i] = rt_bits_to_unit(x);
   }
+}
+
+/* The 16 soft-shadow points of (pixel, sample, depth, light) as smart_shadow
+ * draws them (spec v4), and the rejection tries they took. */
+void oracle_soft_points(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t depth, uint32_t light, double out[48],
+                        int32_t* tries) {
+  ocounts c;
+  memset(&c, 0, sizeof c);
+  ostream ps;
+  ps.c = &c;
+  ps.soft_key = rt_soft_key(rt_rng_seed_key(seed), pixel, sample);
+  ps.rng.x = rt_soft_state(ps.soft_key, depth, light);
+  for (int i = 0; i < 16; i++) {
+    const vec3 p = random_in_unit_sphere(&ps);
+    out[3 * i + 0] = p.x;
+    out[3 * i + 1] = p.y;
+    out[3 * i + 2] = p.z;
+  }
+  if (tries) *tries = (int32_t)(c.rng_draws / 3);
 }
 
 void oracle_cube_triangles(const double position[3], const double size[3], double out[108]) {

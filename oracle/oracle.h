@@ -73,6 +73,8 @@ int oracle_scatter(const rt_material* m, const double ray_o[3], const double ray
                    uint64_t seed, uint32_t pixel, uint32_t sample, int32_t skip, double out[6], int32_t* draws);
 /* First n draws of stream (seed, pixel, sample) — RNG known answers. */
 void oracle_rng_draws(uint64_t seed, uint32_t pixel, uint32_t sample, int32_t n, double* out, uint64_t* raw);
+void oracle_soft_points(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t depth, uint32_t light, double out[48],
+                        int32_t* tries);
 /* AtmosphereConfig.GetSkyColor of preset `sky` (RT_SKY_DEFAULT..NIGHT) for a ray direction. */
 void oracle_sky_color(int sky, const double dir[3], double out[3]);
 /* Flattened cube triangles (createCube, scene.go:150-190): 12 x 9 doubles. */

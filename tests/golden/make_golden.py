@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Writes tests/golden/oracle_*.npz: small whole-image fixtures rendered by
-the CPU oracle (oracle/oracle.c) with the random stream spec v3.
+the CPU oracle (oracle/oracle.c) with the random stream spec v4 (regenerated in round 5 for v4).
 
 These are SELF-PINS of this build (the reference has no renderer goldens and
 no Go toolchain exists here — SURVEY.md §4, §8c): they freeze the oracle's

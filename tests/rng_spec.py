@@ -1,4 +1,5 @@
-"""Pure-Python statement of the random stream spec v3 (include/rt_rng.h).
+"""Pure-Python statement of the random stream spec v4 (include/rt_rng.h):
+v3's per-sample stream, plus v4's soft-shadow streams.
 
 Independent of the C code: used to check the oracle's stream and to make
 the committed known-answer vectors (tests/golden/make_rng_vectors.py).
@@ -47,3 +48,39 @@ def jump(j):
         c = (c * MULT + INC) & M64
         a = (a * MULT) & M64
     return a, c
+
+
+SOFT_TAG = 0x5F0F7A11E5EED5A1
+
+
+def soft_init(seed, pixel, sample, depth, light):
+    """v4: the state of the soft-shadow stream of (pixel, sample, depth, light)."""
+    k = mix64(mix64(seed & M64) ^ SOFT_TAG ^ (((pixel & 0xFFFFFFFF) << 32) | (sample & 0xFFFFFFFF)))
+    return mix64(k ^ (((depth & 0xFFFFFFFF) << 32) | (light & 0xFFFFFFFF)))
+
+
+def soft_draws(seed, pixel, sample, depth, light, n):
+    x = soft_init(seed, pixel, sample, depth, light)
+    raw = []
+    for _ in range(n):
+        raw.append(out(x))
+        x = step(x)
+    return raw
+
+
+def soft_points(seed, pixel, sample, depth, light):
+    """calculateSmartShadow's 16 accepted RandomVec3InUnitSphere points of one
+    (sample, bounce, light) and the tries taken (binary64 arithmetic of the
+    kernel: 2 u - 1 per axis from u = raw * 2^-32, accepted when |p|^2 < 1)."""
+    x = soft_init(seed, pixel, sample, depth, light)
+    pts, tries = [], 0
+    while len(pts) < 16:
+        r = []
+        for _ in range(3):
+            r.append(out(x))
+            x = step(x)
+        tries += 1
+        p = [v * 2.0**-32 * 2 - 1 for v in r]
+        if p[0] * p[0] + p[1] * p[1] + p[2] * p[2] < 1:
+            pts.append(tuple(p))
+    return pts, tries

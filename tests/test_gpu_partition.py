@@ -161,7 +161,11 @@ def test_counts_with_an_opted_in_sky_keep_the_image():
     assert counted[1].tobytes() == plain[1].tobytes()
     c = counted[3]
     assert c.camera_rays == 64 * 48 * 3
-    assert all(v == 0 for v in c.culled_dict().values())  # a sky culls nothing
+    # a sky culls no camera sample; only soft-shadow draws of lights whose
+    # rays cannot be blocked are culled (spec v4: not drawn by the product)
+    cull = c.culled_dict()
+    assert all(v == 0 for k, v in cull.items() if k != "rng_draws")
+    assert cull["rng_draws"] % 3 == 0
 
 
 def test_culled_counts_are_the_skipped_camera_samples():
@@ -171,7 +175,11 @@ def test_culled_counts_are_the_skipped_camera_samples():
     cull, ex = c.culled_dict(), c.executed_dict()
     assert c.camera_rays == 160 * 120 * 10
     assert 0 < cull["camera_rays"] < c.camera_rays
-    assert cull["rng_draws"] == 2 * cull["camera_rays"]  # a culled sample draws its jitter only
+    # a culled sample draws its jitter only; the rest of the culled draws are
+    # the rejection tries (3 draws each) of soft rays that cannot be blocked,
+    # which the product does not draw (spec v4, include/rt_rng.h)
+    extra = cull["rng_draws"] - 2 * cull["camera_rays"]
+    assert extra >= 0 and extra % 3 == 0
     assert cull["shade_events"] == cull["shadow_rays"] == cull["light_evals"] == 0  # culled samples miss
     assert ex["shade_events"] == c.shade_events
     # the as-committed scene: every camera ray misses, every sample is culled

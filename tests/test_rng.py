@@ -1,4 +1,5 @@
-"""Random stream spec v3 (include/rt_rng.h), CPU.
+"""Random stream spec v4 (include/rt_rng.h; v3's per-sample stream plus the
+soft-shadow streams of v4), CPU.
 
 The reference draws from Go's global, unseedable math/rand
 (internal/math/random.go:8-14), so a Go run's draw order depends on the
@@ -22,12 +23,32 @@ from conftest import GOLDEN, ROOT
 
 
 def test_oracle_stream_matches_committed_vectors():
-    with open(os.path.join(GOLDEN, "rng_v3.json")) as f:
+    with open(os.path.join(GOLDEN, "rng_v4.json")) as f:
         vecs = json.load(f)["vectors"]
     for v in vecs:
         vals, raw = oracle.rng_draws(v["seed"], v["pixel"], v["sample"], len(v["raw"]))
         assert raw.tolist() == v["raw"]
         assert [float.fromhex(h) for h in v["draws"]] == vals.tolist()
+
+
+def test_oracle_soft_streams_match_committed_vectors():
+    """v4: calculateSmartShadow's 16 points of a (sample, bounce, light) come
+    from a stream of their own; the oracle's points and tries equal the
+    committed vectors of the Python statement."""
+    with open(os.path.join(GOLDEN, "rng_v4.json")) as f:
+        vecs = json.load(f)["soft_vectors"]
+    for v in vecs:
+        pts, tries = oracle.soft_points(v["seed"], v["pixel"], v["sample"], v["depth"], v["light"])
+        assert tries == v["tries"]
+        assert [[float.fromhex(h) for h in p] for p in v["points"]] == pts.tolist()
+        assert v["raw"] == rng_spec.soft_draws(v["seed"], v["pixel"], v["sample"], v["depth"], v["light"], 12)
+
+
+def test_soft_streams_are_distinct_per_bounce_and_light():
+    a = rng_spec.soft_draws(3, 77, 5, 0, 0, 6)
+    others = [rng_spec.soft_draws(3, 77, 5, 1, 0, 6), rng_spec.soft_draws(3, 77, 5, 0, 1, 6),
+              rng_spec.soft_draws(3, 77, 6, 0, 0, 6), rng_spec.draws(3, 77, 5, 6)[0]]
+    assert all(a != o for o in others)
 
 
 @pytest.mark.parametrize("seed,pixel,sample", [(1, 0, 0), (7, 5, 3), (2**63 + 5, 12345, 64), (3, 2**32 - 1, 7)])
@@ -76,6 +97,7 @@ def test_header_jump_coeffs_compiled_with_gcc(tmp_path):
           rt_rng r;
           rt_rng_init(&r, rt_rng_seed_key(9), 4242, 17);
           for (int i = 0; i < 4; ++i) printf("d %a\\n", rt_rng_draw(&r));
+          printf("s %" PRIu64 "\\n", rt_soft_state(rt_soft_key(rt_rng_seed_key(9), 4242, 17), 3, 1));
           return 0;
         }
     """))
@@ -89,6 +111,9 @@ def test_header_jump_coeffs_compiled_with_gcc(tmp_path):
             continue
         if ln.startswith("d "):
             ds.append(float.fromhex(ln[2:]))
+            continue
+        if ln.startswith("s "):
+            assert int(ln[2:]) == rng_spec.soft_init(9, 4242, 17, 3, 1)
             continue
         j, a, c = (int(t) for t in ln.split())
         assert (a, c) == rng_spec.jump(j)
