@@ -916,6 +916,7 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   WfParams p;
   memset(&p, 0, sizeof p);
   p.g = Geo{kp.spheres, kp.tris, kp.boxes, kp.bvh, kp.ns, kp.nt, kp.use_bvh, kp.nb};
+  p.jump = kp.jump;
   p.qbvh = c->d_qbvh;
   memcpy(p.q0, f.q0, sizeof p.q0);
   memcpy(p.qd, f.qd, sizeof p.qd);

@@ -241,7 +241,7 @@ struct WfCtl {                 // device-resident loop state; counters of shard 
   int32_t hard_cnt[kWfShards * 32];  // hard shadow rays queued per shard
   int32_t soft_cnt[kWfShards * 32];  // soft shadow rays queued per shard
   int32_t cone_cnt[kWfShards * 32];  // shadow cones queued per shard
-  int32_t list_cnt[kWfShards * 32];  // soft rays of listed cones per shard (from the far end of the soft queue)
+  int32_t list_cnt[kWfShards * 32];  // entries of listed cones per shard (two each, from the far end of the soft queue)
   int32_t job_head[4][kWfShards * 32];  // persistent kernels (extend, hard, soft, cone): jobs taken per range
   unsigned long long next_sample;    // first sample id of the chunk not started yet
   unsigned long long total;          // sample ids in the chunk
@@ -286,6 +286,8 @@ struct WfParams {
   uint32_t* lstate;          // [slot][light]: kHardBit | blocked soft rays
   uint32_t* hardq;           // kWfShards queues of hard_cap entries: slot * nl + light
   uint32_t* softq;           // kWfShards queues of soft_cap entries, 4 words: {slot * nl + light, draws x, y, z}
+                             // (listed cones, from the far end: 2 entries, wf_softgen)
+  const uint64_t* jump;      // PCG jump table (KParams::jump)
   uint32_t* coneq;           // kWfShards queues of hard_cap entries: slot * nl + light (clear hard ray)
   int32_t* cand;             // [slot * nl + light][kWfConeK]: the shadow cone's candidate spheres, -1 ends
   double* rad;               // [sample id][3] radiance

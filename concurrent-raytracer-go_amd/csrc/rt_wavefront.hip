@@ -323,26 +323,80 @@ __device__ __forceinline__ void load_pair(glb_node* __restrict__ qb, lds_node* _
   }
 }
 template <bool kCount, bool kFull>
+__device__ __forceinline__ void node_step(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
+                                          const RayQ& r, float tminf, float tmaxf, int& cur, int& sp, int* stack,
+                                          Counters& c) {
+  uint4 L, R;
+  load_pair<kFull>(qb, lt, nlds, cur >> 3, L, R);
+  cnt<kCount>(c, C_BOX, 2);
+  float tl, tr;
+  const bool hl = box_q(L, r, tminf, tmaxf, tl), hr = box_q(R, r, tminf, tmaxf, tr);
+  if (hl || hr) {
+    const bool lfirst = hl && (!hr || tl <= tr);
+    if (hl && hr) {
+      stack[sp * 64] = lfirst ? (int)R.w : (int)L.w;
+      ++sp;
+    }
+    cur = lfirst ? (int)L.w : (int)R.w;
+  } else {
+    cur = sp == 0 ? -1 : stack[--sp * 64];
+  }
+}
+template <bool kCount, bool kFull>
 __device__ __forceinline__ void descend(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
                                         const RayQ& r, float tminf, float tmaxf, int& cur, int& sp, int* stack,
                                         Counters& c) {
-  while ((cur & 7) == 0) {
-    uint4 L, R;
-    load_pair<kFull>(qb, lt, nlds, cur >> 3, L, R);
-    cnt<kCount>(c, C_BOX, 2);
-    float tl, tr;
-    const bool hl = box_q(L, r, tminf, tmaxf, tl), hr = box_q(R, r, tminf, tmaxf, tr);
-    if (hl || hr) {
-      const bool lfirst = hl && (!hr || tl <= tr);
-      if (hl && hr) {
-        stack[sp * 64] = lfirst ? (int)R.w : (int)L.w;
-        ++sp;
-      }
-      cur = lfirst ? (int)L.w : (int)R.w;
-    } else {
-      cur = sp == 0 ? -1 : stack[--sp * 64];
+  while ((cur & 7) == 0) node_step<kCount, kFull>(qb, lt, nlds, r, tminf, tmaxf, cur, sp, stack, c);
+}
+
+// (r05) Speculative traversal (Aila & Laine 2009, postponed leaves): a lane
+// that reaches a leaf while its stack is not empty parks it in `pend` and
+// keeps descending from the stack; the node loop ends once no lane is still
+// looking for its first leaf, so the leaf tests that follow run on more lanes
+// at once.  The answer does not depend on the order leaves are tested
+// (any-hit; closest hit: the least t with the obj tie rule, as the BVH order
+// already differs from the scan order), so the images are unchanged.
+#ifndef RT_WF_SPEC
+#define RT_WF_SPEC 0
+#endif
+__device__ __forceinline__ bool is_leaf(int cur) { return cur != -1 && (cur & 7) != 0; }
+template <bool kCount, bool kFull>
+__device__ __forceinline__ void descend_spec(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
+                                             const RayQ& r, float tminf, float tmaxf, int& cur, int& sp, int& pend,
+                                             int* stack, Counters& c) {
+  for (;;) {
+    if (pend < 0 && is_leaf(cur) && sp > 0) {
+      pend = cur;
+      cur = stack[--sp * 64];
     }
+    if (__ballot(pend < 0 && (cur & 7) == 0) == 0) break;
+    if ((cur & 7) == 0) node_step<kCount, kFull>(qb, lt, nlds, r, tminf, tmaxf, cur, sp, stack, c);
   }
+}
+// The leaf to test after a descent (-1: none), the parked one first; cur
+// moves on past a leaf it takes.  The ray is done when cur is -1 afterwards.
+__device__ __forceinline__ int take_leaf(int& cur, int& sp, int& pend, const int* stack) {
+  if (pend >= 0) {
+    const int lf = pend;
+    pend = -1;
+    return lf;
+  }
+  if (!is_leaf(cur)) return -1;
+  const int lf = cur;
+  cur = sp == 0 ? -1 : stack[--sp * 64];
+  return lf;
+}
+// Either form: descend, then the leaf to test
+template <bool kCount, bool kFull>
+__device__ __forceinline__ int next_leaf(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
+                                         const RayQ& r, float tminf, float tmaxf, int& cur, int& sp, int& pend,
+                                         int* stack, Counters& c) {
+#if RT_WF_SPEC
+  descend_spec<kCount, kFull>(qb, lt, nlds, r, tminf, tmaxf, cur, sp, pend, stack, c);
+#else
+  descend<kCount, kFull>(qb, lt, nlds, r, tminf, tmaxf, cur, sp, stack, c);
+#endif
+  return take_leaf(cur, sp, pend, stack);
 }
 
 // The spheres of a leaf: the loads of the first kLeafBatch are issued
@@ -426,7 +480,7 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
   double av = 0, inv_a = 0, closest = 0;
   RayQ r32{};
   float tminf = 0;
-  int cur = -1, sp = 0, best_obj = -1, bidx = -1;
+  int cur = -1, sp = 0, pend = -1, best_obj = -1, bidx = -1;
   for (;;) {
     const unsigned long long idle = __ballot(!busy);
     if (more && (__popcll(idle) >= kRefill || idle == ~0ull) && js.next >= js.hi)
@@ -470,9 +524,11 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
       continue;
     }
     if (busy) {
-      descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, t_hi32(closest), cur, sp, stack, c);
-      if (cur != -1) {  // a leaf: the exact Sphere.Hit tests, in hittable order
-        const int first = cur >> 3, count = cur & 7;
+      const int lf =
+          next_leaf<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, t_hi32(closest), cur, sp, pend,
+                                   stack, c);
+      if (lf != -1) {  // a leaf: the exact Sphere.Hit tests, in hittable order
+        const int first = lf >> 3, count = lf & 7;
         DSphere ls[kLeafBatch];
         load_leaf(p.g.spheres, first, count, ls);
         for (int i = first; i < first + count; ++i) {
@@ -487,9 +543,8 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
             best_obj = S.obj;
           }
         }
-        cur = sp == 0 ? -1 : stack[--sp * 64];
       }
-      if (cur == -1) {  // traversal done
+      if (cur == -1 && pend < 0) {  // traversal done
         busy = false;
         if (best_obj >= 0) {
           // the hit point (HitRecord.P, sphere.go:44: t = the root / a, as
@@ -612,7 +667,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
   double av = 0, inv_a = 0, tmax = 0;
   RayQ r32{};
   float tminf = 0, tmaxf = 0;
-  int cur = -1, sp = 0;
+  int cur = -1, sp = 0, pend = -1;
   for (;;) {
     const unsigned long long idle = __ballot(!busy);
     if (more && (__popcll(idle) >= kRefill || idle == ~0ull) && js.next >= js.hi)
@@ -650,6 +705,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
           tmaxf = t_hi32(tmax);
           cur = bvh_code(p.g.bvh[0]);
           sp = 0;
+          pend = -1;
           busy = true;
         }
       }
@@ -659,10 +715,11 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
       continue;
     }
     if (busy) {
-      descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, tmaxf, cur, sp, stack, c);
+      const int lf =
+          next_leaf<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, tmaxf, cur, sp, pend, stack, c);
       bool blocked = false;
-      if (cur != -1) {
-        const int first = cur >> 3, count = cur & 7;
+      if (lf != -1) {
+        const int first = lf >> 3, count = lf & 7;
         DSphere ls[kLeafBatch];
         load_leaf(p.g.spheres, first, count, ls);
         for (int i = first; i < first + count && !blocked; ++i) {
@@ -670,7 +727,6 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
           double num;
           blocked = sphere_query(leaf_sphere(p.g.spheres, ls, first, i), o, d, av, inv_a, tmin, tmax, num) != 0;
         }
-        cur = sp == 0 ? -1 : stack[--sp * 64];
       }
       if (blocked) {
         if constexpr (kSoft)
@@ -678,7 +734,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
         else
           p.lstate[key] = kHardBit;
       }
-      if (blocked || cur == -1) busy = false;
+      if (blocked || (cur == -1 && pend < 0)) busy = false;
     }
   }
   flush_counts<kCount>(p, c, kSoft ? kGroupSoft : kGroupHard);
@@ -694,7 +750,8 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
 // the scene.  wf_conegen queues every (path, light) whose hard ray is clear;
 // wf_cone walks the BVH with the cone and, when at most kWfConeK spheres are
 // candidates, leaves their list and kListBit in lstate; wf_softgen queues
-// such a light's 16 rays apart, and wf_listtest tests them against the list
+// such a cone's key apart, and wf_listtest draws its 16 rays and tests them
+// against the list
 // -- the same Sphere.Hit test the traversal runs -- instead
 // of walking the tree.  C4 (scripts/cone_stats.py): 45 % of the clear cones
 // are empty, the median cone has 1 candidate, 6 % have more than 16.
@@ -783,23 +840,43 @@ __device__ __forceinline__ bool cone_keeps(const DSphere& S, d3 P, d3 u, double 
 }
 
 template <bool kCount, bool kFull>
-__device__ __forceinline__ void cone_descend(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
-                                             const ConeQ& k, int& cur, int& sp, int* stack, Counters& c) {
-  while ((cur & 7) == 0) {
-    uint4 L, R;
-    load_pair<kFull>(qb, lt, nlds, cur >> 3, L, R);
-    cnt<kCount>(c, C_BOX, 2);
-    const bool hl = cone_node(L, k), hr = cone_node(R, k);
-    if (hl || hr) {
-      if (hl && hr) {
-        stack[sp * 64] = (int)R.w;
-        ++sp;
-      }
-      cur = hl ? (int)L.w : (int)R.w;
-    } else {
-      cur = sp == 0 ? -1 : stack[--sp * 64];
+__device__ __forceinline__ void cone_step(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
+                                          const ConeQ& k, int& cur, int& sp, int* stack, Counters& c) {
+  uint4 L, R;
+  load_pair<kFull>(qb, lt, nlds, cur >> 3, L, R);
+  cnt<kCount>(c, C_BOX, 2);
+  const bool hl = cone_node(L, k), hr = cone_node(R, k);
+  if (hl || hr) {
+    if (hl && hr) {
+      stack[sp * 64] = (int)R.w;
+      ++sp;
     }
+    cur = hl ? (int)L.w : (int)R.w;
+  } else {
+    cur = sp == 0 ? -1 : stack[--sp * 64];
   }
+}
+// descend (speculatively with RT_WF_SPEC, as next_leaf), then the leaf to
+// walk: the candidate set, and so the list's use, does not depend on the
+// order leaves are visited (a cone with more than kWfConeK candidates
+// overflows whichever leaves come first)
+template <bool kCount, bool kFull>
+__device__ __forceinline__ int cone_next_leaf(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
+                                              const ConeQ& k, int& cur, int& sp, int& pend, int* stack,
+                                              Counters& c) {
+#if RT_WF_SPEC
+  for (;;) {
+    if (pend < 0 && is_leaf(cur) && sp > 0) {
+      pend = cur;
+      cur = stack[--sp * 64];
+    }
+    if (__ballot(pend < 0 && (cur & 7) == 0) == 0) break;
+    if ((cur & 7) == 0) cone_step<kCount, kFull>(qb, lt, nlds, k, cur, sp, stack, c);
+  }
+#else
+  while ((cur & 7) == 0) cone_step<kCount, kFull>(qb, lt, nlds, k, cur, sp, stack, c);
+#endif
+  return take_leaf(cur, sp, pend, stack);
 }
 
 // lights base + i (i < 32) of a path that are lit (wf_shade1: not within
@@ -871,7 +948,7 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
   d3 P = mk(0, 0, 0), u = mk(0, 0, 0);
   double ldist = 0;
   ConeQ k{};
-  int excl = -1, found = 0, cur = -1, sp = 0;
+  int excl = -1, found = 0, cur = -1, sp = 0, pend = -1;
   for (;;) {
     const unsigned long long idle = __ballot(!busy);
     if (more && (__popcll(idle) >= kRefill || idle == ~0ull) && js.next >= js.hi)
@@ -895,6 +972,7 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
         found = ok ? 0 : kWfConeK + 1;
         cur = ok ? bvh_code(p.g.bvh[0]) : -1;
         sp = 0;
+        pend = -1;
         busy = true;
       }
     }
@@ -903,9 +981,9 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
       continue;
     }
     if (busy) {
-      cone_descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, k, cur, sp, stack, c);
-      if (cur != -1) {
-        const int first = cur >> 3, count = cur & 7;
+      const int lf = cone_next_leaf<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, k, cur, sp, pend, stack, c);
+      if (lf != -1) {
+        const int first = lf >> 3, count = lf & 7;
         DSphere ls[kLeafBatch];
         load_leaf(p.g.spheres, first, count, ls);
         int32_t* cl = p.cand + (size_t)key * kWfConeK;
@@ -918,9 +996,9 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
             ++found;
           }
         }
-        cur = found > kWfConeK || sp == 0 ? -1 : stack[--sp * 64];
+        if (found > kWfConeK) cur = pend = -1;
       }
-      if (cur == -1) {  // walked (or too many candidates: the rays are traced)
+      if (cur == -1 && pend < 0) {  // walked (or too many candidates: the rays are traced)
         busy = false;
         if (found == 0) {
           p.lstate[key] = kListBit | kEmptyBit;
@@ -947,12 +1025,13 @@ __device__ __forceinline__ uint64_t sid_soft_key(const WfParams& p, uint32_t sid
 }
 
 // ---------------------------------------------------------------- softgen
-// For every light whose hard ray is clear, in light order, the 16 points of
-// calculateSmartShadow's soft rays from the path's stream (rejection
-// sampling, vector.go:132-139), as 16 consecutive soft-queue entries.  A
-// light whose cone left a candidate list (wf_cone) has its 16 entries
-// written from the far end of the shard's queue instead (list_cnt counts
-// them), for wf_listtest; the others are traced by wf_occlude<soft>.
+// For every light whose hard ray is clear, in light order: a cone with more
+// than kWfConeK candidates gets the 16 points of calculateSmartShadow's soft
+// rays from its stream (rejection sampling, vector.go:132-139) as 16
+// consecutive soft-queue entries, traced by wf_occlude<soft>; a listed cone
+// (wf_cone) gets one entry, its key, from the far end of the shard's queue
+// (list_cnt counts them), and wf_listtest draws its points; an empty cone
+// gets nothing (its rays cannot be blocked).
 template <bool kCount>
 __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
   __shared__ int s_wave[kWfBlock / 64];
@@ -973,8 +1052,8 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
   }
   const int shard = blockIdx.x % kWfShards;
   // the 16 points of each light of `own`: traced rays at entries q.. of the
-  // shard's queue, a listed light's at the 16 entries ending before
-  // soft_cap - ql (ql += 16).  Each light's points come from its own stream
+  // shard's queue, a listed light's two entries ending before soft_cap - ql
+  // (ql += 2).  Each light's points come from its own stream
   // (spec v4: (sample, depth, light), include/rt_rng.h); an empty cone's rays
   // cannot be blocked and need none, so nothing is drawn for it (the
   // counting variant walks its tries for the reference's draw count).
@@ -989,23 +1068,33 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
       cnt<kCount>(c, C_SHADOW, 16);
       const bool keep = !(empty & bit);
       if (!keep && !kCount) continue;
-      size_t at;  // (an index, not a bumped pointer)
-      if (!keep) {
-        at = 0;
-      } else if (listed & bit) {
-        at = (size_t)(p.soft_cap - ql - 16);
-        ql += 16;
-      } else {
+      // (r05) a listed cone gets two entries at the far end: its stream state
+      // and which of its first 64 tries were accepted; wf_listtest rebuilds
+      // the points from them through the jump table.  (Both kinds run the one
+      // rejection loop below: separate loops for listed and traced cones
+      // diverged, 20.5 -> 25.2 ms per C4 frame.)
+      const bool lst = keep && (listed & bit);
+      size_t at = 0;  // (an index, not a bumped pointer)
+      if (keep && !lst) {
         at = (size_t)q;
         q += 16;
       }
       rt_rng rng{rt_soft_state(skey, depth, (uint32_t)li)};
-      for (int k = 0; k < 16;) {
+      const uint64_t x0 = rng.x;
+      uint64_t mask = 0;
+      for (int k = 0, t = 0; k < 16; ++t) {
         const uint32_t ux = rt_rng_next(&rng), uy = rt_rng_next(&rng), uz = rt_rng_next(&rng);
-        cnt<kCount>(c, C_RNG, 3);
+        if (!lst || t < 64) cnt<kCount>(c, C_RNG, 3);  // (a listed cone's later tries: wf_listtest)
         const bool acc = unit_ball_accept(ux, uy, uz);
-        if (acc && keep) sq[at + k] = make_uint4(key, ux, uy, uz);
+        if (acc && keep && !lst) sq[at + k] = make_uint4(key, ux, uy, uz);
+        mask |= acc && t < 64 ? 1ull << (t & 63) : 0ull;
         k += acc ? 1 : 0;
+      }
+      if (lst) {
+        uint4* le = sq + (p.soft_cap - ql - 2);
+        le[0] = make_uint4(key, (uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)mask);
+        le[1] = make_uint4((uint32_t)(mask >> 32), 0u, 0u, 0u);
+        ql += 2;
       }
     }
   };
@@ -1029,7 +1118,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
     const uint32_t ws = work ? s_slot[threadIdx.x] : 0u, wo = work ? s_own[threadIdx.x] : 0u;
     const uint32_t wl = work ? s_list[threadIdx.x] : 0u, we = work ? s_empty[threadIdx.x] : 0u;
     const int q = block_append(16 * __popc(wo & ~wl), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
-    const int ql = block_append(16 * __popc(wl & ~we), &p.ctl->list_cnt[shard * 32], s_wave, &s_base);
+    const int ql = block_append(2 * __popc(wl & ~we), &p.ctl->list_cnt[shard * 32], s_wave, &s_base);
     if (work) gen(ws, wo, wl, we, 0, q, ql);
     flush_counts<kCount>(p, c);
     return;
@@ -1039,7 +1128,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
     uint32_t listed, empty;
     const uint32_t own = clear_lights(p, slot, hit, base, &listed, &empty);
     const int q = block_append(16 * __popc(own & ~listed), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
-    const int ql = block_append(16 * __popc(listed & ~empty), &p.ctl->list_cnt[shard * 32], s_wave, &s_base);
+    const int ql = block_append(2 * __popc(listed & ~empty), &p.ctl->list_cnt[shard * 32], s_wave, &s_base);
     if (own) gen(slot, own, listed, empty, base, q, ql);
   }
   flush_counts<kCount>(p, c);
@@ -1054,13 +1143,17 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
 // (One ray per thread, the cone's 16 lanes sharing its loads and a ballot
 // for the count: 41 vs 31 ms per C4 frame; rays outer, each entry read once
 // and the candidates re-read from L2 per ray: 51 vs 31 ms.)
-#ifndef RT_LISTTEST_REGS
-#define RT_LISTTEST_REGS 1
-#endif
+// the two entries of listed cone j at the far end of its shard (wf_softgen):
+// {key, stream state lo, hi, accepted-try mask lo}, {mask hi, 0, 0, 0}
+__device__ __forceinline__ const uint4* list_entry(const WfParams& p, const Dense& dn, int j) {
+  const size_t at = dense_at(dn, 2 * j, p.soft_cap);
+  const size_t sh = at / (size_t)p.soft_cap, off = at - sh * (size_t)p.soft_cap;
+  return reinterpret_cast<const uint4*>(p.softq) + sh * (size_t)p.soft_cap + (p.soft_cap - off - 2);
+}
 template <bool kCount>
 __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
-  const Dense dn = dense(p.ctl->list_cnt);  // (entries: 16 per cone, so no cone spans two shards)
-  const int n = dn.start[kWfShards] / 16;
+  const Dense dn = dense(p.ctl->list_cnt);  // (two entries per cone, in one shard)
+  const int n = dn.start[kWfShards] / 2;
   if ((int)(blockIdx.x * kWfBlock) >= n) return;
   int j = blockIdx.x * kWfBlock + threadIdx.x;
   Counters c;
@@ -1075,9 +1168,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
     __syncthreads();
     int b = 0;
     if (j < n) {
-      const size_t at = dense_at(dn, 16 * j, p.soft_cap);
-      const size_t sh = at / (size_t)p.soft_cap, off = at - sh * (size_t)p.soft_cap;
-      const uint32_t key = reinterpret_cast<const uint4*>(p.softq)[sh * (size_t)p.soft_cap + (p.soft_cap - off - 16)].x;
+      const uint32_t key = list_entry(p, dn, j)->x;
       // groups of four up to the one holding the list's end (-1; entries
       // past it are stale): bucket 1, 2, 3-4, 5+ groups
       const int4* cl = reinterpret_cast<const int4*>(p.cand + (size_t)key * kWfConeK);
@@ -1094,29 +1185,52 @@ __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
     j = s_order[threadIdx.x];
   }
   if (j < n) {
-    const size_t at = dense_at(dn, 16 * j, p.soft_cap);
-    const size_t sh = at / (size_t)p.soft_cap, off = at - sh * (size_t)p.soft_cap;
-    const uint4* e = reinterpret_cast<const uint4*>(p.softq) + sh * (size_t)p.soft_cap + (p.soft_cap - off - 16);
-    // (r05) the cone's 16 entries (256 contiguous bytes) are read once, all
-    // loads issued together, and kept in registers for every candidate group:
-    // re-reading entry r per group let the lines of a wave's 64 cones (16 KB)
-    // fall out of L2 between the reads -- the soft queue is GBs per frame --
-    // so the kernel fetched 140 GB per C4 frame for ~20 GB of entries
-    // (profiles/r05_pmc_traffic.json)
-#if RT_LISTTEST_REGS
+    // (r05) the cone's 16 points, rebuilt from its stream state and the
+    // tries wf_softgen accepted: try t's draws are 3t..3t+2 (the jump table
+    // gives the state before draw 3t), so no rejection loop runs here; the
+    // queue carries 32 B per cone instead of the 16 points' 256 B.  (If the
+    // 16th point needs more than 64 tries, about once in 10^6 cones, the
+    // rest come from the sequential loop from try 64.)  Kept in registers
+    // for every candidate group.
+    const uint4* e = list_entry(p, dn, j);
+    const uint4 e0 = e[0];
+    const uint32_t key = e0.x;
+    const uint64_t x0 = (uint64_t)e0.y | (uint64_t)e0.z << 32;
+    uint64_t mask = (uint64_t)e0.w | (uint64_t)e[1].x << 32;
     uint32_t ux[16], uy[16], uz[16];
-    uint32_t key = 0;
+    {
+      uint64_t xt = 0;
+      bool tail = false;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const uint4 er = e[r];
-      if (r == 0) key = er.x;
-      ux[r] = er.y;
-      uy[r] = er.z;
-      uz[r] = er.w;
+      for (int r = 0; r < 16; ++r) {
+        if (mask != 0) {
+          const int t = __builtin_ctzll(mask);
+          mask &= mask - 1;
+          const uint64_t s0 = state_at3(x0, p.jump, t), s1 = s0 * RT_PCG_MULT + RT_PCG_INC,
+                         s2 = s1 * RT_PCG_MULT + RT_PCG_INC;
+          ux[r] = rt_pcg_out(s0);
+          uy[r] = rt_pcg_out(s1);
+          uz[r] = rt_pcg_out(s2);
+        } else {
+          if (!tail) {
+            xt = state_at3(x0, p.jump, 64);
+            tail = true;
+          }
+          rt_rng rng{xt};
+          for (;;) {
+            const uint32_t a = rt_rng_next(&rng), b = rt_rng_next(&rng), z = rt_rng_next(&rng);
+            cnt<kCount>(c, C_RNG, 3);
+            if (unit_ball_accept(a, b, z)) {
+              ux[r] = a;
+              uy[r] = b;
+              uz[r] = z;
+              break;
+            }
+          }
+          xt = rng.x;
+        }
+      }
     }
-#else
-    const uint32_t key = e[0].x;
-#endif
     const uint32_t slot = key / (uint32_t)p.nl, li = key - slot * (uint32_t)p.nl;
     const d3 o = ld_P(p, (int)slot);
     d3 ldir;
@@ -1138,12 +1252,8 @@ __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
 #pragma unroll 1
       for (int r = 0; r < 16; ++r) {
         if (blocked & (1u << r)) continue;
-#if RT_LISTTEST_REGS  // (a wave-uniform index: v_movrels, no scratch)
+        // (a wave-uniform index: v_movrels, no scratch)
         const d3 pt = mk(rt_bits_to_unit(ux[r]) * 2 - 1, rt_bits_to_unit(uy[r]) * 2 - 1, rt_bits_to_unit(uz[r]) * 2 - 1);
-#else
-        const uint4 er = e[r];
-        const d3 pt = mk(rt_bits_to_unit(er.y) * 2 - 1, rt_bits_to_unit(er.z) * 2 - 1, rt_bits_to_unit(er.w) * 2 - 1);
-#endif
         const d3 d = normalize(ldir + muls(pt, 0.1));
         const double av = len2(d), inv_a = approx_rcp(av);
         bool b = false;
