@@ -161,11 +161,12 @@ def test_counts_with_an_opted_in_sky_keep_the_image():
     assert counted[1].tobytes() == plain[1].tobytes()
     c = counted[3]
     assert c.camera_rays == 64 * 48 * 3
-    # a sky culls no camera sample; only soft-shadow draws of lights whose
-    # rays cannot be blocked are culled (spec v4: not drawn by the product)
+    # a sky culls no camera sample; the culled work is the shadow rays the
+    # product does not trace (empty shadow cones, inert lights), their sphere
+    # tests and their soft-shadow draws (spec v4: not drawn by the product)
     cull = c.culled_dict()
-    assert all(v == 0 for k, v in cull.items() if k != "rng_draws")
-    assert cull["rng_draws"] % 3 == 0
+    assert cull["camera_rays"] == cull["bounce_rays"] == cull["shade_events"] == cull["light_evals"] == 0
+    assert cull["rng_draws"] % 3 == 0 and cull["shadow_rays"] <= c.shadow_rays
 
 
 def test_culled_counts_are_the_skipped_camera_samples():
@@ -180,7 +181,9 @@ def test_culled_counts_are_the_skipped_camera_samples():
     # which the product does not draw (spec v4, include/rt_rng.h)
     extra = cull["rng_draws"] - 2 * cull["camera_rays"]
     assert extra >= 0 and extra % 3 == 0
-    assert cull["shade_events"] == cull["shadow_rays"] == cull["light_evals"] == 0  # culled samples miss
+    assert cull["shade_events"] == cull["light_evals"] == 0  # culled samples miss
+    # (shadow rays the product does not trace: empty cones, inert lights)
+    assert 0 < cull["shadow_rays"] < c.shadow_rays
     assert ex["shade_events"] == c.shade_events
     # the as-committed scene: every camera ray misses, every sample is culled
     black = render_dev(load_case(rtgo, ("file", "sphere_reflections_light.json")), 64, 48,
