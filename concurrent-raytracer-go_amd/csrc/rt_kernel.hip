@@ -288,6 +288,26 @@ __device__ __forceinline__ unsigned long long cone_wide(const Geo& g, bool need,
   return __shfl(m, lead);
 }
 
+// ------------------------------------------------------------ inert lights
+// (r05) A lit light whose shadow rays cannot change the shading: cos =
+// Max(0, N.L) is 0, so calculateDirectLighting's intensity is 0 * I / d^2 =
+// +0 and each term it adds is (finite) * 0 * shadowFactor * ... = +-0, and
+// adding +-0 to D, which has no zero component, leaves D's bits unchanged --
+// whether the term is added (shadow factor > 0) or not (= 0).  Finite means:
+// the light's intensity and colour, the material's albedo, metallic and
+// diffuse strength (the specular power is of a unit or zero half vector:
+// Vec3.Normalize keeps zero, vector.go:61-67, so it is finite).  Such a
+// light's hard and soft
+// shadow rays are not traced (their result is not observable) and its soft
+// points are not drawn (spec v4).  `D` is the ambient plus the terms of the
+// lights before this one.
+__device__ __forceinline__ bool light_inert(const DMat* m, const DLight& Lt, d3 N, d3 ldir, d3 D) {
+  return gmax0(dot(N, ldir)) == 0.0 && D.x != 0.0 && D.y != 0.0 && D.z != 0.0 && __builtin_isfinite(Lt.intensity) &&
+         __builtin_isfinite(Lt.color[0] + Lt.color[1] + Lt.color[2]) &&
+         __builtin_isfinite(m->albedo[0] + m->albedo[1] + m->albedo[2]) && __builtin_isfinite(m->metallic) &&
+         __builtin_isfinite(m->diffuse_strength);
+}
+
 // ------------------------------------------------------------ soft shadows
 // Cooperative form for ONE owner lane, executed by the whole (converged)
 // wave: lane h evaluates rejection try h of the owner's stream (draws
@@ -1051,13 +1071,8 @@ __device__ RT_SOLO_ATTR d3 solo_path(KArg karg, int ow, d3 o, d3 d, d3 T, d3 L, 
       const bool occl = __ballot(blk) != 0;
       int unocc = 0;
       if (!occl && h.soft) {
-        // the 16 soft rays (renderer.go:311-327); `quiet` as in the main loop
-        const bool quiet = gmax0(dot(N, ldir)) == 0.0 && D.x != 0.0 && D.y != 0.0 && D.z != 0.0 &&
-                           __builtin_isfinite(Lt.intensity) &&
-                           __builtin_isfinite(Lt.color[0] + Lt.color[1] + Lt.color[2]) &&
-                           __builtin_isfinite(m->albedo[0] + m->albedo[1] + m->albedo[2]) &&
-                           __builtin_isfinite(m->metallic);
-        const bool trace = (cm.s | cm.t) != 0 && !quiet;
+        // the 16 soft rays (renderer.go:311-327), not traced for an inert light
+        const bool trace = (cm.s | cm.t) != 0 && !light_inert(m, Lt, N, ldir, D);
         // (spec v4: the points come from the light's own stream; rays that
         // cannot be blocked need none of them)
         if (trace) {
@@ -1583,42 +1598,48 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
               cnt<kCount>(c, C_SHADOW);
             }
           }
+          // (r05) an inert light (light_inert): its shadow rays are not
+          // traced (the counting variant traces them, for the reference's
+          // counts, and books them as culled)
+          const bool dark = shade && lit && light_inert(m, Lt, N, ldir, D);
+          const bool hard = shade && lit && (kCount || !dark);
           bool wide_c = false;
           if constexpr (kStage) {  // few lit hit points: the cone tests with helpers
             if (masks && gg.nt == 0) {
-              const unsigned long long cq = __ballot(shade && lit);
+              const unsigned long long cq = __ballot(hard);
               const int ncq = __popcll(cq);
               if (ncq > 0 && ncq <= 16) {
-                const unsigned long long ms = cone_wide(gg, shade && lit, cq, ncq, P, N, front, self, ldir, ldist);
-                if (shade && lit) cm = Cand{ms, 0ull};
+                const unsigned long long ms = cone_wide(gg, hard, cq, ncq, P, N, front, self, ldir, ldist);
+                if (hard) cm = Cand{ms, 0ull};
                 wide_c = true;
               }
             }
           }
-          if (shade && lit) {
+          if (hard) {
             if (masks && !wide_c) cm = cone_candidates(gg, P, N, front, self, ldir, ldist);
-            occl = shadow_blocked<kCount>(gg, masks, P, ldir, ldist, cm, stack, c);  // hard shadow ray
+            if constexpr (kCount) {
+              const unsigned long long s0 = c.v[C_SPH], t0 = c.v[C_TRI];
+              occl = shadow_blocked<kCount>(gg, masks, P, ldir, ldist, cm, stack, c);  // hard shadow ray
+              if (dark) {
+                culled.v[C_SHADOW] += 1;
+                culled.v[C_SPH] += c.v[C_SPH] - s0;
+                culled.v[C_TRI] += c.v[C_TRI] - t0;
+              }
+            } else {
+              occl = shadow_blocked<kCount>(gg, masks, P, ldir, ldist, cm, stack, c);  // hard shadow ray
+            }
           }
 #ifdef RT_WG_TIMING
           dbg_hard += __builtin_amdgcn_s_memtime() - th0;
 #endif
           const bool need_soft = lit && !occl && soft;
-          // The 16 soft rays' draws are always consumed, but their result
-          // only scales terms multiplied by cos = Max(0, N.L): when that is
-          // exactly 0 (the light is behind the surface), the light and
-          // material terms are finite and D has no zero component (so adding
-          // a signed zero cannot change it), the shading is the same
-          // whatever the rays hit, and they are not traced (exact shortcut).
-          const bool quiet = gmax0(dot(N, ldir)) == 0.0 && D.x != 0.0 && D.y != 0.0 && D.z != 0.0 &&
-                             __builtin_isfinite(Lt.intensity) &&
-                             __builtin_isfinite(Lt.color[0] + Lt.color[1] + Lt.color[2]) &&
-                             __builtin_isfinite(m->albedo[0] + m->albedo[1] + m->albedo[2]) &&
-                             __builtin_isfinite(m->metallic);
-          const bool trace = (!masks || (cm.s | cm.t) != 0) && !quiet;
+          // the 16 soft rays are traced unless their shadow cone is empty or
+          // the light is inert (dark: the shading is the same whatever they hit)
+          const bool trace = (!masks || (cm.s | cm.t) != 0) && !dark;
           int unocc = 0;
           // Spec v4 (include/rt_rng.h): the 16 points come from the stream of
           // (sample, depth, light), not from the path's.  A lane whose rays
-          // cannot be blocked (empty shadow cone, or quiet) needs none of them:
+          // cannot be blocked (empty shadow cone, or dark) needs none of them:
           // all 16 are unoccluded, nothing is drawn.  (The counting variant
           // still walks their tries, for the reference's draw count, and
           // books them as culled: executed work is the difference.)
@@ -1634,6 +1655,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
               }
               cnt<kCount>(c, C_SHADOW, 16);
               cnt<kCount>(c, C_RNG, 3ull * tries);
+              culled.v[C_SHADOW] += 16;
               culled.v[C_RNG] += 3ull * tries;
             }
           }

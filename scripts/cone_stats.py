@@ -146,6 +146,7 @@ def main():
         "candidates_mean": round(float(cands.mean()), 3),
         "candidates_p50_p90_p99_max": [float(x) for x in np.percentile(cands, [50, 90, 99])] + [int(cands.max())],
         "more_than_16": round(float(over.mean()), 4),
+        "more_than_32_64_128": [round(float((cands > k).mean()), 4) for k in (32, 64, 128)],
         "cone_walk_nodes_mean": round(float(cone_vis.mean()), 1),
         "soft_rays_nodes_mean_per_cone": round(float(soft_vis.mean()), 1),
         "nodes_with_lists_vs_rays": round(float((cone_vis.sum() + soft_vis[over].sum()) / soft_vis.sum()), 4),
