@@ -671,11 +671,14 @@ static int run_pilot(const rt_context* c, const KParams& p, SchedParams* sp, cha
 // 144.8 k, 1536 143.0 k, 2048 139.9 k Mrays/s; C3 256 -> 393.9 k, 512
 // 419.8 k, 768 461.8 k, 1024 474.9 k, 2048 480.1 k (16 frames per launch:
 // C2 896 144.4 k, 1024 146.2 k, 1280 145.4 k; C3 1024 463.7 k, 1536 476.1 k,
-// 2048 479.1 k).
+// 2048 479.1 k).  (r05, RNG spec v4: a bounce-sample costs less, so blocks
+// grow: the driver's 20 frames as 2 launches of 10, C2 1024 -> 212.5 k, 1536
+// 223.7 k, 2048 215.0 k, 3072 212.6 k, 4096 208.6 k; 100 frames as 4 of 25:
+// 247.8 k, 251.6 k, 251.0 k, 249.6 k, 248.3 k; scripts/k20_tuning.sh)
 static double default_block_work(const rt_context* c, int frames = 1) {
   const FlatScene& f = c->flat;
   double block_work = !f.bvh.empty() ? 8192.0
-                      : frames > 1    ? (f.tris.empty() ? 1024.0 : 2048.0)
+                      : frames > 1    ? (f.tris.empty() ? 1536.0 : 2048.0)
                                       : (f.tris.empty() ? 384.0 : 256.0);
   if (c->tun.block_work > 0) block_work = std::max(1.0, c->tun.block_work);
   return block_work;

@@ -2,7 +2,7 @@
 # GPU-box: one bench line per BASELINE config (c1 as committed, c2 headline,
 # c3, c4, c5 on one GPU) with their CPU baselines, into gpurun_out/TAG_configs.jsonl
 set -eu
-TAG=${1:-r04}
+TAG=${1:-r05}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 O=gpurun_out/${TAG}_configs.jsonl
