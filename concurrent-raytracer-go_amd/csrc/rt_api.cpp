@@ -1503,6 +1503,8 @@ int rt_context_get_stats(const rt_context* c, rt_context_stats* out) {
     return RT_E_INVALID;
   }
   *out = c->stats;
+  out->blocks = c->num_blocks;
+  out->split_pixels = c->nsplit;
   return RT_OK;
 }
 

@@ -170,7 +170,7 @@ class ContextStats(ctypes.Structure):
     """rt_context_stats (rt_context_get_stats)."""
 
     _fields_ = [(n, ctypes.c_int64) for n in ("schedules_built", "measuring_frames", "frames", "launches",
-                                             "batched_launches")]
+                                             "batched_launches", "blocks", "split_pixels")]
 
 
 COUNT_FIELDS = [
@@ -745,7 +745,8 @@ class Context:
         return {k: (s[i], int(n[i])) for i, k in enumerate(WF_KERNELS)}
 
     def stats(self) -> dict:
-        """rt_context_get_stats: schedules built, measuring frames, frames, launches, batched launches."""
+        """rt_context_get_stats: schedules built, measuring frames, frames, launches, batched launches;
+        the last schedule's work blocks and split pixels."""
         s = ContextStats()
         _check(lib().rt_context_get_stats(self._h, ctypes.byref(s)))
         return {k: getattr(s, k) for k, _ in ContextStats._fields_}

@@ -378,6 +378,7 @@ int rt_context_render_frames_async(rt_context* ctx, int32_t width, int32_t heigh
  * and the launches that rendered several frames at once. */
 typedef struct {
   int64_t schedules_built, measuring_frames, frames, launches, batched_launches;
+  int64_t blocks, split_pixels;  /* of the schedule last used: work blocks, pixels split over sub-blocks */
 } rt_context_stats;
 int rt_context_get_stats(const rt_context* ctx, rt_context_stats* out);
 
