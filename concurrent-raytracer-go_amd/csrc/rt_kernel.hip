@@ -64,12 +64,6 @@ constexpr int kSqTail = RT_SQ_TAIL;
 #define RT_SQ_TRIES 2
 #endif
 constexpr int kSqTries = RT_SQ_TRIES;
-// soft_queue: with at most this many owners still drawing, the wave draws
-// in groups (each owner's tries spread over 64 / owners lanes; 0: off)
-#ifndef RT_SQ_GROUP
-#define RT_SQ_GROUP 0
-#endif
-constexpr int kSqGroup = RT_SQ_GROUP;
 
 namespace rtgo {
 
@@ -384,134 +378,83 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
   }
 #endif
   for (;;) {
-    const unsigned long long rem = __ballot(need > 0);
-    if (kSqGroup > 0 && rem != 0 && __popcll(rem) <= kSqGroup) {
-      // (r05) Grouped draws: with nr owners still drawing, group g (of
-      // G = 2^floor(log2(64 / nr)) lanes) serves the g-th of them: lane h
-      // evaluates try h of that owner's stream from the jump table (as
-      // soft_coop does with 64 lanes), the group's first `need` accepted
-      // tries are queued, and the owner's stream jumps past the last one
-      // taken -- the same draws and points as its sequential loop.  Groups
-      // are re-formed every round, so the last owners get the widest ones.
-      const int nr = __popcll(rem);
-      const int lgG = 31 - __builtin_clz(64 / nr);
-      const int G = 1 << lgG;
-      const int g = lane >> lgG, h = lane & (G - 1);
-      const bool act = g < nr;
-      // owner lane of group g: owners' lane ids compacted by rank (a permutation)
-      const int rank_own = lanes_below(rem);
-      const int dst = need > 0 ? rank_own : nr + lanes_below(~rem);
-      const int owl = __builtin_amdgcn_ds_permute(dst << 2, lane);
-      const int ow = __builtin_amdgcn_ds_bpermute((act ? g : 0) << 2, owl);
-      const uint64_t xg = __shfl(rng.x, ow);
-      const int ng = __shfl(need, ow);
-      const uint64_t x0 = state_at3(xg, jump, h), x1 = x0 * RT_PCG_MULT + RT_PCG_INC,
-                     x2 = x1 * RT_PCG_MULT + RT_PCG_INC;
-      const uint32_t o0 = rt_pcg_out(x0), o1 = rt_pcg_out(x1), o2 = rt_pcg_out(x2);
-      const bool acc = act && unit_ball_accept(o0, o1, o2);
-      const unsigned long long gm = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (g * G & 63);
-      const unsigned long long am = __ballot(acc);
-      const bool chosen = acc && lanes_below(am & gm) < ng;
-      const unsigned long long chm = __ballot(chosen);
-      const unsigned long long cg = chm & gm;
-      const int nch = __popcll(cg);
-      const int used = nch == ng ? 64 - __clzll(cg) - g * G : G;
-      // (only rays that can be blocked are queued: an owner that does not
-      // trace counts its points as unoccluded)
-      const unsigned long long qm = __ballot(chosen && __shfl(trace ? 1 : 0, ow) != 0);
-      if (qm >> lane & 1) sq[(unsigned)(tail + lanes_below(qm)) % kRing] = make_uint4(o0, o1, o2, (uint32_t)ow);
-      tail += __popcll(qm);
-      const uint64_t xn = state_at3(xg, jump, used);
-      // back to the owners: the owner of rank r reads its group's first lane
-      const int src = rank_own << lgG;
-      const uint64_t x_new = __shfl(xn, src);
-      const int need_new = __shfl(ng - nch, src), used_src = __shfl(used, src);
-      if (need > 0) {
-        cnt<kCount>(c, C_RNG, 3ull * used_src);
-        cnt<kCount>(c, C_SHADOW, need - need_new);
-        if (!trace) free_rays += need - need_new;
-        rng.x = x_new;
-        need = need_new;
-      }
-    } else {
-      // kSqTries tries per pass: the later tries are drawn ahead and each
-      // is consumed only when the owner still needs a point after the ones
-      // before it (so the stream advances by exactly the draws the sequential
-      // loop takes).
-      constexpr int K = kSqTries;
-      bool acc[K];
-      uint32_t u[K][3];
-  #pragma unroll
+    // kSqTries tries per pass: the later tries are drawn ahead and each
+    // is consumed only when the owner still needs a point after the ones
+    // before it (so the stream advances by exactly the draws the sequential
+    // loop takes).
+    constexpr int K = kSqTries;
+    bool acc[K];
+    uint32_t u[K][3];
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      acc[t] = false;
+      u[t][0] = u[t][1] = u[t][2] = 0;
+    }
+    if (need > 0) {
+      rt_rng r = rng;
+#pragma unroll
       for (int t = 0; t < K; ++t) {
-        acc[t] = false;
-        u[t][0] = u[t][1] = u[t][2] = 0;
-      }
-      if (need > 0) {
-        rt_rng r = rng;
-  #pragma unroll
-        for (int t = 0; t < K; ++t) {
-          u[t][0] = rt_rng_next(&r);
-          u[t][1] = rt_rng_next(&r);
-          u[t][2] = rt_rng_next(&r);
-          if (need > 0) {
-            rng = r;
-            cnt<kCount>(c, C_RNG, 3);
-            if (unit_ball_accept(u[t][0], u[t][1], u[t][2])) {
-              --need;
-              cnt<kCount>(c, C_SHADOW);
-              if (trace) acc[t] = true;  // only rays that can be blocked are queued
-              else ++free_rays;
-            }
+        u[t][0] = rt_rng_next(&r);
+        u[t][1] = rt_rng_next(&r);
+        u[t][2] = rt_rng_next(&r);
+        if (need > 0) {
+          rng = r;
+          cnt<kCount>(c, C_RNG, 3);
+          if (unit_ball_accept(u[t][0], u[t][1], u[t][2])) {
+            --need;
+            cnt<kCount>(c, C_SHADOW);
+            if (trace) acc[t] = true;  // only rays that can be blocked are queued
+            else ++free_rays;
           }
         }
       }
-  #pragma unroll
-      for (int t = 0; t < K; ++t) {
-        const unsigned long long am = __ballot(acc[t]);
-        if (acc[t]) sq[(unsigned)(tail + lanes_below(am)) % kRing] = make_uint4(u[t][0], u[t][1], u[t][2], (uint32_t)lane);
-        tail += __popcll(am);
-      }
-      if constexpr (kSqTail > 0) {
-        // The last few owners still drawing finish cooperatively, one at a
-        // time: lane h evaluates try h of the owner's stream (jump table), as
-        // in soft_coop; the first `need` accepted tries are its points, queued
-        // in try order, and the stream advances past the last one taken.  The
-        // wave no longer loops on its unluckiest owners' tries one by one.
-        // (at most 16 points per owner: the ring holds them, see kRing)
-        const unsigned long long rem = __ballot(need > 0);
-        if (rem != 0 && __popcll(rem) <= kSqTail) {
-          for (unsigned long long b = rem; b; b &= b - 1) {
-            const int ow = __builtin_ctzll(b);
-            int nd = __builtin_amdgcn_readlane(need, ow);
-            const bool tr = __builtin_amdgcn_readlane(trace ? 1 : 0, ow) != 0;
-            uint64_t x = rl64(rng.x, ow);
-            int got = 0, tries = 0;
-            while (nd > 0) {
-              const uint64_t x0 = state_at3(x, jump, lane), x1 = x0 * RT_PCG_MULT + RT_PCG_INC,
-                             x2 = x1 * RT_PCG_MULT + RT_PCG_INC;
-              const uint32_t o0 = rt_pcg_out(x0), o1 = rt_pcg_out(x1), o2 = rt_pcg_out(x2);
-              const bool acc = unit_ball_accept(o0, o1, o2);
-              const unsigned long long am = __ballot(acc);
-              const bool chosen = acc && lanes_below(am) < nd;
-              const unsigned long long chm = __ballot(chosen);
-              const int nch = __popcll(chm);
-              const int used = nch == nd ? 64 - __clzll(chm) : 64;
-              if (tr) {
-                if (chosen) sq[(unsigned)(tail + lanes_below(chm)) % kRing] = make_uint4(o0, o1, o2, (uint32_t)ow);
-                tail += nch;
-              }
-              got += nch;
-              nd -= nch;
-              tries += used;
-              x = state_at3(x, jump, used);
+    }
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const unsigned long long am = __ballot(acc[t]);
+      if (acc[t]) sq[(unsigned)(tail + lanes_below(am)) % kRing] = make_uint4(u[t][0], u[t][1], u[t][2], (uint32_t)lane);
+      tail += __popcll(am);
+    }
+    if constexpr (kSqTail > 0) {
+      // The last few owners still drawing finish cooperatively, one at a
+      // time: lane h evaluates try h of the owner's stream (jump table), as
+      // in soft_coop; the first `need` accepted tries are its points, queued
+      // in try order, and the stream advances past the last one taken.  The
+      // wave no longer loops on its unluckiest owners' tries one by one.
+      // (at most 16 points per owner: the ring holds them, see kRing)
+      const unsigned long long rem = __ballot(need > 0);
+      if (rem != 0 && __popcll(rem) <= kSqTail) {
+        for (unsigned long long b = rem; b; b &= b - 1) {
+          const int ow = __builtin_ctzll(b);
+          int nd = __builtin_amdgcn_readlane(need, ow);
+          const bool tr = __builtin_amdgcn_readlane(trace ? 1 : 0, ow) != 0;
+          uint64_t x = rl64(rng.x, ow);
+          int got = 0, tries = 0;
+          while (nd > 0) {
+            const uint64_t x0 = state_at3(x, jump, lane), x1 = x0 * RT_PCG_MULT + RT_PCG_INC,
+                           x2 = x1 * RT_PCG_MULT + RT_PCG_INC;
+            const uint32_t o0 = rt_pcg_out(x0), o1 = rt_pcg_out(x1), o2 = rt_pcg_out(x2);
+            const bool acc = unit_ball_accept(o0, o1, o2);
+            const unsigned long long am = __ballot(acc);
+            const bool chosen = acc && lanes_below(am) < nd;
+            const unsigned long long chm = __ballot(chosen);
+            const int nch = __popcll(chm);
+            const int used = nch == nd ? 64 - __clzll(chm) : 64;
+            if (tr) {
+              if (chosen) sq[(unsigned)(tail + lanes_below(chm)) % kRing] = make_uint4(o0, o1, o2, (uint32_t)ow);
+              tail += nch;
             }
-            if (lane == ow) {
-              rng.x = x;
-              need = 0;
-              if (!tr) free_rays += got;
-              cnt<kCount>(c, C_RNG, 3ull * tries);
-              cnt<kCount>(c, C_SHADOW, got);
-            }
+            got += nch;
+            nd -= nch;
+            tries += used;
+            x = state_at3(x, jump, used);
+          }
+          if (lane == ow) {
+            rng.x = x;
+            need = 0;
+            if (!tr) free_rays += got;
+            cnt<kCount>(c, C_RNG, 3ull * tries);
+            cnt<kCount>(c, C_SHADOW, got);
           }
         }
       }

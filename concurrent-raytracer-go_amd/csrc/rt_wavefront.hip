@@ -323,80 +323,26 @@ __device__ __forceinline__ void load_pair(glb_node* __restrict__ qb, lds_node* _
   }
 }
 template <bool kCount, bool kFull>
-__device__ __forceinline__ void node_step(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
-                                          const RayQ& r, float tminf, float tmaxf, int& cur, int& sp, int* stack,
-                                          Counters& c) {
-  uint4 L, R;
-  load_pair<kFull>(qb, lt, nlds, cur >> 3, L, R);
-  cnt<kCount>(c, C_BOX, 2);
-  float tl, tr;
-  const bool hl = box_q(L, r, tminf, tmaxf, tl), hr = box_q(R, r, tminf, tmaxf, tr);
-  if (hl || hr) {
-    const bool lfirst = hl && (!hr || tl <= tr);
-    if (hl && hr) {
-      stack[sp * 64] = lfirst ? (int)R.w : (int)L.w;
-      ++sp;
-    }
-    cur = lfirst ? (int)L.w : (int)R.w;
-  } else {
-    cur = sp == 0 ? -1 : stack[--sp * 64];
-  }
-}
-template <bool kCount, bool kFull>
 __device__ __forceinline__ void descend(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
                                         const RayQ& r, float tminf, float tmaxf, int& cur, int& sp, int* stack,
                                         Counters& c) {
-  while ((cur & 7) == 0) node_step<kCount, kFull>(qb, lt, nlds, r, tminf, tmaxf, cur, sp, stack, c);
-}
-
-// (r05) Speculative traversal (Aila & Laine 2009, postponed leaves): a lane
-// that reaches a leaf while its stack is not empty parks it in `pend` and
-// keeps descending from the stack; the node loop ends once no lane is still
-// looking for its first leaf, so the leaf tests that follow run on more lanes
-// at once.  The answer does not depend on the order leaves are tested
-// (any-hit; closest hit: the least t with the obj tie rule, as the BVH order
-// already differs from the scan order), so the images are unchanged.
-#ifndef RT_WF_SPEC
-#define RT_WF_SPEC 0
-#endif
-__device__ __forceinline__ bool is_leaf(int cur) { return cur != -1 && (cur & 7) != 0; }
-template <bool kCount, bool kFull>
-__device__ __forceinline__ void descend_spec(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
-                                             const RayQ& r, float tminf, float tmaxf, int& cur, int& sp, int& pend,
-                                             int* stack, Counters& c) {
-  for (;;) {
-    if (pend < 0 && is_leaf(cur) && sp > 0) {
-      pend = cur;
-      cur = stack[--sp * 64];
+  while ((cur & 7) == 0) {
+    uint4 L, R;
+    load_pair<kFull>(qb, lt, nlds, cur >> 3, L, R);
+    cnt<kCount>(c, C_BOX, 2);
+    float tl, tr;
+    const bool hl = box_q(L, r, tminf, tmaxf, tl), hr = box_q(R, r, tminf, tmaxf, tr);
+    if (hl || hr) {
+      const bool lfirst = hl && (!hr || tl <= tr);
+      if (hl && hr) {
+        stack[sp * 64] = lfirst ? (int)R.w : (int)L.w;
+        ++sp;
+      }
+      cur = lfirst ? (int)L.w : (int)R.w;
+    } else {
+      cur = sp == 0 ? -1 : stack[--sp * 64];
     }
-    if (__ballot(pend < 0 && (cur & 7) == 0) == 0) break;
-    if ((cur & 7) == 0) node_step<kCount, kFull>(qb, lt, nlds, r, tminf, tmaxf, cur, sp, stack, c);
   }
-}
-// The leaf to test after a descent (-1: none), the parked one first; cur
-// moves on past a leaf it takes.  The ray is done when cur is -1 afterwards.
-__device__ __forceinline__ int take_leaf(int& cur, int& sp, int& pend, const int* stack) {
-  if (pend >= 0) {
-    const int lf = pend;
-    pend = -1;
-    return lf;
-  }
-  if (!is_leaf(cur)) return -1;
-  const int lf = cur;
-  cur = sp == 0 ? -1 : stack[--sp * 64];
-  return lf;
-}
-// Either form: descend, then the leaf to test
-template <bool kCount, bool kFull>
-__device__ __forceinline__ int next_leaf(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
-                                         const RayQ& r, float tminf, float tmaxf, int& cur, int& sp, int& pend,
-                                         int* stack, Counters& c) {
-#if RT_WF_SPEC
-  descend_spec<kCount, kFull>(qb, lt, nlds, r, tminf, tmaxf, cur, sp, pend, stack, c);
-#else
-  descend<kCount, kFull>(qb, lt, nlds, r, tminf, tmaxf, cur, sp, stack, c);
-#endif
-  return take_leaf(cur, sp, pend, stack);
 }
 
 // The spheres of a leaf: the loads of the first kLeafBatch are issued
@@ -480,7 +426,7 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
   double av = 0, inv_a = 0, closest = 0;
   RayQ r32{};
   float tminf = 0;
-  int cur = -1, sp = 0, pend = -1, best_obj = -1, bidx = -1;
+  int cur = -1, sp = 0, best_obj = -1, bidx = -1;
   for (;;) {
     const unsigned long long idle = __ballot(!busy);
     if (more && (__popcll(idle) >= kRefill || idle == ~0ull) && js.next >= js.hi)
@@ -524,11 +470,9 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
       continue;
     }
     if (busy) {
-      const int lf =
-          next_leaf<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, t_hi32(closest), cur, sp, pend,
-                                   stack, c);
-      if (lf != -1) {  // a leaf: the exact Sphere.Hit tests, in hittable order
-        const int first = lf >> 3, count = lf & 7;
+      descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, t_hi32(closest), cur, sp, stack, c);
+      if (cur != -1) {  // a leaf: the exact Sphere.Hit tests, in hittable order
+        const int first = cur >> 3, count = cur & 7;
         DSphere ls[kLeafBatch];
         load_leaf(p.g.spheres, first, count, ls);
         for (int i = first; i < first + count; ++i) {
@@ -543,8 +487,9 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
             best_obj = S.obj;
           }
         }
+        cur = sp == 0 ? -1 : stack[--sp * 64];
       }
-      if (cur == -1 && pend < 0) {  // traversal done
+      if (cur == -1) {  // traversal done
         busy = false;
         if (best_obj >= 0) {
           // the hit point (HitRecord.P, sphere.go:44: t = the root / a, as
@@ -667,7 +612,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
   double av = 0, inv_a = 0, tmax = 0;
   RayQ r32{};
   float tminf = 0, tmaxf = 0;
-  int cur = -1, sp = 0, pend = -1;
+  int cur = -1, sp = 0;
   for (;;) {
     const unsigned long long idle = __ballot(!busy);
     if (more && (__popcll(idle) >= kRefill || idle == ~0ull) && js.next >= js.hi)
@@ -705,7 +650,6 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
           tmaxf = t_hi32(tmax);
           cur = bvh_code(p.g.bvh[0]);
           sp = 0;
-          pend = -1;
           busy = true;
         }
       }
@@ -715,11 +659,10 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
       continue;
     }
     if (busy) {
-      const int lf =
-          next_leaf<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, tmaxf, cur, sp, pend, stack, c);
+      descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, tmaxf, cur, sp, stack, c);
       bool blocked = false;
-      if (lf != -1) {
-        const int first = lf >> 3, count = lf & 7;
+      if (cur != -1) {
+        const int first = cur >> 3, count = cur & 7;
         DSphere ls[kLeafBatch];
         load_leaf(p.g.spheres, first, count, ls);
         for (int i = first; i < first + count && !blocked; ++i) {
@@ -727,6 +670,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
           double num;
           blocked = sphere_query(leaf_sphere(p.g.spheres, ls, first, i), o, d, av, inv_a, tmin, tmax, num) != 0;
         }
+        cur = sp == 0 ? -1 : stack[--sp * 64];
       }
       if (blocked) {
         if constexpr (kSoft)
@@ -734,7 +678,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
         else
           p.lstate[key] = kHardBit;
       }
-      if (blocked || (cur == -1 && pend < 0)) busy = false;
+      if (blocked || cur == -1) busy = false;
     }
   }
   flush_counts<kCount>(p, c, kSoft ? kGroupSoft : kGroupHard);
@@ -750,8 +694,8 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
 // the scene.  wf_conegen queues every (path, light) whose hard ray is clear;
 // wf_cone walks the BVH with the cone and, when at most kWfConeK spheres are
 // candidates, leaves their list and kListBit in lstate; wf_softgen queues
-// such a cone's key apart, and wf_listtest draws its 16 rays and tests them
-// against the list
+// such a cone's stream state and accepted tries apart, and wf_listtest
+// rebuilds its 16 rays and tests them against the list
 // -- the same Sphere.Hit test the traversal runs -- instead
 // of walking the tree.  C4 (scripts/cone_stats.py): 45 % of the clear cones
 // are empty, the median cone has 1 candidate, 6 % have more than 16.
@@ -840,43 +784,23 @@ __device__ __forceinline__ bool cone_keeps(const DSphere& S, d3 P, d3 u, double 
 }
 
 template <bool kCount, bool kFull>
-__device__ __forceinline__ void cone_step(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
-                                          const ConeQ& k, int& cur, int& sp, int* stack, Counters& c) {
-  uint4 L, R;
-  load_pair<kFull>(qb, lt, nlds, cur >> 3, L, R);
-  cnt<kCount>(c, C_BOX, 2);
-  const bool hl = cone_node(L, k), hr = cone_node(R, k);
-  if (hl || hr) {
-    if (hl && hr) {
-      stack[sp * 64] = (int)R.w;
-      ++sp;
+__device__ __forceinline__ void cone_descend(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
+                                             const ConeQ& k, int& cur, int& sp, int* stack, Counters& c) {
+  while ((cur & 7) == 0) {
+    uint4 L, R;
+    load_pair<kFull>(qb, lt, nlds, cur >> 3, L, R);
+    cnt<kCount>(c, C_BOX, 2);
+    const bool hl = cone_node(L, k), hr = cone_node(R, k);
+    if (hl || hr) {
+      if (hl && hr) {
+        stack[sp * 64] = (int)R.w;
+        ++sp;
+      }
+      cur = hl ? (int)L.w : (int)R.w;
+    } else {
+      cur = sp == 0 ? -1 : stack[--sp * 64];
     }
-    cur = hl ? (int)L.w : (int)R.w;
-  } else {
-    cur = sp == 0 ? -1 : stack[--sp * 64];
   }
-}
-// descend (speculatively with RT_WF_SPEC, as next_leaf), then the leaf to
-// walk: the candidate set, and so the list's use, does not depend on the
-// order leaves are visited (a cone with more than kWfConeK candidates
-// overflows whichever leaves come first)
-template <bool kCount, bool kFull>
-__device__ __forceinline__ int cone_next_leaf(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
-                                              const ConeQ& k, int& cur, int& sp, int& pend, int* stack,
-                                              Counters& c) {
-#if RT_WF_SPEC
-  for (;;) {
-    if (pend < 0 && is_leaf(cur) && sp > 0) {
-      pend = cur;
-      cur = stack[--sp * 64];
-    }
-    if (__ballot(pend < 0 && (cur & 7) == 0) == 0) break;
-    if ((cur & 7) == 0) cone_step<kCount, kFull>(qb, lt, nlds, k, cur, sp, stack, c);
-  }
-#else
-  while ((cur & 7) == 0) cone_step<kCount, kFull>(qb, lt, nlds, k, cur, sp, stack, c);
-#endif
-  return take_leaf(cur, sp, pend, stack);
 }
 
 // lights base + i (i < 32) of a path that are lit (wf_shade1: not within
@@ -948,7 +872,7 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
   d3 P = mk(0, 0, 0), u = mk(0, 0, 0);
   double ldist = 0;
   ConeQ k{};
-  int excl = -1, found = 0, cur = -1, sp = 0, pend = -1;
+  int excl = -1, found = 0, cur = -1, sp = 0;
   for (;;) {
     const unsigned long long idle = __ballot(!busy);
     if (more && (__popcll(idle) >= kRefill || idle == ~0ull) && js.next >= js.hi)
@@ -972,7 +896,6 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
         found = ok ? 0 : kWfConeK + 1;
         cur = ok ? bvh_code(p.g.bvh[0]) : -1;
         sp = 0;
-        pend = -1;
         busy = true;
       }
     }
@@ -981,9 +904,9 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
       continue;
     }
     if (busy) {
-      const int lf = cone_next_leaf<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, k, cur, sp, pend, stack, c);
-      if (lf != -1) {
-        const int first = lf >> 3, count = lf & 7;
+      cone_descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, k, cur, sp, stack, c);
+      if (cur != -1) {
+        const int first = cur >> 3, count = cur & 7;
         DSphere ls[kLeafBatch];
         load_leaf(p.g.spheres, first, count, ls);
         int32_t* cl = p.cand + (size_t)key * kWfConeK;
@@ -996,9 +919,9 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
             ++found;
           }
         }
-        if (found > kWfConeK) cur = pend = -1;
+        cur = found > kWfConeK || sp == 0 ? -1 : stack[--sp * 64];
       }
-      if (cur == -1 && pend < 0) {  // walked (or too many candidates: the rays are traced)
+      if (cur == -1) {  // walked (or too many candidates: the rays are traced)
         busy = false;
         if (found == 0) {
           p.lstate[key] = kListBit | kEmptyBit;
@@ -1029,9 +952,10 @@ __device__ __forceinline__ uint64_t sid_soft_key(const WfParams& p, uint32_t sid
 // than kWfConeK candidates gets the 16 points of calculateSmartShadow's soft
 // rays from its stream (rejection sampling, vector.go:132-139) as 16
 // consecutive soft-queue entries, traced by wf_occlude<soft>; a listed cone
-// (wf_cone) gets one entry, its key, from the far end of the shard's queue
-// (list_cnt counts them), and wf_listtest draws its points; an empty cone
-// gets nothing (its rays cannot be blocked).
+// (wf_cone) gets two entries, its stream state and accepted tries, from the
+// far end of the shard's queue (list_cnt counts them), and wf_listtest
+// rebuilds its points; an empty cone gets nothing (its rays cannot be
+// blocked).
 template <bool kCount>
 __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
   __shared__ int s_wave[kWfBlock / 64];
