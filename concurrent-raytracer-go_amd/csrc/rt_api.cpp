@@ -253,7 +253,8 @@ int rt_context_set_tuning(rt_context* c, const rt_tuning* t) {
     return RT_E_INVALID;
   }
   if (t->pilot_depth < 0 || t->split_samples < 0 || t->split_samples > 64 || t->bvh_leaf < 0 || t->bvh_leaf > 7 || t->bvh_bins < 0 || t->block_work < 0 || t->block_samples < 0 ||
-      t->wf_paths < 0 || t->wf_chunk < 0 || t->wf_trav_block < 0 || t->wf_trav_block > 1024 || t->wf_trav_wgs < 0) {
+      t->wf_paths < 0 || t->wf_chunk < 0 || t->wf_trav_block < 0 || t->wf_trav_block > 1024 || t->wf_trav_wgs < 0 ||
+      t->wf_list_tries < 0 || t->wf_list_tries > 64) {
     set_error("tuning value out of range");
     return RT_E_INVALID;
   }
@@ -920,6 +921,7 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   memset(&p, 0, sizeof p);
   p.g = Geo{kp.spheres, kp.tris, kp.boxes, kp.bvh, kp.ns, kp.nt, kp.use_bvh, kp.nb};
   p.jump = kp.jump;
+  p.list_tries = c->tun.wf_list_tries > 0 ? std::min(64, c->tun.wf_list_tries) : 64;
   p.qbvh = c->d_qbvh;
   memcpy(p.q0, f.q0, sizeof p.q0);
   memcpy(p.qd, f.qd, sizeof p.qd);

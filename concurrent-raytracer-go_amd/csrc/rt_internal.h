@@ -288,6 +288,7 @@ struct WfParams {
   uint32_t* softq;           // kWfShards queues of soft_cap entries, 4 words: {slot * nl + light, draws x, y, z}
                              // (listed cones, from the far end: 2 entries, wf_softgen)
   const uint64_t* jump;      // PCG jump table (KParams::jump)
+  int32_t list_tries;        // tries a listed cone's accepted-try mask covers (1..64, rt_tuning.wf_list_tries)
   uint32_t* coneq;           // kWfShards queues of hard_cap entries: slot * nl + light (clear hard ray)
   int32_t* cand;             // [slot * nl + light][kWfConeK]: the shadow cone's candidate spheres, -1 ends
   double* rad;               // [sample id][3] radiance

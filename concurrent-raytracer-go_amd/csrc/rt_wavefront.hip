@@ -1008,10 +1008,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
       uint64_t mask = 0;
       for (int k = 0, t = 0; k < 16; ++t) {
         const uint32_t ux = rt_rng_next(&rng), uy = rt_rng_next(&rng), uz = rt_rng_next(&rng);
-        if (!lst || t < 64) cnt<kCount>(c, C_RNG, 3);  // (a listed cone's later tries: wf_listtest)
+        if (!lst || t < p.list_tries) cnt<kCount>(c, C_RNG, 3);  // (a listed cone's later tries: wf_listtest)
         const bool acc = unit_ball_accept(ux, uy, uz);
         if (acc && keep && !lst) sq[at + k] = make_uint4(key, ux, uy, uz);
-        mask |= acc && t < 64 ? 1ull << (t & 63) : 0ull;
+        mask |= acc && t < p.list_tries ? 1ull << (t & 63) : 0ull;
         k += acc ? 1 : 0;
       }
       if (lst) {
@@ -1113,9 +1113,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
     // tries wf_softgen accepted: try t's draws are 3t..3t+2 (the jump table
     // gives the state before draw 3t), so no rejection loop runs here; the
     // queue carries 32 B per cone instead of the 16 points' 256 B.  (If the
-    // 16th point needs more than 64 tries, about once in 10^6 cones, the
-    // rest come from the sequential loop from try 64.)  Kept in registers
-    // for every candidate group.
+    // 16th point needs more than p.list_tries (64) tries, about once in 10^6
+    // cones, the rest come from the sequential loop from that try; the GPU
+    // tests force the limit low to exercise it.)  Kept in registers for
+    // every candidate group.
     const uint4* e = list_entry(p, dn, j);
     const uint4 e0 = e[0];
     const uint32_t key = e0.x;
@@ -1137,7 +1138,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
           uz[r] = rt_pcg_out(s2);
         } else {
           if (!tail) {
-            xt = state_at3(x0, p.jump, 64);
+            xt = state_at3(x0, p.jump, p.list_tries);
             tail = true;
           }
           rt_rng rng{xt};

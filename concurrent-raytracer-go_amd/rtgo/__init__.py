@@ -145,7 +145,7 @@ class Tuning(ctypes.Structure):
         ("measure", ctypes.c_int32),
         ("split_depth", ctypes.c_int32),
         ("partition", ctypes.c_int32),
-        ("_pad", ctypes.c_int32),
+        ("wf_list_tries", ctypes.c_int32),
     ]
 
 

@@ -330,7 +330,8 @@ typedef struct {
   int32_t split_depth;    /* measured schedules split a pixel with a path of more bounces than this; 0: 16 */
   int32_t partition;      /* rt_renderer with N > 1 ranks: RT_PARTITION_*; 0: auto (balanced for linear-scan
                              scenes, strided for BVH scenes, whose frames have thousands of busy tiles) */
-  int32_t _pad;
+  int32_t wf_list_tries;  /* wavefront list test: rejection tries a listed cone's accepted-try mask covers
+                             (1..64; 0: 64); later points continue the sequential loop (tests force it low) */
 } rt_tuning;
 #define RT_PARTITION_AUTO 0
 #define RT_PARTITION_STRIDED 1

@@ -209,3 +209,23 @@ def test_cone_routes_match_megakernel_and_oracle():
     assert soft["shadow_rays"] > 0, soft                     # traced (overflowing cones)
     assert soft["shadow_rays"] < c.shadow_rays, (soft, c.shadow_rays)  # not all: lists and empty cones
     assert soft["sphere_tests"] > 0 and soft["box_tests"] > 0
+
+
+@pytest.mark.parametrize("tries", [1, 8, 20])
+def test_listed_cones_past_their_try_mask(tries):
+    """wf_listtest rebuilds a listed cone's 16 points from its stream state
+    and the mask of accepted tries among its first wf_list_tries (64) tries,
+    and continues the sequential rejection loop past them when the 16th point
+    needs more (about once in 10^6 cones at 64).  Forced low here, so most
+    listed cones take that path: the image and the path counts (RNG draws
+    included) stay the oracle's."""
+    scene = rtgo.Scene.from_json_text(json.dumps(_curtain_scene()))
+    st = make_settings(rtgo, {"samples": 4, "max_depth": 6})
+    w, h = 60, 40
+    lb, rb, cb = _render(scene, w, h, st, mega=False, count=True)
+    lo, ro, co = _render(scene, w, h, st, mega=False, count=True, tuning=rtgo.default_tuning(wf_list_tries=tries))
+    assert lo.tobytes() == lb.tobytes() and ro.tobytes() == rb.tobytes()
+    assert {k: co[k] for k in PATH_KEYS} == {k: cb[k] for k in PATH_KEYS}
+    ref, ref_rgba, _ = oracle.render(scene, w, h, st)
+    assert lo.reshape(h, w, 3).tobytes() == ref.astype(np.float32).tobytes()
+    assert ro.reshape(h, w, 4).tobytes() == ref_rgba.tobytes()
