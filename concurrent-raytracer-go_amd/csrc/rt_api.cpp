@@ -891,7 +891,8 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
                       + (size_t)kWfShards * qcap * 4    // hard queues
                       + (size_t)kWfShards * qcap * 16 * 16  // soft queues
                       + (size_t)kWfShards * qcap * 4    // cone queues
-                      + cap * nlk * kWfConeK * 4        // cone candidate lists
+                      + cap * nlk * kWfConeWide * 4     // cone candidate lists
+                      + (size_t)kWfShards * qcap * 2 * 16  // wide-cone queues
                       + 64 * 256;                       // alignment
   if (need > c->wf_mem_bytes) {
     int rq = quiesce(c);
@@ -988,7 +989,9 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
     p.hardq = (uint32_t*)take((size_t)kWfShards * qcap * sizeof(uint32_t));
     p.softq = (uint32_t*)take((size_t)kWfShards * qcap * 16 * 4 * sizeof(uint32_t));
     p.coneq = (uint32_t*)take((size_t)kWfShards * qcap * sizeof(uint32_t));
-    p.cand = (int32_t*)take(cap * nlk * kWfConeK * sizeof(int32_t));
+    p.cand = (int32_t*)take(cap * nlk * kWfConeWide * sizeof(int32_t));
+    p.wide_cap = (int64_t)qcap * 2;
+    p.wideq = (uint32_t*)take((size_t)kWfShards * qcap * 2 * 4 * sizeof(uint32_t));
     if ((size_t)(m - (char*)c->wf_mem) > c->wf_mem_bytes) {
       set_error("wavefront buffer layout overflow");
       return RT_E_NOMEM;

@@ -235,6 +235,13 @@ constexpr uint32_t kDeadSid = 0xFFFFFFFFu;  // a slot with no sample (out-of-ima
 // knob (C4: 16 -> 412.6 ms per frame, 24 -> 416.0, 32 -> 421.1; with the
 // list tests ordered by length: 16 -> 403.4, 32 -> 405.7)
 constexpr int kWfConeK = 16;
+// (r05) a cone with kWfConeK < candidates <= kWfConeWide is "wide": its 16 rays
+// are tested against its list, one ray per lane (wf_widetest), instead of
+// being traced; the candidate lists hold kWfConeWide entries per (path, light)
+#ifndef RT_CONE_WIDE
+#define RT_CONE_WIDE 32
+#endif
+constexpr int kWfConeWide = RT_CONE_WIDE;
 struct WfCtl {                 // device-resident loop state; counters of shard s at [32 s] (own 128-B line)
   int32_t cur_cnt[kWfShards * 32];   // live paths per shard of the current array
   int32_t next_cnt[kWfShards * 32];  // survivors appended per shard of the next array
@@ -242,6 +249,7 @@ struct WfCtl {                 // device-resident loop state; counters of shard 
   int32_t soft_cnt[kWfShards * 32];  // soft shadow rays queued per shard
   int32_t cone_cnt[kWfShards * 32];  // shadow cones queued per shard
   int32_t list_cnt[kWfShards * 32];  // entries of listed cones per shard (two each, from the far end of the soft queue)
+  int32_t wide_cnt[kWfShards * 32];  // entries of wide cones per shard (two each, in the wide queue)
   int32_t job_head[4][kWfShards * 32];  // persistent kernels (extend, hard, soft, cone): jobs taken per range
   unsigned long long next_sample;    // first sample id of the chunk not started yet
   unsigned long long total;          // sample ids in the chunk
@@ -290,7 +298,9 @@ struct WfParams {
   const uint64_t* jump;      // PCG jump table (KParams::jump)
   int32_t list_tries;        // tries a listed cone's accepted-try mask covers (1..64, rt_tuning.wf_list_tries)
   uint32_t* coneq;           // kWfShards queues of hard_cap entries: slot * nl + light (clear hard ray)
-  int32_t* cand;             // [slot * nl + light][kWfConeK]: the shadow cone's candidate spheres, -1 ends
+  int32_t* cand;             // [slot * nl + light][kWfConeWide]: the shadow cone's candidate spheres, -1 ends
+  uint32_t* wideq;           // kWfShards queues of wide_cap 4-word entries: two per wide cone (as the listed cones')
+  int64_t wide_cap;
   double* rad;               // [sample id][3] radiance
   unsigned long long* counts;
   float* out_linear;

@@ -79,6 +79,10 @@ constexpr uint32_t kHardBit = 1u << 16;   // the hard shadow ray is blocked
 constexpr uint32_t kUnlitBit = 1u << 17;  // the hit point is within 0.001 of the light (no shadow rays)
 constexpr uint32_t kListBit = 1u << 18;   // the light's shadow cone left a candidate list (wf_cone)
 constexpr uint32_t kEmptyBit = 1u << 19;  // ... an empty one: no soft ray can be blocked
+#ifndef RT_WIDE_EXIT
+#define RT_WIDE_EXIT 1
+#endif
+constexpr uint32_t kWideBit = 1u << 20;   // ... a wide one (kWfConeK < candidates <= kWfConeWide, wf_widetest)
 // hidx of a path whose ray hit nothing while a sky is opted in: wf_shade1
 // ends it with the sky's radiance (GetSkyColor, atmosphere.go:100-135) --
 // kept out of the traversal kernel, whose registers it would cost
@@ -807,8 +811,9 @@ __device__ __forceinline__ void cone_descend(glb_node* __restrict__ qb, lds_node
 // 0.001 of the hit point) and whose hard ray is clear; `listed`: those of
 // them whose cone left a candidate list
 __device__ __forceinline__ uint32_t clear_lights(const WfParams& p, size_t slot, bool hit, int base,
-                                                 uint32_t* listed = nullptr, uint32_t* empty = nullptr) {
-  uint32_t own = 0, lst = 0, emp = 0;
+                                                 uint32_t* listed = nullptr, uint32_t* empty = nullptr,
+                                                 uint32_t* wide = nullptr) {
+  uint32_t own = 0, lst = 0, emp = 0, wid = 0;
   if (hit) {
     const int end = min(p.nl, base + 32);
     for (int li = base; li < end; ++li) {
@@ -816,10 +821,12 @@ __device__ __forceinline__ uint32_t clear_lights(const WfParams& p, size_t slot,
       if (!(ls & (kHardBit | kUnlitBit))) own |= 1u << (li - base);
       if (ls & kListBit) lst |= 1u << (li - base);
       if (ls & kEmptyBit) emp |= 1u << (li - base);
+      if (ls & kWideBit) wid |= 1u << (li - base);
     }
   }
   if (listed) *listed = lst;
   if (empty) *empty = emp;
+  if (wide) *wide = wid;
   return own;
 }
 
@@ -893,7 +900,7 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
         k = cone_q(p, P, u, ldist, ok);
         // (a cone whose bounds cannot be evaluated is not walked: "too many
         // candidates", so its rays are traced)
-        found = ok ? 0 : kWfConeK + 1;
+        found = ok ? 0 : kWfConeWide + 1;
         cur = ok ? bvh_code(p.g.bvh[0]) : -1;
         sp = 0;
         busy = true;
@@ -909,25 +916,28 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
         const int first = cur >> 3, count = cur & 7;
         DSphere ls[kLeafBatch];
         load_leaf(p.g.spheres, first, count, ls);
-        int32_t* cl = p.cand + (size_t)key * kWfConeK;
+        int32_t* cl = p.cand + (size_t)key * kWfConeWide;
         for (int i = first; i < first + count; ++i) {
           const DSphere& S = leaf_sphere(p.g.spheres, ls, first, i);
           if (S.obj == excl && S.r > 0) continue;
           cnt<kCount>(c, C_SPH);
           if (cone_keeps(S, P, u, ldist)) {
-            if (found < kWfConeK) cl[found] = i;
+            if (found < kWfConeWide) cl[found] = i;
             ++found;
           }
         }
-        cur = found > kWfConeK || sp == 0 ? -1 : stack[--sp * 64];
+        cur = found > kWfConeWide || sp == 0 ? -1 : stack[--sp * 64];
       }
       if (cur == -1) {  // walked (or too many candidates: the rays are traced)
         busy = false;
         if (found == 0) {
           p.lstate[key] = kListBit | kEmptyBit;
         } else if (found <= kWfConeK) {
-          if (found < kWfConeK) p.cand[(size_t)key * kWfConeK + found] = -1;
+          if (found < kWfConeK) p.cand[(size_t)key * kWfConeWide + found] = -1;
           p.lstate[key] = kListBit;
+        } else if (found <= kWfConeWide) {
+          if (found < kWfConeWide) p.cand[(size_t)key * kWfConeWide + found] = -1;
+          p.lstate[key] = kWideBit;
         }
       }
     }
@@ -960,7 +970,7 @@ template <bool kCount>
 __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
   __shared__ int s_wave[kWfBlock / 64];
   __shared__ int s_base;
-  __shared__ uint32_t s_slot[kWfBlock], s_own[kWfBlock], s_list[kWfBlock], s_empty[kWfBlock];
+  __shared__ uint32_t s_slot[kWfBlock], s_own[kWfBlock], s_list[kWfBlock], s_empty[kWfBlock], s_wide[kWfBlock];
   const Dense dn = dense(p.ctl->cur_cnt);
   const int n = dn.start[kWfShards];
   if ((int)(blockIdx.x * kWfBlock) >= n) return;
@@ -981,7 +991,8 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
   // (spec v4: (sample, depth, light), include/rt_rng.h); an empty cone's rays
   // cannot be blocked and need none, so nothing is drawn for it (the
   // counting variant walks its tries for the reference's draw count).
-  auto gen = [&](size_t sl, uint32_t own, uint32_t listed, uint32_t empty, int base, int q, int ql) {
+  auto gen = [&](size_t sl, uint32_t own, uint32_t listed, uint32_t empty, uint32_t wide, int base, int q, int ql,
+                 int qw) {
     uint4* sq = reinterpret_cast<uint4*>(p.softq) + (size_t)shard * p.soft_cap;
     const uint64_t skey = sid_soft_key(p, p.cur.sid[sl]);
     const uint32_t depth = (uint32_t)p.cur.depth[sl];
@@ -997,9 +1008,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
       // the points from them through the jump table.  (Both kinds run the one
       // rejection loop below: separate loops for listed and traced cones
       // diverged, 20.5 -> 25.2 ms per C4 frame.)
-      const bool lst = keep && (listed & bit);
+      // (a wide cone's two entries, the same, go to the wide queue: wf_widetest)
+      const bool lst = keep && (listed & bit), wid = keep && (wide & bit), two = lst || wid;
       size_t at = 0;  // (an index, not a bumped pointer)
-      if (keep && !lst) {
+      if (keep && !two) {
         at = (size_t)q;
         q += 16;
       }
@@ -1008,17 +1020,21 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
       uint64_t mask = 0;
       for (int k = 0, t = 0; k < 16; ++t) {
         const uint32_t ux = rt_rng_next(&rng), uy = rt_rng_next(&rng), uz = rt_rng_next(&rng);
-        if (!lst || t < p.list_tries) cnt<kCount>(c, C_RNG, 3);  // (a listed cone's later tries: wf_listtest)
+        if (!two || t < p.list_tries) cnt<kCount>(c, C_RNG, 3);  // (a listed cone's later tries: wf_listtest)
         const bool acc = unit_ball_accept(ux, uy, uz);
-        if (acc && keep && !lst) sq[at + k] = make_uint4(key, ux, uy, uz);
+        if (acc && keep && !two) sq[at + k] = make_uint4(key, ux, uy, uz);
         mask |= acc && t < p.list_tries ? 1ull << (t & 63) : 0ull;
         k += acc ? 1 : 0;
       }
-      if (lst) {
-        uint4* le = sq + (p.soft_cap - ql - 2);
+      if (two) {
+        uint4* le = lst ? sq + (p.soft_cap - ql - 2)
+                        : reinterpret_cast<uint4*>(p.wideq) + (size_t)shard * p.wide_cap + qw;
         le[0] = make_uint4(key, (uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)mask);
         le[1] = make_uint4((uint32_t)(mask >> 32), 0u, 0u, 0u);
-        ql += 2;
+        if (lst)
+          ql += 2;
+        else
+          qw += 2;
       }
     }
   };
@@ -1027,8 +1043,8 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
     // paths that have one are gathered to the workgroup's first lanes, so
     // the rejection sampling runs on full waves and the other waves of the
     // workgroup skip it (one path per lane either way: same draws, same order)
-    uint32_t listed, empty;
-    const uint32_t own = clear_lights(p, slot, hit, 0, &listed, &empty);
+    uint32_t listed, empty, wide;
+    const uint32_t own = clear_lights(p, slot, hit, 0, &listed, &empty, &wide);
     int total;
     const int at = block_prefix(own != 0 ? 1 : 0, s_wave, total);
     if (own) {
@@ -1036,24 +1052,28 @@ __global__ __launch_bounds__(kWfBlock) void wf_softgen(const WfParams p) {
       s_own[at] = own;
       s_list[at] = listed;
       s_empty[at] = empty;
+      s_wide[at] = wide;
     }
     __syncthreads();
     const bool work = (int)threadIdx.x < total;
     const uint32_t ws = work ? s_slot[threadIdx.x] : 0u, wo = work ? s_own[threadIdx.x] : 0u;
     const uint32_t wl = work ? s_list[threadIdx.x] : 0u, we = work ? s_empty[threadIdx.x] : 0u;
-    const int q = block_append(16 * __popc(wo & ~wl), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
+    const uint32_t ww = work ? s_wide[threadIdx.x] : 0u;
+    const int q = block_append(16 * __popc(wo & ~wl & ~ww), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
     const int ql = block_append(2 * __popc(wl & ~we), &p.ctl->list_cnt[shard * 32], s_wave, &s_base);
-    if (work) gen(ws, wo, wl, we, 0, q, ql);
+    const int qw = block_append(2 * __popc(ww), &p.ctl->wide_cnt[shard * 32], s_wave, &s_base);
+    if (work) gen(ws, wo, wl, we, ww, 0, q, ql, qw);
     flush_counts<kCount>(p, c);
     return;
   }
   // more than 32 lights: in chunks of 32 (one bit each), in light order
   for (int base = 0; base < p.nl; base += 32) {
-    uint32_t listed, empty;
-    const uint32_t own = clear_lights(p, slot, hit, base, &listed, &empty);
-    const int q = block_append(16 * __popc(own & ~listed), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
+    uint32_t listed, empty, wide;
+    const uint32_t own = clear_lights(p, slot, hit, base, &listed, &empty, &wide);
+    const int q = block_append(16 * __popc(own & ~listed & ~wide), &p.ctl->soft_cnt[shard * 32], s_wave, &s_base);
     const int ql = block_append(2 * __popc(listed & ~empty), &p.ctl->list_cnt[shard * 32], s_wave, &s_base);
-    if (own) gen(slot, own, listed, empty, base, q, ql);
+    const int qw = block_append(2 * __popc(wide), &p.ctl->wide_cnt[shard * 32], s_wave, &s_base);
+    if (own) gen(slot, own, listed, empty, wide, base, q, ql, qw);
   }
   flush_counts<kCount>(p, c);
 }
@@ -1095,7 +1115,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
       const uint32_t key = list_entry(p, dn, j)->x;
       // groups of four up to the one holding the list's end (-1; entries
       // past it are stale): bucket 1, 2, 3-4, 5+ groups
-      const int4* cl = reinterpret_cast<const int4*>(p.cand + (size_t)key * kWfConeK);
+      const int4* cl = reinterpret_cast<const int4*>(p.cand + (size_t)key * kWfConeWide);
       int g = 1;
       while (g < kWfConeK / 4 && (cl[g - 1].x | cl[g - 1].y | cl[g - 1].z | cl[g - 1].w) >= 0) ++g;
       b = g == 1 ? 0 : (g == 2 ? 1 : (g <= 4 ? 2 : 3));
@@ -1161,7 +1181,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
     d3 ldir;
     double tmax;
     light_vec(p.lights[li], o, ldir, tmax);
-    const int32_t* cl = p.cand + (size_t)key * kWfConeK;
+    const int32_t* cl = p.cand + (size_t)key * kWfConeWide;
     uint32_t blocked = 0;  // one bit per ray
     for (int g = 0; g < kWfConeK; g += 4) {
       const int4 q4 = *reinterpret_cast<const int4*>(cl + g);
@@ -1194,6 +1214,100 @@ __global__ __launch_bounds__(kWfBlock) void wf_listtest(const WfParams p) {
       if (!valid[3]) break;
     }
     p.lstate[key] = (uint32_t)__popc(blocked);
+  }
+  flush_counts<kCount>(p, c, kGroupSoft);
+}
+
+// ---------------------------------------------------------------- widetest
+// (r05) The 16 soft rays of a wide cone (kWfConeK < candidates <=
+// kWfConeWide) against its list, one ray per lane: 16 lanes per cone, four
+// cones per wave, each lane looping over the cone's candidates (the same
+// sphere for the 16 lanes: one broadcast load) with the traversal's ray,
+// range and Sphere.Hit test, so the blocked count is the traversal's.  Such
+// a cone's rays were traced through the BVH before (wf_occlude<soft>, in
+// the densest parts of the scene).  Lane r rebuilds point r from the cone's
+// stream state and accepted-try mask (wf_softgen), as wf_listtest does; a
+// point past the mask continues the sequential loop.  Persistent: the grid
+// loops over the cones.
+template <bool kCount>
+__global__ __launch_bounds__(kWfBlock) void wf_widetest(const WfParams p) {
+  const Dense dn = dense(p.ctl->wide_cnt);  // (two entries per cone, in one shard)
+  const int n = dn.start[kWfShards] / 2;
+  if ((int)(blockIdx.x * (kWfBlock / 16)) >= n) return;
+  Counters c;
+  if constexpr (kCount)
+    for (int k = 0; k < 9; ++k) c.v[k] = 0;
+  const int lane = (int)(threadIdx.x & 63), r = lane & 15;
+  const int groups = (int)gridDim.x * (kWfBlock / 16);
+  for (int j = (int)(blockIdx.x * (kWfBlock / 16) + threadIdx.x / 16); j < n; j += groups) {
+    const size_t at = dense_at(dn, 2 * j, p.wide_cap);
+    const uint4* e = reinterpret_cast<const uint4*>(p.wideq) + at;
+    const uint4 e0 = e[0];
+    const uint32_t key = e0.x;
+    const uint64_t x0 = (uint64_t)e0.y | (uint64_t)e0.z << 32;
+    const uint64_t mask = (uint64_t)e0.w | (uint64_t)e[1].x << 32;
+    uint32_t ux = 0, uy = 0, uz = 0;
+    const int na = __popcll(mask);
+    if (r < na) {  // the r-th accepted try among the mask's
+      uint64_t m = mask;
+      for (int i = 0; i < r; ++i) m &= m - 1;
+      const uint64_t s0 = state_at3(x0, p.jump, __builtin_ctzll(m)), s1 = s0 * RT_PCG_MULT + RT_PCG_INC,
+                     s2 = s1 * RT_PCG_MULT + RT_PCG_INC;
+      ux = rt_pcg_out(s0);
+      uy = rt_pcg_out(s1);
+      uz = rt_pcg_out(s2);
+    } else {  // past the mask: the sequential loop from try p.list_tries (lane 15 counts its draws)
+      rt_rng rng{state_at3(x0, p.jump, p.list_tries)};
+      for (int k = na;;) {
+        const uint32_t a = rt_rng_next(&rng), b = rt_rng_next(&rng), z = rt_rng_next(&rng);
+        if (r == 15) cnt<kCount>(c, C_RNG, 3);
+        if (unit_ball_accept(a, b, z)) {
+          if (k == r) {
+            ux = a;
+            uy = b;
+            uz = z;
+            break;
+          }
+          ++k;
+        }
+      }
+    }
+    const uint32_t slot = key / (uint32_t)p.nl, li = key - slot * (uint32_t)p.nl;
+    const d3 o = ld_P(p, (int)slot);
+    d3 ldir;
+    double tmax;
+    light_vec(p.lights[li], o, ldir, tmax);
+    const d3 pt = mk(rt_bits_to_unit(ux) * 2 - 1, rt_bits_to_unit(uy) * 2 - 1, rt_bits_to_unit(uz) * 2 - 1);
+    const d3 d = normalize(ldir + muls(pt, 0.1));
+    const double av = len2(d), inv_a = approx_rcp(av);
+    const int32_t* cl = p.cand + (size_t)key * kWfConeWide;
+    bool blocked = false;
+    // candidates four at a time: their ids and spheres loaded together (the
+    // same for the cone's 16 lanes), then tested in list order
+    for (int g = 0; g < kWfConeWide; g += 4) {
+      const int4 q4 = *reinterpret_cast<const int4*>(cl + g);
+      const int id[4] = {q4.x, q4.y, q4.z, q4.w};
+      bool valid[4];
+      DSphere ls[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        valid[k] = id[k] >= 0 && (k == 0 || valid[k - 1]);
+        ls[k] = p.g.spheres[valid[k] ? id[k] : 0];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (valid[k] && !blocked) {
+          cnt<kCount>(c, C_SPH);
+          double num;
+          blocked = sphere_query(ls[k], o, d, av, inv_a, 0.001, tmax, num) != 0;
+        }
+      if (!valid[3]) break;
+#if RT_WIDE_EXIT
+      if (((__ballot(blocked) >> (lane & 48)) & 0xFFFFull) == 0xFFFFull) break;  // all 16 blocked
+#endif
+    }
+    const unsigned long long bm = __ballot(blocked);
+    if (r == 0) p.lstate[key] = (uint32_t)__popcll((bm >> (lane & 48)) & 0xFFFFull);
   }
   flush_counts<kCount>(p, c, kGroupSoft);
 }
@@ -1371,6 +1485,7 @@ __global__ void wf_book(const WfParams p) {
     ctl->soft_cnt[s * 32] = 0;
     ctl->cone_cnt[s * 32] = 0;
     ctl->list_cnt[s * 32] = 0;
+    ctl->wide_cnt[s * 32] = 0;
     ctl->job_head[3][s * 32] = 0;
     ctl->job_head[0][s * 32] = 0;
     ctl->job_head[1][s * 32] = 0;
@@ -1525,6 +1640,9 @@ static int enqueue_bounce(const WfParams& p, hipStream_t st, const hipEvent_t* e
   if (p.nl > 0 && p.soft) {  // (at most one listed cone per path and light)
     const long long cones = live * p.nl;
     hipLaunchKernelGGL((wf_listtest<kCount>), dim3((unsigned)((cones + kWfBlock - 1) / kWfBlock)), b, 0, st, p);
+    // wide cones: a persistent grid (16 lanes per cone; far fewer cones)
+    const long long wblocks = std::min<long long>((cones + kWfBlock / 16 - 1) / (kWfBlock / 16), 4096);
+    hipLaunchKernelGGL((wf_widetest<kCount>), dim3((unsigned)wblocks), b, 0, st, p);
   }
   mark(ev, kWfSoft, st);
   if (p.nl > 0 && p.soft) trav(2);
