@@ -64,6 +64,12 @@ constexpr int kSqTail = RT_SQ_TAIL;
 #define RT_SQ_TRIES 2
 #endif
 constexpr int kSqTries = RT_SQ_TRIES;
+#ifndef RT_EXP_NO_SOLO  // (measurement switches: lone-path and cone-helper forms off; exact either way)
+#define RT_EXP_NO_SOLO 0
+#endif
+#ifndef RT_EXP_NO_CONE_WIDE
+#define RT_EXP_NO_CONE_WIDE 0
+#endif
 
 namespace rtgo {
 
@@ -1413,7 +1419,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
             fresh()->dbg[(size_t)blockIdx.x * kDbgStride + 16 + dbg_iter / 4] = __builtin_amdgcn_s_memrealtime();
           ts0 = __builtin_amdgcn_s_memtime();
 #endif
-          if constexpr (kStage && !kCount && !kPilot) {
+          if constexpr (kStage && !kCount && !kPilot && !RT_EXP_NO_SOLO) {
             // one path left (no free lane found an entry to start): the whole
             // wave runs it to its end (solo_path)
             const unsigned long long am = __ballot(alive);
@@ -1548,7 +1554,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
           const bool hard = shade && lit && (kCount || !dark);
           bool wide_c = false;
           if constexpr (kStage) {  // few lit hit points: the cone tests with helpers
-            if (masks && gg.nt == 0) {
+            if (masks && gg.nt == 0 && !RT_EXP_NO_CONE_WIDE) {
               const unsigned long long cq = __ballot(hard);
               const int ncq = __popcll(cq);
               if (ncq > 0 && ncq <= 16) {
