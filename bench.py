@@ -762,16 +762,21 @@ def main():
     # frame's longest paths, so it needs more frames per launch
     # (scripts/rank_share_probe.py).  BVH frames: one at a time.
     # At one GPU the timed steps fill the F slots: ceil(K / F) frames per
-    # launch up to RT_MAX_FRAMES (K = 20: two launches of 10 side by side;
-    # K = 100: four of 25, two at a time -- 25-frame launches measured 2 %
-    # faster than 16-frame ones at K = 100, and K = 20 the same either way,
-    # DESIGN.md §6).
+    # launch up to RT_MAX_FRAMES (K = 20: one launch of 20, below; K = 100:
+    # four of 25, two at a time -- 25-frame launches measured 2 % faster than
+    # 16-frame ones at K = 100).
     if cfg in WAVEFRONT:
         F, B = 1, 1
     elif world > 1:
         F, B = 3, 16
     else:
-        F = fif_default
+        # (r05) K steps that fit one launch run as one launch (one tail for
+        # all of them): the driver's 20 frames as one launch of 20 measured
+        # 228.1 k Mrays/s against 222.5 k as 10 + 10 side by side and 218.8 k
+        # as 7 + 7 + 6 (scripts/k20_probe.sh, three runs each); more steps
+        # run F = 2 launches in flight, so that each tail overlaps the next
+        # launch's start
+        F = 1 if steps <= rtgo.RT_MAX_FRAMES else fif_default
         B = -(-steps // (args.frames_in_flight or F))
     F = args.frames_in_flight or F
     B = max(1, min(rtgo.RT_MAX_FRAMES, args.frames_per_launch or B))

@@ -15,10 +15,10 @@ l=[x for x in open('gpurun_out/k20_tmp.log') if x.startswith('{')][-1]
 d=json.loads(l); print(json.dumps({'tag':'$tag','value':d['value'],'ms_per_step':d['ms_per_step'],'launch_frames':d.get('launch_frames')}))" >> $O
   tail -1 $O
 }
-for i in 1 2; do
+for i in 1 2 3; do
   run driver --steps 20 --warmup 5 || exit $?
   run k100 --steps 100 --warmup 5 || exit $?
+  run k20_f3 --steps 20 --warmup 5 --frames-in-flight 3 || exit $?
+  run k100_f3 --steps 100 --warmup 5 --frames-in-flight 3 || exit $?
   run k20_f1x20 --steps 20 --warmup 5 --frames-in-flight 1 --frames-per-launch 20 || exit $?
-  run k20_f4x5 --steps 20 --warmup 5 --frames-in-flight 4 --frames-per-launch 5 || exit $?
-  run k20_f3x7 --steps 20 --warmup 5 --frames-in-flight 3 --frames-per-launch 7 || exit $?
 done
