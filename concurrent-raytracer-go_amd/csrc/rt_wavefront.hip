@@ -13,10 +13,15 @@
 //   shade1    the HitRecord (sphere.go:42-58); one hard shadow ray per lit
 //             light (calculateSmartShadow, renderer.go:299-305) queued
 //   occlude   any-hit of the hard rays
-//   softgen   per light whose hard ray is clear, in light order, the 16
-//             RandomVec3InUnitSphere points (renderer.go:311-318) queued as
-//             16 consecutive soft rays
-//   occlude   any-hit of the soft rays, blocked ones counted per (path, light)
+//   cone      per light whose hard ray is clear, the shadow cone's candidate
+//             spheres (a list of <= 16, a wide list of <= 32, or too many)
+//   softgen   the 16 RandomVec3InUnitSphere points (renderer.go:311-318) of
+//             each clear light from its own stream (RNG spec v4): 16 queued
+//             soft rays, or for a (wide) listed cone its stream state and
+//             accepted tries; none for an empty cone
+//   listtest  a listed cone's 16 rays against its list, one cone per thread
+//   widetest  a wide cone's 16 rays against its list, one ray per lane
+//   occlude   any-hit of the other soft rays, blocked ones counted per (path, light)
 //   shade     calculateDirectLighting (renderer.go:229-297) with those counts,
 //             Material.Scatter, the traceRay combination; survivors appended
 //             to the next path array, finished paths write their radiance
@@ -31,8 +36,9 @@
 // kWfShards): one atomic per workgroup and queue, spread over 8 words.
 //
 // The arithmetic is the megakernel's (rt_device.h).  Each path consumes its
-// RNG stream in the reference's order (hard rays draw nothing; soft-shadow
-// draws light by light, then the scatter draws), and each sample's radiance
+// RNG streams as the spec says (include/rt_rng.h: the sample's stream for
+// the camera and scatter draws, one stream per (sample, bounce, light) for
+// the soft-shadow points; hard rays draw nothing), and each sample's radiance
 // lands in its own slot of a per-frame buffer; resolve sums every pixel's
 // samples in sample order (tracePixel) — so images are bit-identical to the
 // megakernel's and the oracle's (tests/test_gpu_wavefront.py).  The loop is
