@@ -73,6 +73,15 @@ constexpr int kSqTries = RT_SQ_TRIES;
 
 namespace rtgo {
 
+// The lane id through a volatile move: an LDS address derived from it is
+// computed where it is used instead of being kept live through the bounce
+// loop (live across the lone-path call, such values are spilled to scratch
+// once per wave: the one-frame launch's bulk HBM writes)
+__device__ __forceinline__ int lane_now() {  // (one-wave workgroups: the lane is threadIdx.x)
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 // Set bits of a wave mask below the calling lane (v_mbcnt): no 64-bit
 // per-lane "below" mask has to stay live (it was spilled to scratch)
 __device__ __forceinline__ int lanes_below(unsigned long long m) {
@@ -373,7 +382,7 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
   constexpr unsigned kRing = kRingNeed <= 256 ? 256u : (unsigned)kRingNeed;
   __shared__ uint4 sq[kRing];
   __shared__ int sq_unocc[64];  // per owner: unoccluded rays
-  const int lane = (int)(threadIdx.x & 63);
+  const int lane = lane_now() & 63;
   sq_unocc[lane] = 0;
   int need = need_soft ? 16 : 0, free_rays = 0;  // free_rays: points of an owner with nothing to trace
   int head = 0, tail = 0;  // wave-uniform ring positions
@@ -1391,7 +1400,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
           Counters nc;  // phase 1 counted this camera ray and its draws
           const int px = loc.tx * 32 + (tp & 31), py = loc.ty * 32 + (tp >> 5);
           camera_ray<false>(k, px, py, s, rng, o, d, nc);
-          skey[lane] = rt_soft_key(k->frame_key[frame_of(k)], (uint32_t)py * (uint32_t)k->W + (uint32_t)px, (uint32_t)s);
+          skey[lane_now()] = rt_soft_key(k->frame_key[frame_of(k)], (uint32_t)py * (uint32_t)k->W + (uint32_t)px, (uint32_t)s);
           entry = e;
           T = mk(1, 1, 1);
           set_path_L(mk(0, 0, 0));
@@ -1596,7 +1605,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
           if (free_soft) {
             unocc = 16;
             if constexpr (kCount) {
-              rt_rng fr{rt_soft_state(skey[lane], (uint32_t)depth, (uint32_t)li)};
+              rt_rng fr{rt_soft_state(skey[lane_now()], (uint32_t)depth, (uint32_t)li)};
               unsigned long long tries = 0;
               for (int got = 0; got < 16; ++tries) {
                 const uint32_t ux = rt_rng_next(&fr), uy = rt_rng_next(&fr), uz = rt_rng_next(&fr);
@@ -1609,7 +1618,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
             }
           }
           const bool traced_soft = need_soft && trace;
-          rt_rng srng{traced_soft ? rt_soft_state(skey[lane], (uint32_t)depth, (uint32_t)li) : 0ull};
+          rt_rng srng{traced_soft ? rt_soft_state(skey[lane_now()], (uint32_t)depth, (uint32_t)li) : 0ull};
           // soft shadows: wave-converged decision between the two forms
           const unsigned long long owners = __ballot(traced_soft);
 #ifdef RT_WG_TIMING
