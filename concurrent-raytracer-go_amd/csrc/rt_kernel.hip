@@ -64,8 +64,15 @@ constexpr int kSqTail = RT_SQ_TAIL;
 #define RT_SQ_TRIES 2
 #endif
 constexpr int kSqTries = RT_SQ_TRIES;
-#ifndef RT_EXP_NO_SOLO  // (measurement switches: lone-path and cone-helper forms off; exact either way)
-#define RT_EXP_NO_SOLO 0
+// The lone-path form (solo_path): off by default since r05.
+// Under RNG spec v4 a lone bounce is cheap, and the form no longer shortens
+// anything (K = 20 frames 229.7 k vs 231.7 k Mrays/s without it, six rounds;
+// one frame 0.574 vs 0.571 ms), while its call frames left ~47 MB of dirty
+// scratch per one-frame launch (74.7 vs 18.6 MB of HBM traffic).  The
+// cross-lane checking build compiles it in (Makefile xlane), so it stays
+// tested; RT_SOLO=1 restores it.  (measurement switch: cone helpers off)
+#ifndef RT_SOLO
+#define RT_SOLO 0
 #endif
 #ifndef RT_EXP_NO_CONE_WIDE
 #define RT_EXP_NO_CONE_WIDE 0
@@ -1428,7 +1435,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
             fresh()->dbg[(size_t)blockIdx.x * kDbgStride + 16 + dbg_iter / 4] = __builtin_amdgcn_s_memrealtime();
           ts0 = __builtin_amdgcn_s_memtime();
 #endif
-          if constexpr (kStage && !kCount && !kPilot && !RT_EXP_NO_SOLO) {
+          if constexpr (kStage && !kCount && !kPilot && RT_SOLO) {
             // one path left (no free lane found an entry to start): the whole
             // wave runs it to its end (solo_path)
             const unsigned long long am = __ballot(alive);

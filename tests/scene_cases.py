@@ -230,7 +230,7 @@ def _cube_scenes():
                    {"position": [-3, 2, -5], "color": [0.8, 0.8, 1], "intensity": 40}],
     }
     # the camera inside a hollow mirror sphere around a glass cube and a light:
-    # 50-bounce paths, so the lone-path form (solo_path) runs them
+    # 50-bounce paths (the lone-path form, solo_path, runs them when built in)
     out["mirror_probe_glass_cube"] = {
         "camera": {"position": [0, 0, 3.2], "aspectRatio": 1.5},
         "objects": [sph((0, 0, 0), 5.0, mirror), cube((0, -0.2, 0), (1.6, 1.6, 1.6), glass),

@@ -9,7 +9,8 @@ that leaves an inner face toward an outside light must still cross the box
 (calculateSmartShadow, renderer.go:299-331).  These scenes reach that case
 through glass and dielectric cubes, a camera inside a cube, lights inside
 and outside cubes and mirrored (negative-size) cubes, on the megakernel's
-main loop, its lone-path form (a 50-bounce mirror probe) and a 70-sphere
+main loop, a 50-bounce mirror probe (the lone-path form's case, held to
+the product in tests/test_gpu_xlane.py) and a 70-sphere
 scene without cone masks.  Bar: bit-identical float32 radiance and RGBA8 at
 seeds 1 and 2, and identical integer path counts (shadow rays included).
 """
