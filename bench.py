@@ -114,9 +114,9 @@ KERNELS = {  # the dominant kernel of each config (rocprofv3 --stats, profiles/)
     "c3": "rtgo::render_kernel<false, true, false, false>",
     # the soft-shadow stage: cone walks, list tests, traced soft rays
     "c4": "rtgo::wf_cone<false, true> + rtgo::wf_listtest<false> + rtgo::wf_widetest<false> + "
-          "rtgo::wf_occlude<false, true, true>",
+          "rtgo::wf_occlude4<false, true>",
     "c5": "rtgo::wf_cone<false, true> + rtgo::wf_listtest<false> + rtgo::wf_widetest<false> + "
-          "rtgo::wf_occlude<false, true, true>",
+          "rtgo::wf_occlude4<false, true>",
 }
 SOFT_STAGE = ("cone", "cone_rays", "occlude_soft")  # its kernel classes (rtgo.WF_KERNELS)
 

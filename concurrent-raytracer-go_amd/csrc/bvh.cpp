@@ -79,6 +79,9 @@ void build_sphere_bvh(FlatScene* fs, int bins, int leaf) {
   const int kLeafMax = leaf > 0 ? std::min(7, leaf) : kDefaultLeaf;
   fs->bvh.clear();
   fs->qbvh.clear();
+  fs->qbvh4.clear();
+  fs->bvh4_stack = 0;
+  fs->bvh4_root = 0;
   const int n = (int)fs->spheres.size();
   if (n == 0) return;
   std::vector<Box> pb(n);
@@ -268,6 +271,69 @@ void build_sphere_bvh(FlatScene* fs, int bins, int leaf) {
       q.w[1] = ql[1] | (qh[1] << 16);
       q.w[2] = ql[2] | (qh[2] << 16);
       q.w[3] = (uint32_t)((nd.left_or_first << 3) | nd.count);
+    }
+  }
+  // 4-wide form for the closest-hit and occlusion traversals (rt_wavefront.hip
+  // descend4): every group holds 2..4 nodes of the binary tree that cover one
+  // internal node's subtree (its children, then the largest internal one
+  // among them replaced by its own children), with the quantized boxes and
+  // codes of qbvh.  Groups are stored back to back, breadth-first, without
+  // empty slots; an internal slot's code is (its group's first slot << 5) |
+  // (its size - 1) << 3, so the low 3 bits stay 0 as in qbvh; 3 padding slots
+  // at the end keep a group's 4-slot load inside the array.  Same leaves,
+  // same boxes: the spheres a ray tests are the binary traversal's.
+  {
+    auto area = [&](int i) {
+      const DBVHNode& b = nodes[i];
+      const double x = (double)b.hi[0] - b.lo[0], y = (double)b.hi[1] - b.lo[1], z = (double)b.hi[2] - b.lo[2];
+      return x * y + y * z + z * x;
+    };
+    fs->qbvh4.clear();
+    fs->bvh4_stack = 0;
+    fs->bvh4_root = 0;
+    if (nodes[0].count == 0) {
+      std::vector<int> bin = {0}, pend = {0};
+      std::vector<std::vector<int>> kids;
+      std::vector<std::vector<int>> sub;  // per kid: its group, or -1 (a leaf)
+      for (size_t g = 0; g < bin.size(); ++g) {
+        std::vector<int> k = {nodes[bin[g]].left_or_first, nodes[bin[g]].left_or_first + 1};
+        while (k.size() < 4) {
+          int best = -1;
+          for (int i = 0; i < (int)k.size(); ++i)
+            if (nodes[k[i]].count == 0 && (best < 0 || area(k[i]) > area(k[best]))) best = i;
+          if (best < 0) break;
+          const int b = k[best];
+          k[best] = nodes[b].left_or_first;
+          k.insert(k.begin() + best + 1, nodes[b].left_or_first + 1);
+        }
+        const int pd = pend[g] + (int)k.size() - 1;
+        fs->bvh4_stack = std::max(fs->bvh4_stack, pd);
+        std::vector<int> sg(k.size(), -1);
+        for (size_t i = 0; i < k.size(); ++i)
+          if (nodes[k[i]].count == 0) {
+            sg[i] = (int)bin.size();
+            bin.push_back(k[i]);
+            pend.push_back(pd);
+          }
+        kids.push_back(std::move(k));
+        sub.push_back(std::move(sg));
+      }
+      std::vector<int> base(kids.size() + 1, 0);
+      for (size_t g = 0; g < kids.size(); ++g) base[g + 1] = base[g] + (int)kids[g].size();
+      auto code = [&](int g) { return (uint32_t)(base[g] << 5) | (uint32_t)((kids[g].size() - 1) << 3); };
+      fs->qbvh4.resize(base[kids.size()] + 3);
+      for (size_t g = 0; g < kids.size(); ++g)
+        for (size_t i = 0; i < kids[g].size(); ++i) {
+          DQNode e = fs->qbvh[kids[g][i]];
+          if (sub[g][i] >= 0) e.w[3] = code(sub[g][i]);
+          fs->qbvh4[base[g] + i] = e;
+        }
+      for (int i = 0; i < 3; ++i) {
+        DQNode& e = fs->qbvh4[base[kids.size()] + i];
+        e.w[0] = e.w[1] = e.w[2] = 0x0000FFFFu;
+        e.w[3] = ~0u;
+      }
+      fs->bvh4_root = (int32_t)code(0);
     }
   }
   std::vector<DSphere> reordered(n);

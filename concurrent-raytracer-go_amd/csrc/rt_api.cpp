@@ -114,6 +114,7 @@ struct rt_context {
   const DLight* d_lights = nullptr;
   const DBVHNode* d_bvh = nullptr;
   const DQNode* d_qbvh = nullptr;
+  const DQNode* d_qbvh4 = nullptr;
   const uint64_t* d_jump = nullptr;
   const DSky* d_sky = nullptr;  // the kSkies presets
   unsigned long long* d_counts = nullptr;
@@ -439,7 +440,8 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   size_t off_j = off_l + al(f.lights.size() * sizeof(DLight));
   size_t off_b = off_j + al(kJump * 2 * sizeof(uint64_t));
   size_t off_q = off_b + al(f.bvh.size() * sizeof(DBVHNode));
-  size_t off_sky = off_q + al(f.qbvh.size() * sizeof(DQNode));
+  size_t off_q4 = off_q + al(f.qbvh.size() * sizeof(DQNode));
+  size_t off_sky = off_q4 + al(f.qbvh4.size() * sizeof(DQNode));
   size_t total = off_sky + al(kSkies * sizeof(DSky)) + 256;
   rc = quiesce(c);  // the last render may still read the scene
   if (rc) return rc;
@@ -480,6 +482,7 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   }
   memcpy(host + off_b, f.bvh.data(), f.bvh.size() * sizeof(DBVHNode));
   memcpy(host + off_q, f.qbvh.data(), f.qbvh.size() * sizeof(DQNode));
+  memcpy(host + off_q4, f.qbvh4.data(), f.qbvh4.size() * sizeof(DQNode));
   sky_presets(reinterpret_cast<DSky*>(host + off_sky));
   HIP_TRY(hipMemcpyAsync(base, host, total, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -490,6 +493,7 @@ int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
   c->d_lights = (const DLight*)(base + off_l);
   c->d_bvh = (const DBVHNode*)(base + off_b);
   c->d_qbvh = (const DQNode*)(base + off_q);
+  c->d_qbvh4 = (const DQNode*)(base + off_q4);
   c->d_jump = (const uint64_t*)(base + off_j);
   c->d_sky = (const DSky*)(base + off_sky);
   // small linear-scan scenes are staged into LDS by every workgroup
@@ -956,6 +960,18 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
   p.lds_nodes = wf_lds_nodes(p.stack_depth, (int)f.qbvh.size(), p.trav_block, trav_wgs);
   if (tn.wf_lds_nodes >= 0)  // stage fewer nodes (an odd count: child pairs never split)
     p.lds_nodes = std::min(p.lds_nodes, tn.wf_lds_nodes | 1);
+  // the occlusion kernels' 4-wide tree, where it fits the LDS whole beside
+  // its stacks (C4: 4,801 slots and 20 stack entries, 157 KB at 1024
+  // threads).  RTGO_BVH4=0 (measurement switch) keeps the binary walk.
+  p.qbvh4 = c->d_qbvh4;
+  p.nodes4 = (int)f.qbvh4.size();
+  p.stack4 = std::max(1, f.bvh4_stack);
+  p.root4 = f.bvh4_root;
+  {
+    const char* e4 = getenv("RTGO_BVH4");
+    p.use4 = !(e4 && atoi(e4) == 0) && p.nodes4 > 0 && tn.wf_lds_nodes < 0 &&
+             wf_lds_nodes(p.stack4, p.nodes4, p.trav_block, trav_wgs) >= p.nodes4;
+  }
   p.shard_cap = shard_cap;
   p.hard_cap = (int64_t)qcap;
   p.soft_cap = (int64_t)qcap * 16;

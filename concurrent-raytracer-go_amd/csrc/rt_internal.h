@@ -40,6 +40,11 @@ struct FlatScene {
   std::vector<DBVHNode> bvh;  // empty => linear scan
   int32_t bvh_depth = 0;      // levels of the BVH (root = 1): the traversal stack holds fewer entries
   std::vector<DQNode> qbvh;   // the BVH with quantized bounds (same node order)
+  // the same tree collapsed to groups of 2..4 nodes (bvh.cpp): DQNode slots,
+  // groups back to back, breadth-first; the root group's code
+  std::vector<DQNode> qbvh4;
+  int32_t bvh4_stack = 0;     // the most pending children a 4-wide traversal holds
+  int32_t bvh4_root = 0;
   double q0[3] = {0, 0, 0}, qd[3] = {1, 1, 1};  // its grid: coordinate = q0 + q * qd
   double cam_pos[3] = {0, 0, 0};
   double aspect = 0;
@@ -278,6 +283,9 @@ struct WfParams {
   int32_t stack_depth;       // BVH stack entries per lane (the tree's depth - 1)
   int32_t lds_nodes;         // leading quantized nodes (breadth-first: the top levels) staged in LDS
   int32_t bvh_nodes;         // quantized nodes in all
+  const DQNode* qbvh4;       // the 4-wide form (FlatScene::qbvh4): wf_occlude4 walks it when use4
+  int32_t nodes4, stack4, use4;  // its slots, stack entries per lane; 1: staged whole in LDS and used
+  int32_t root4;             // the root group's code
   int32_t trav_block;        // threads per workgroup of the traversal kernels (<= kWfTravBlock)
   int32_t shard_cap;         // path slots per shard
   int32_t live_bound;        // the host's bound on this bounce's live paths (launch sizes only)

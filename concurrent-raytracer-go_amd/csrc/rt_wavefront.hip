@@ -12,7 +12,8 @@
 //             through the BVH); a miss or the depth cut-off ends the path
 //   shade1    the HitRecord (sphere.go:42-58); one hard shadow ray per lit
 //             light (calculateSmartShadow, renderer.go:299-305) queued
-//   occlude   any-hit of the hard rays
+//   occlude   any-hit of the hard rays (wf_occlude4: over the 4-wide tree,
+//             when it fits the LDS whole, as on C4 / C5; else wf_occlude)
 //   cone      per light whose hard ray is clear, the shadow cone's candidate
 //             spheres (a list of <= 16, a wide list of <= 32, or too many)
 //   softgen   the 16 RandomVec3InUnitSphere points (renderer.go:311-318) of
@@ -117,6 +118,16 @@ __device__ __forceinline__ lds_node* stage_tree(const WfParams& p) {
   uint4* t = reinterpret_cast<uint4*>(wf_lds + (size_t)p.trav_block * p.stack_depth * sizeof(int));
   const uint4* src = reinterpret_cast<const uint4*>(p.qbvh);
   for (int i = threadIdx.x; i < p.lds_nodes; i += p.trav_block) t[i] = src[i];
+  __syncthreads();
+  return (lds_node*)t;
+}
+
+// The 4-wide tree (bvh.cpp qbvh4), staged whole behind stacks of p.stack4
+// entries per lane (the host sets use4 only when it fits).
+__device__ __forceinline__ lds_node* stage_tree4(const WfParams& p) {
+  uint4* t = reinterpret_cast<uint4*>(wf_lds + (size_t)p.trav_block * p.stack4 * sizeof(int));
+  const uint4* src = reinterpret_cast<const uint4*>(p.qbvh4);
+  for (int i = threadIdx.x; i < p.nodes4; i += p.trav_block) t[i] = src[i];
   __syncthreads();
   return (lds_node*)t;
 }
@@ -352,6 +363,37 @@ __device__ __forceinline__ void descend(glb_node* __restrict__ qb, lds_node* __r
     } else {
       cur = sp == 0 ? -1 : stack[--sp * 64];
     }
+  }
+}
+
+// The any-hit descent over the 4-wide tree (bvh.cpp qbvh4: groups of 2..4
+// child boxes): a group's boxes are tested at once, the first hit child in
+// slot order is entered and the other hit children are pushed.  Half the
+// dependent LDS round trips of the binary walk.  No distance order: an
+// occlusion query ends at any hit, and sorting the children (full sort, or
+// the nearest first) measured slower, as did the 4-wide tree for closest hit
+// (DESIGN.md §4.2).  The order does not change which rays are blocked.
+template <bool kCount>
+__device__ __forceinline__ void descend4(lds_node* __restrict__ lt, const RayQ& r, float tminf, float tmaxf, int& cur,
+                                         int& sp, int* stack, Counters& c) {
+  while ((cur & 7) == 0) {
+    const int base = cur >> 5, nk = ((cur >> 3) & 3) + 1;  // the group's first slot and size (bvh.cpp)
+    const uint4 n0 = as_uint4(lt[base]), n1 = as_uint4(lt[base + 1]), n2 = as_uint4(lt[base + 2]),
+                n3 = as_uint4(lt[base + 3]);
+    cnt<kCount>(c, C_BOX, nk);
+    float t0, t1, t2, t3;
+    const int cs[4] = {(int)n0.w, (int)n1.w, (int)n2.w, (int)n3.w};
+    const bool hs[4] = {box_q(n0, r, tminf, tmaxf, t0), box_q(n1, r, tminf, tmaxf, t1),
+                        box_q(n2, r, tminf, tmaxf, t2) && nk > 2, box_q(n3, r, tminf, tmaxf, t3) && nk > 3};
+    bool taken = false;
+#pragma unroll
+    for (int k = 3; k >= 0; --k)
+      if (hs[k]) {
+        if (taken) stack[sp++ * 64] = cur;
+        cur = cs[k];
+        taken = true;
+      }
+    if (!taken) cur = sp == 0 ? -1 : stack[--sp * 64];
   }
 }
 
@@ -601,12 +643,12 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade1(const WfParams p) {
 // queued point p (renderer.go:316-318) and a blocked ray adds 1 to its
 // (path, light) count; hard: the ray is lightDir and a blocked ray sets
 // kHardBit.
-template <bool kCount, bool kSoft, bool kFull>
-__global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
+template <bool kCount, bool kSoft, bool kFull, bool kB4>
+__device__ __forceinline__ void occlude_body(const WfParams& p) {
   const Dense dn = dense(kSoft ? p.ctl->soft_cnt : p.ctl->hard_cnt);
   const int n = dn.start[kWfShards];
   if (n == 0) return;
-  lds_node* lt = stage_tree(p);
+  lds_node* lt = kB4 ? stage_tree4(p) : stage_tree(p);
   JobSrc js = job_src(n);
   bool more = true;  // wave-uniform: jobs may remain
   Counters c;
@@ -614,7 +656,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
     for (int k = 0; k < 9; ++k) c.v[k] = 0;
   const int lane = threadIdx.x & 63;
   const unsigned long long below = (1ull << lane) - 1ull;
-  int* stack = wf_stack(p.stack_depth);
+  int* stack = wf_stack(kB4 ? p.stack4 : p.stack_depth);
   const double tmin = 0.001;
   bool busy = false;
   uint32_t key = 0;
@@ -658,7 +700,7 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
           r32 = ray_q(p, o, id);
           tminf = t_lo32(tmin);
           tmaxf = t_hi32(tmax);
-          cur = bvh_code(p.g.bvh[0]);
+          cur = kB4 ? p.root4 : bvh_code(p.g.bvh[0]);
           sp = 0;
           busy = true;
         }
@@ -669,7 +711,10 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
       continue;
     }
     if (busy) {
-      descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, tmaxf, cur, sp, stack, c);
+      if constexpr (kB4)
+        descend4<kCount>(lt, r32, tminf, tmaxf, cur, sp, stack, c);
+      else
+        descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, tmaxf, cur, sp, stack, c);
       bool blocked = false;
       if (cur != -1) {
         const int first = cur >> 3, count = cur & 7;
@@ -692,6 +737,14 @@ __global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
     }
   }
   flush_counts<kCount>(p, c, kSoft ? kGroupSoft : kGroupHard);
+}
+template <bool kCount, bool kSoft, bool kFull>
+__global__ RT_TRAV_ATTR void wf_occlude(const WfParams p) {
+  occlude_body<kCount, kSoft, kFull, false>(p);
+}
+template <bool kCount, bool kSoft>  // over the 4-wide tree (WfParams.use4)
+__global__ RT_TRAV_ATTR void wf_occlude4(const WfParams p) {
+  occlude_body<kCount, kSoft, true, true>(p);
 }
 
 // ---------------------------------------------------------------- cones
@@ -1589,6 +1642,29 @@ static void enqueue_trav(const WfParams& p, hipStream_t st, int which) {
   struct Grids {
     int ext = 0, occ_h = 0, occ_s = 0, cone = 0;
   };
+  if (p.use4 && (which == 1 || which == 2)) {  // occlusion over the 4-wide tree
+    const size_t sh4 = (size_t)p.trav_block * p.stack4 * sizeof(int) + (size_t)p.nodes4 * sizeof(uint4);
+    static std::mutex mu4;
+    static std::map<std::tuple<int, size_t, int>, Grids> cache4;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    Grids g;
+    {
+      std::lock_guard<std::mutex> lock(mu4);
+      const auto key = std::make_tuple(dev, sh4, p.trav_block);
+      auto it = cache4.find(key);
+      if (it == cache4.end()) {
+        Grids c;
+        c.occ_h = resident_grid(wf_occlude4<kCount, false>, p.trav_block, sh4);
+        c.occ_s = resident_grid(wf_occlude4<kCount, true>, p.trav_block, sh4);
+        it = cache4.emplace(key, c).first;
+      }
+      g = it->second;
+    }
+    if (which == 1) hipLaunchKernelGGL((wf_occlude4<kCount, false>), dim3(g.occ_h), bt, sh4, st, p);
+    if (which == 2) hipLaunchKernelGGL((wf_occlude4<kCount, true>), dim3(g.occ_s), bt, sh4, st, p);
+    return;
+  }
   static std::mutex mu;
   static std::map<std::tuple<int, size_t, int>, Grids> cache;
   int dev = 0;

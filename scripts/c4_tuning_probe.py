@@ -26,8 +26,12 @@ def main():
     lin = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
     for var in sys.argv[1:] or [""]:
         over = {}
+        os.environ.pop("RTGO_BVH4", None)
         for kv in filter(None, var.split(",")):
             k, _, v = kv.partition("=")
+            if k.startswith("env."):  # an environment switch of the library (env.RTGO_BVH4=1)
+                os.environ[k[4:]] = v
+                continue
             over[k] = float(v) if "." in v else int(v)
         ctx = rtgo.Context(0)
         ctx.set_tuning(rtgo.default_tuning(**over))

@@ -15,7 +15,7 @@ reports half the bytes of wide streaming reads on gfx950 (x2 here);
 WRITE_SIZE is exact for this code's store patterns (calibrated on
 unpack_kernel, profiles/r02_pmc_calibration.json).
 c2 / c3: the render kernel, the median over its launches.  c4 / c5: the
-soft-shadow stage's kernels (wf_cone, wf_listtest, wf_widetest, wf_occlude<soft>: the
+soft-shadow stage's kernels (wf_cone, wf_listtest, wf_widetest, wf_occlude4<soft>: the
 roofline's kernels for those configs), summed over a frame's launches
 (bench.py prices them per frame), and the whole frame's bytes beside it.
 """

@@ -28,7 +28,7 @@ for scene in ${INSTMIX_SCENES:-headline c4}; do
     dirs+=("$d")
   done
   if [ "$scene" = c4 ]; then
-    for k in "wf_extend<false, true>" "wf_occlude<false, true, true>" "wf_occlude<false, false, true>" \
+    for k in "wf_extend<false, true>" "wf_occlude4<false, true>" "wf_occlude4<false, false>" \
       "wf_cone<false, true>" "wf_listtest<false>"; do
       tag=$(echo "$k" | tr -dc 'a-z_,' | tr ',' '_')
       python3 scripts/pmc_instmix.py "$k" gpurun_out/profiles_${R}/${R}_instmix_c4_${tag}.json "${dirs[@]}"
