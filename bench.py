@@ -113,9 +113,9 @@ KERNELS = {  # the dominant kernel of each config (rocprofv3 --stats, profiles/)
     "c2_committed": "rtgo::render_kernel<false, true, false, false>",
     "c3": "rtgo::render_kernel<false, true, false, false>",
     # the soft-shadow stage: cone walks, list tests, traced soft rays
-    "c4": "rtgo::wf_cone<false, true> + rtgo::wf_listtest<false> + rtgo::wf_widetest<false> + "
+    "c4": "rtgo::wf_cone4<false> + rtgo::wf_listtest<false> + rtgo::wf_widetest<false> + "
           "rtgo::wf_occlude4<false, true>",
-    "c5": "rtgo::wf_cone<false, true> + rtgo::wf_listtest<false> + rtgo::wf_widetest<false> + "
+    "c5": "rtgo::wf_cone4<false> + rtgo::wf_listtest<false> + rtgo::wf_widetest<false> + "
           "rtgo::wf_occlude4<false, true>",
 }
 SOFT_STAGE = ("cone", "cone_rays", "occlude_soft")  # its kernel classes (rtgo.WF_KERNELS)

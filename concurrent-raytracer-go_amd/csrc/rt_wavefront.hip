@@ -12,8 +12,9 @@
 //             through the BVH); a miss or the depth cut-off ends the path
 //   shade1    the HitRecord (sphere.go:42-58); one hard shadow ray per lit
 //             light (calculateSmartShadow, renderer.go:299-305) queued
-//   occlude   any-hit of the hard rays (wf_occlude4: over the 4-wide tree,
-//             when it fits the LDS whole, as on C4 / C5; else wf_occlude)
+//   occlude   any-hit of the hard rays (wf_occlude4 / wf_cone4: occlusion and
+//             cone walks over the 4-wide tree when it fits the LDS whole, as
+//             on C4 / C5; else wf_occlude / wf_cone over the binary one)
 //   cone      per light whose hard ray is clear, the shadow cone's candidate
 //             spheres (a list of <= 16, a wide list of <= 32, or too many)
 //   softgen   the 16 RandomVec3InUnitSphere points (renderer.go:311-318) of
@@ -866,6 +867,30 @@ __device__ __forceinline__ void cone_descend(glb_node* __restrict__ qb, lds_node
   }
 }
 
+// The same walk over the 4-wide tree (descend4's order: the first hit child
+// entered, the other hit children pushed)
+template <bool kCount>
+__device__ __forceinline__ void cone_descend4(lds_node* __restrict__ lt, const ConeQ& k, int& cur, int& sp, int* stack,
+                                              Counters& c) {
+  while ((cur & 7) == 0) {
+    const int base = cur >> 5, nk = ((cur >> 3) & 3) + 1;  // the group's first slot and size (bvh.cpp)
+    const uint4 n0 = as_uint4(lt[base]), n1 = as_uint4(lt[base + 1]), n2 = as_uint4(lt[base + 2]),
+                n3 = as_uint4(lt[base + 3]);
+    cnt<kCount>(c, C_BOX, nk);
+    const int cs[4] = {(int)n0.w, (int)n1.w, (int)n2.w, (int)n3.w};
+    const bool hs[4] = {cone_node(n0, k), cone_node(n1, k), cone_node(n2, k) && nk > 2, cone_node(n3, k) && nk > 3};
+    bool taken = false;
+#pragma unroll
+    for (int i = 3; i >= 0; --i)
+      if (hs[i]) {
+        if (taken) stack[sp++ * 64] = cur;
+        cur = cs[i];
+        taken = true;
+      }
+    if (!taken) cur = sp == 0 ? -1 : stack[--sp * 64];
+  }
+}
+
 // lights base + i (i < 32) of a path that are lit (wf_shade1: not within
 // 0.001 of the hit point) and whose hard ray is clear; `listed`: those of
 // them whose cone left a candidate list
@@ -919,12 +944,12 @@ __global__ __launch_bounds__(kWfBlock) void wf_conegen(const WfParams p) {
 // kWfConeK (one more ends the walk: the cone's rays are traced instead).
 // The hit sphere itself is left out as in cone_candidates (rt_kernel.hip)
 // when the cone leaves its front face at a clear angle.
-template <bool kCount, bool kFull>
-__global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
+template <bool kCount, bool kFull, bool kB4>
+__device__ __forceinline__ void cone_body(const WfParams& p) {
   const Dense dn = dense(p.ctl->cone_cnt);
   const int n = dn.start[kWfShards];
   if (n == 0) return;
-  lds_node* lt = stage_tree(p);
+  lds_node* lt = kB4 ? stage_tree4(p) : stage_tree(p);
   JobSrc js = job_src(n);
   bool more = true;  // wave-uniform: jobs may remain
   Counters c;
@@ -932,7 +957,7 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
     for (int k = 0; k < 9; ++k) c.v[k] = 0;
   const int lane = threadIdx.x & 63;
   const unsigned long long below = (1ull << lane) - 1ull;
-  int* stack = wf_stack(p.stack_depth);
+  int* stack = wf_stack(kB4 ? p.stack4 : p.stack_depth);
   bool busy = false;
   uint32_t key = 0;
   d3 P = mk(0, 0, 0), u = mk(0, 0, 0);
@@ -960,7 +985,7 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
         // (a cone whose bounds cannot be evaluated is not walked: "too many
         // candidates", so its rays are traced)
         found = ok ? 0 : kWfConeWide + 1;
-        cur = ok ? bvh_code(p.g.bvh[0]) : -1;
+        cur = ok ? (kB4 ? p.root4 : bvh_code(p.g.bvh[0])) : -1;
         sp = 0;
         busy = true;
       }
@@ -970,7 +995,10 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
       continue;
     }
     if (busy) {
-      cone_descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, k, cur, sp, stack, c);
+      if constexpr (kB4)
+        cone_descend4<kCount>(lt, k, cur, sp, stack, c);
+      else
+        cone_descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, k, cur, sp, stack, c);
       if (cur != -1) {
         const int first = cur >> 3, count = cur & 7;
         DSphere ls[kLeafBatch];
@@ -1002,6 +1030,14 @@ __global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
     }
   }
   flush_counts<kCount>(p, c, kGroupSoft);
+}
+template <bool kCount, bool kFull>
+__global__ RT_TRAV_ATTR void wf_cone(const WfParams p) {
+  cone_body<kCount, kFull, false>(p);
+}
+template <bool kCount>  // over the 4-wide tree (WfParams.use4)
+__global__ RT_TRAV_ATTR void wf_cone4(const WfParams p) {
+  cone_body<kCount, true, true>(p);
 }
 
 // The image pixel (y W + x) and sample index of sample id `sid` (wf_regen's
@@ -1642,7 +1678,7 @@ static void enqueue_trav(const WfParams& p, hipStream_t st, int which) {
   struct Grids {
     int ext = 0, occ_h = 0, occ_s = 0, cone = 0;
   };
-  if (p.use4 && (which == 1 || which == 2)) {  // occlusion over the 4-wide tree
+  if (p.use4 && which != 0) {  // occlusion and cone walks over the 4-wide tree
     const size_t sh4 = (size_t)p.trav_block * p.stack4 * sizeof(int) + (size_t)p.nodes4 * sizeof(uint4);
     static std::mutex mu4;
     static std::map<std::tuple<int, size_t, int>, Grids> cache4;
@@ -1657,12 +1693,14 @@ static void enqueue_trav(const WfParams& p, hipStream_t st, int which) {
         Grids c;
         c.occ_h = resident_grid(wf_occlude4<kCount, false>, p.trav_block, sh4);
         c.occ_s = resident_grid(wf_occlude4<kCount, true>, p.trav_block, sh4);
+        c.cone = resident_grid(wf_cone4<kCount>, p.trav_block, sh4);
         it = cache4.emplace(key, c).first;
       }
       g = it->second;
     }
     if (which == 1) hipLaunchKernelGGL((wf_occlude4<kCount, false>), dim3(g.occ_h), bt, sh4, st, p);
     if (which == 2) hipLaunchKernelGGL((wf_occlude4<kCount, true>), dim3(g.occ_s), bt, sh4, st, p);
+    if (which == 3) hipLaunchKernelGGL((wf_cone4<kCount>), dim3(g.cone), bt, sh4, st, p);
     return;
   }
   static std::mutex mu;

@@ -29,7 +29,7 @@ for scene in ${INSTMIX_SCENES:-headline c4}; do
   done
   if [ "$scene" = c4 ]; then
     for k in "wf_extend<false, true>" "wf_occlude4<false, true>" "wf_occlude4<false, false>" \
-      "wf_cone<false, true>" "wf_listtest<false>"; do
+      "wf_cone4<false>" "wf_listtest<false>"; do
       tag=$(echo "$k" | tr -dc 'a-z_,' | tr ',' '_')
       python3 scripts/pmc_instmix.py "$k" gpurun_out/profiles_${R}/${R}_instmix_c4_${tag}.json "${dirs[@]}"
     done
