@@ -82,7 +82,10 @@ def test_wavefront_all_sphere_materials_matches_oracle():
                               "small_traversal_groups", "leaf1", "leaf7_bins4"])
 def test_capacity_and_chunks_do_not_change_the_image(tun):
     """... nor how much of the BVH the traversal kernels stage in LDS (by
-    default all of it; here none, or only the top 31 nodes)."""
+    default all of it; here none, or only the top 31 nodes).  With
+    wf_lds_nodes set, occlusion and cone walks take the binary tree instead
+    of the 4-wide one (WfParams.use4), so those cases also hold the two
+    walks to the same bits."""
     scene = rtgo.Scene.from_json_text(json.dumps(_sphere_field(200, seed=9)))
     st = make_settings(rtgo, {"samples": 7})
     base = _render(scene, 50, 37, st, mega=False)
