@@ -24,13 +24,17 @@ def main():
     spec, W, H, SPP = CONFIGS["c4"][:4]
     scene = load_scene(rtgo, spec)
     lin = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
+    set_env = []
     for var in sys.argv[1:] or [""]:
         over = {}
-        os.environ.pop("RTGO_BVH4", None)
+        for k in set_env:  # (a variant's environment switches end with it)
+            os.environ.pop(k, None)
+        set_env = []
         for kv in filter(None, var.split(",")):
             k, _, v = kv.partition("=")
-            if k.startswith("env."):  # an environment switch of the library (env.RTGO_BVH4=1)
+            if k.startswith("env."):  # an environment switch of the library (env.RTGO_BVH4=0)
                 os.environ[k[4:]] = v
+                set_env.append(k[4:])
                 continue
             over[k] = float(v) if "." in v else int(v)
         ctx = rtgo.Context(0)
