@@ -2,7 +2,8 @@
 //
 //   raytracer <scene_file> <output_file> <width> <height>
 //             [--samples N] [--max-depth N] [--seed N] [--no-soft-shadows]
-//             [--no-recursive] [--devices N] [--sky default|white|sunset|night]
+//             [--no-recursive] [--devices N] [--watchdog SECONDS]
+//             [--sky default|white|sunset|night]
 //
 // Same positional arguments, stdout lines, ".png" default extension
 // (main.go:53-56) and benchmark_data.json next to the output
@@ -138,6 +139,7 @@ static void save_benchmark(const std::string& out_path, long long w, long long h
 
 int main(int argc, char** argv) {
   std::vector<std::string> args;
+  double watchdog_s = 0;  // --watchdog (0: no bound, as Go's Render)
   rt_settings st;
   rt_settings_default(&st);
   st.num_workers = (int32_t)sysconf(_SC_NPROCESSORS_ONLN);  // runtime.NumCPU(), main.go:46
@@ -167,6 +169,14 @@ int main(int argc, char** argv) {
     } else if (a == "--devices") {  // GPUs the tiles are sharded over (rt_settings.num_devices)
       if (!parse_int(need("--devices"), &v) || v < 1) return 2;
       st.num_devices = (int32_t)v;
+    } else if (a == "--watchdog") {  // multi-device frames: RT_E_TIMEOUT after SECONDS (rt_renderer_set_watchdog)
+      const char* x = need("--watchdog");
+      char* end = nullptr;
+      watchdog_s = strtod(x, &end);
+      if (!end || *end || !(watchdog_s >= 0)) {
+        fprintf(stderr, "invalid --watchdog %s\n", x);
+        return 2;
+      }
     } else if (a == "--sky") {  // opt-in sky on miss (atmosphere.go presets); default: black
       const std::string k = need("--sky");
       if (k == "none") st.sky = RT_SKY_NONE;
@@ -262,6 +272,7 @@ int main(int argc, char** argv) {
     rt_scene_free(sb);
     return 2;
   }
+  if (watchdog_s > 0) rt_renderer_set_watchdog(rr, watchdog_s);
   const double new_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_new).count();
   printf("Rendering at %lldx%lld resolution...\n", w, h);
   fflush(stdout);

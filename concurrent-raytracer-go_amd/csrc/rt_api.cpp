@@ -15,6 +15,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt_rng.h"
@@ -179,6 +180,9 @@ struct rt_context {
   std::vector<ProfBlock> prof_pending;
   double prof_secs[kWfClasses] = {0};
   int64_t prof_launches[kWfClasses] = {0};
+  // a multi-rank renderer's frame deadline (steady_now_s() clock; <= 0:
+  // none), set by rt_renderer_render for the frame (context_set_deadline)
+  double deadline = 0;
 };
 
 // Events for kernel classes [first, last] of one launch sequence: ev[k] opens
@@ -240,6 +244,58 @@ namespace rtgo {
 bool context_has_bvh(const rt_context* c) { return c && !c->flat.bvh.empty(); }
 double context_bvh_seconds(const rt_context* c) { return c ? c->bvh_seconds : 0.0; }
 void* context_stream(const rt_context* c) { return c ? (void*)c->stream : nullptr; }
+}  // namespace rtgo
+
+namespace rtgo {
+double steady_now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void context_set_deadline(rt_context* c, double deadline) {
+  if (c) c->deadline = deadline;
+}
+
+// The context's host waits during a render.  Without a deadline they block
+// (hipStreamSynchronize / hipEventSynchronize); with one (a multi-rank
+// renderer's frame, rt_renderer_set_watchdog) they poll (yield, then 20 us
+// sleeps) and return RT_E_TIMEOUT once it has passed, so a stalled rank ends
+// the frame instead of blocking its host thread forever.
+template <class Query>
+int bounded_wait(rt_context* c, Query query, const char* what) {
+  for (unsigned spin = 0;; ++spin) {
+    const hipError_t e = query();
+    if (e == hipSuccess) return RT_OK;
+    if (e != hipErrorNotReady) {
+      set_error(std::string(what) + " failed: " + hipGetErrorString(e));
+      return RT_E_DEVICE;
+    }
+    if (steady_now_s() > c->deadline) {
+      set_error(std::string("watchdog: ") + what + " did not complete before the frame's deadline");
+      return RT_E_TIMEOUT;
+    }
+    if (spin < 256)
+      std::this_thread::yield();
+    else
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+int wait_stream(rt_context* c, hipStream_t s) {
+  if (c->deadline <= 0) {
+    HIP_TRY(hipStreamSynchronize(s));
+    return RT_OK;
+  }
+  return bounded_wait(c, [s] { return hipStreamQuery(s); }, "a wait for the render stream");
+}
+
+int wait_event(rt_context* c, hipEvent_t ev) {
+  if (c->deadline <= 0) {
+    HIP_TRY(hipEventSynchronize(ev));
+    return RT_OK;
+  }
+  return bounded_wait(c, [ev] { return hipEventQuery(ev); }, "a wait for a render event");
+}
+
 }  // namespace rtgo
 
 extern "C" {
@@ -404,9 +460,9 @@ void rt_context_destroy(rt_context* c) {
 // Wait until the last render enqueued on this context has finished: before
 // the host overwrites buffers it reads (scene, schedule, wavefront state).
 static int quiesce(rt_context* c) {
-  if (c->have_timing) HIP_TRY(hipEventSynchronize(c->ev1));
-  if (c->stream) HIP_TRY(hipStreamSynchronize(c->stream));
-  return RT_OK;
+  int rc = c->have_timing ? wait_event(c, c->ev1) : RT_OK;
+  if (!rc && c->stream) rc = wait_stream(c, c->stream);
+  return rc;
 }
 
 int rt_context_set_scene(rt_context* c, const rt_scene* s, int32_t force_bvh) {
@@ -792,7 +848,8 @@ static int prepare_schedule(rt_context* c, KParams* p, const rt_settings* st, hi
       if (!hip_ok(hipMemcpyAsync(c->h_small, sp.totals, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s),
                   "schedule count read-back"))
         return fail_synced(RT_E_DEVICE);
-      HIP_TRY(hipStreamSynchronize(s));
+      rc = wait_stream(c, s);  // (bounded under a renderer's deadline)
+      if (rc) return rc;
       memcpy(c->h_totals, c->h_small, 3 * sizeof(int32_t));
       const int nblocks = c->h_totals[0], nsplit = c->h_totals[1];
       rc = grow(c, &c->d_blocks, &c->d_blocks_cap, (size_t)std::max(nblocks, 1) * kBlockInts * sizeof(int32_t));
@@ -1048,7 +1105,8 @@ static int render_wavefront(rt_context* c, const KParams& kp, const rt_settings*
         HIP_TRY(hipEventRecord(c->wf_ev[r], s));
         if (it >= 1) {
           const int pr = (int)((it - 1) % kWfRing);
-          HIP_TRY(hipEventSynchronize(c->wf_ev[pr]));
+          const int rw = wait_event(c, c->wf_ev[pr]);  // (bounded under a renderer's deadline)
+          if (rw) return rw;
           const WfCtl& h = c->wf_host[pr];
           if (h.live == 0 && h.dry) break;  // bounce `it` had nothing to do
           // once dry, live counts only fall: bounce it + 1 has at most h.live paths

@@ -45,14 +45,7 @@ __device__ __forceinline__ d3 operator+(d3 a, d3 b) { return mk(a.x + b.x, a.y +
 __device__ __forceinline__ d3 operator-(d3 a, d3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 __device__ __forceinline__ d3 mul(d3 a, d3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
 __device__ __forceinline__ d3 muls(d3 a, double s) { return mk(a.x * s, a.y * s, a.z * s); }
-#ifdef RT_EXP_FASTDIV  // timing experiment only (scripts/build_variant.sh): inexact, wrong images
-__device__ __forceinline__ d3 divs(d3 a, double s) {
-  const double r = __builtin_amdgcn_rcp(s);
-  return mk(a.x * r, a.y * r, a.z * r);
-}
-#else
 __device__ __forceinline__ d3 divs(d3 a, double s) { return mk(a.x / s, a.y / s, a.z / s); }
-#endif
 __device__ __forceinline__ d3 neg(d3 a) { return mk(a.x * -1, a.y * -1, a.z * -1); }  // MulScalar(-1)
 __device__ __forceinline__ double dot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 __device__ __forceinline__ d3 cross(d3 a, d3 b) {

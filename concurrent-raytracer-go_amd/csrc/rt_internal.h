@@ -360,6 +360,12 @@ rt_partition* make_partition(PartitionData&& d);
 bool context_has_bvh(const rt_context* c);
 double context_bvh_seconds(const rt_context* c);
 void* context_stream(const rt_context* c);  // its own non-blocking stream (hipStream_t)
+// A multi-rank renderer's frame deadline on a context (steady_now_s() clock,
+// <= 0: none): the context's host waits during a render (the previous render
+// before buffers are reused, the schedule's count read-back, the wavefront
+// loop's per-bounce state) poll until it and return RT_E_TIMEOUT after it.
+void context_set_deadline(rt_context* c, double deadline);
+double steady_now_s();
 const PartitionData& partition_data(const rt_partition* p);
 
 // ---------------------------------------------------------------- output

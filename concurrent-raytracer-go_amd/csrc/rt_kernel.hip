@@ -74,8 +74,8 @@ constexpr int kSqTries = RT_SQ_TRIES;
 #ifndef RT_SOLO
 #define RT_SOLO 0
 #endif
-#ifndef RT_EXP_NO_CONE_WIDE
-#define RT_EXP_NO_CONE_WIDE 0
+#ifndef RT_CONE_WIDE
+#define RT_CONE_WIDE 1
 #endif
 
 namespace rtgo {
@@ -393,12 +393,6 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
   sq_unocc[lane] = 0;
   int need = need_soft ? 16 : 0, free_rays = 0;  // free_rays: points of an owner with nothing to trace
   int head = 0, tail = 0;  // wave-uniform ring positions
-#ifdef RT_EXP_FREE_SKIP  // timing experiment only: an owner with nothing to trace draws no tries (wrong stream)
-  if (need > 0 && !trace) {
-    free_rays = 16;
-    need = 0;
-  }
-#endif
   for (;;) {
     // kSqTries tries per pass: the later tries are drawn ahead and each
     // is consumed only when the owner still needs a point after the ones
@@ -494,14 +488,8 @@ __device__ __forceinline__ int soft_queue(const Geo& p, bool masks, bool need_so
       const Cand co{__shfl(cm.s, ow), p.nt ? __shfl(cm.t, ow) : 0ull};  // (no triangles: cm.t is 0)
       if (lane < n) {
         const d3 pt = mk(rt_bits_to_unit(e.x) * 2 - 1, rt_bits_to_unit(e.y) * 2 - 1, rt_bits_to_unit(e.z) * 2 - 1);
-#if defined(RT_EXP_NO_SOFT_TRACE)  // timing experiments only (scripts/build_variant.sh): wrong images
-        atomicAdd(&sq_unocc[ow], 1);
-#elif defined(RT_EXP_NO_SOFT_NORM)
-        if (!shadow_blocked<kCount>(p, masks, Po, Lo + muls(pt, 0.1), dist, co, stack, c)) atomicAdd(&sq_unocc[ow], 1);
-#else
         if (!shadow_blocked<kCount>(p, masks, Po, normalize(Lo + muls(pt, 0.1)), dist, co, stack, c))
           atomicAdd(&sq_unocc[ow], 1);
-#endif
       }
       head += n;
       __syncthreads();
@@ -1570,7 +1558,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
           const bool hard = shade && lit && (kCount || !dark);
           bool wide_c = false;
           if constexpr (kStage) {  // few lit hit points: the cone tests with helpers
-            if (masks && gg.nt == 0 && !RT_EXP_NO_CONE_WIDE) {
+            if (masks && gg.nt == 0 && RT_CONE_WIDE) {
               const unsigned long long cq = __ballot(hard);
               const int ncq = __popcll(cq);
               if (ncq > 0 && ncq <= 16) {
@@ -1631,12 +1619,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
 #ifdef RT_WG_TIMING
           const unsigned long long ts2 = __builtin_amdgcn_s_memtime();
 #endif
-#ifdef RT_EXP_NO_SOFT  // timing experiment only (scripts/build_variant.sh): no soft-shadow draws or rays
-          if (need_soft) unocc = 16;
-          if (false) {
-#else
           if (owners != 0) {
-#endif
 #ifdef RT_WG_TIMING
             if (__popcll(owners) <= kCoopMax) dbg_coop += __popcll(owners); else ++dbg_seq;
 #endif

@@ -172,7 +172,7 @@ struct rt_renderer {
   void* h_img = nullptr;
   size_t h_img_cap = 0;
   int64_t frames = 0;              // Render calls so far
-  double watchdog_s = 120.0;       // bound on a multi-rank frame's wait (rt_renderer_set_watchdog)
+  double watchdog_s = 0;           // bound on a multi-rank frame (rt_renderer_set_watchdog; 0: none, as Go's Render)
   std::string stalled;             // set when the watchdog fired: the renderer is unusable
   int stall_rank = -1;             // test hook (rt_renderer_test_stall)
   double stall_ms = 0;
@@ -495,12 +495,44 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
   if (!rc) rc = r->img_rgba.grow(root, npix * 4);
   if (rc) return rc;
   hipStream_t root_s = r->ranks[0].stream;
+  // A multi-rank frame with a watchdog (rt_renderer_set_watchdog) has one
+  // deadline, taken here before anything of the frame runs: every host wait
+  // of the frame is bounded by it -- each rank's own waits inside its render
+  // (its previous render, the schedule build, a BVH scene's bounce loop: the
+  // rank contexts poll, context_set_deadline) and the waits for the ranks'
+  // streams after the launches (bounded_sync, below).
+  const double deadline = n > 1 && r->watchdog_s > 0 ? now_s() + r->watchdog_s : 0.0;
+  for (Rank& q : r->ranks) context_set_deadline(q.ctx, deadline);
+  struct ClearDeadline {
+    rt_renderer* r;
+    ~ClearDeadline() {
+      for (Rank& q : r->ranks) context_set_deadline(q.ctx, 0.0);
+    }
+  } clear_deadline{r};
+  // the watchdog fired for rank k: the communicators are aborted and the
+  // renderer refuses later calls (the stalled work may never end)
+  auto timed_out = [&](int k, const char* where) {
+    const std::string part =
+        r->part ? "balanced, " + std::to_string(rt_partition_local_tiles(r->part, k)) + " tiles on this rank"
+                : "strided t % " + std::to_string(n) + ", " + std::to_string(rt_tiles_for_rank(w, h, k, n)) +
+                      " tiles on this rank";
+    r->stalled = "rt_renderer_render: watchdog: rank " + std::to_string(k) + " (device " +
+                 std::to_string(r->ranks[k].device) + ") did not finish frame " + std::to_string(r->frames) + " (" +
+                 std::to_string(w) + "x" + std::to_string(h) + ", " + std::to_string(st->samples) + " spp) within " +
+                 std::to_string(r->watchdog_s) + " s: " + where + " (partition " + part +
+                 "); communicators aborted, the renderer is unusable";
+    for (ncclComm_t c : r->comms) (void)ncclCommAbort(c);
+    r->comms.clear();
+    set_error(r->stalled);
+    return RT_E_TIMEOUT;
+  };
   if (n == 1) {
     rc = rt_context_render_async(r->ranks[0].ctx, w, h, st, 0, 1, RT_LAYOUT_IMAGE, (float*)r->img_lin.p,
                                  (uint8_t*)r->img_rgba.p, root_s, nullptr);
     if (rc) return rc;
   } else {
     rc = renderer_partition(r, scene, w, h, st);
+    if (rc == RT_E_TIMEOUT) return timed_out(0, "the partition's measuring render stalled");
     if (rc) return rc;
     const size_t share = r->part ? rt_partition_packed_bytes(r->part) : rt_packed_bytes(w, h, n);
     const size_t rgba_off = r->part ? rt_partition_rgba_offset(r->part) : rt_packed_rgba_offset(w, h, n);
@@ -544,6 +576,8 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
     }
     render_rank(0);
     for (std::thread& t : pool) t.join();
+    for (int k = 1; k <= n; ++k)  // (the other ranks first, as below)
+      if (rcs[k % n] == RT_E_TIMEOUT) return timed_out(k % n, "its share render stalled before its launches");
     for (int k = 0; k < n; ++k)
       if (rcs[k]) {
         set_error(errs[k]);
@@ -575,31 +609,17 @@ int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t w, int32_t
   // stream it starts at once.
   double ks = 0;
   r->rank_secs.assign(n, 0.0);
-  // a multi-rank frame waits at most watchdog_s from here (its launches and
-  // the gather are all enqueued): a stalled rank or collective ends the wait
-  const double deadline = n > 1 && r->watchdog_s > 0 ? t_launch + r->watchdog_s : 0.0;
+  // (a multi-rank frame waits at most until its deadline: a stalled rank or
+  // collective ends the wait)
   // (the other ranks first: the root's stream waits for every rank's share
   // before its unpack, so a stalled rank is named as itself, not as the root)
   for (int i = 1; i <= n; ++i) {
     const int k = i % n;
     Rank& q = r->ranks[k];
     rc = bounded_sync(q.device, q.stream, deadline);
-    if (rc == RT_E_TIMEOUT) {
-      const std::string part =
-          r->part ? "balanced, " + std::to_string(rt_partition_local_tiles(r->part, k)) + " tiles on this rank"
-                  : "strided t % " + std::to_string(n) + ", " + std::to_string(rt_tiles_for_rank(w, h, k, n)) +
-                        " tiles on this rank";
-      r->stalled = "rt_renderer_render: watchdog: rank " + std::to_string(k) + " (device " +
-                   std::to_string(q.device) + ") did not finish frame " + std::to_string(r->frames) + " (" +
-                   std::to_string(w) + "x" + std::to_string(h) + ", " + std::to_string(st->samples) +
-                   " spp) within " + std::to_string(r->watchdog_s) + " s of its launch: its share render" +
-                   (r->devices.size() > 1 ? ", the RCCL gather" : "") + " or the unpack stalled (partition " + part +
-                   "); communicators aborted, the renderer is unusable";
-      for (ncclComm_t c : r->comms) (void)ncclCommAbort(c);
-      r->comms.clear();
-      set_error(r->stalled);
-      return RT_E_TIMEOUT;
-    }
+    if (rc == RT_E_TIMEOUT)
+      return timed_out(k, r->devices.size() > 1 ? "its share render, the RCCL gather or the unpack stalled"
+                                                 : "its share render or the unpack stalled");
     if (rc) return rc;
     double s = 0;
     rc = rt_context_last_kernel_seconds(q.ctx, &s);

@@ -273,16 +273,20 @@ int rt_renderer_create(const int32_t* devices, int32_t num_devices, rt_renderer*
 int rt_renderer_render(rt_renderer* r, const rt_scene* scene, int32_t width, int32_t height,
                        const rt_settings* settings, float* out_linear_rgb, uint8_t* out_rgba, rt_stats* stats);
 void rt_renderer_destroy(rt_renderer* r);
-/* Watchdog of a multi-rank Render (more than one rank): if a rank's share
- * render, the RCCL gather into the first device (renderer.go:398-436 is the
- * tile farm-out it replaces) or the unpack has not completed `seconds` after
- * the frame was enqueued, Render stops waiting, aborts the renderer's RCCL
- * communicators and returns RT_E_TIMEOUT with the rank, device, frame and
- * partition in rt_last_error().  The renderer is then unusable: later calls
- * return RT_E_TIMEOUT, and rt_renderer_destroy releases only what does not
- * wait on the stalled work (exit the process to reclaim the rest).  Default
- * 120 s; seconds <= 0 waits without a bound.  One-rank renders have no
- * collective and are never bounded. */
+/* Watchdog of a multi-rank Render (more than one rank): the frame gets one
+ * deadline, `seconds` after Render starts (after the scene upload).  Every
+ * host wait of the frame is bounded by it: each rank's waits inside its share
+ * render (its previous render, the schedule build, a BVH scene's bounce loop),
+ * the partition's measuring render, and the waits for the ranks' streams, the
+ * RCCL gather into the first device (renderer.go:398-436 is the tile farm-out
+ * it replaces) and the unpack.  Past it, Render stops waiting, aborts the
+ * renderer's RCCL communicators and returns RT_E_TIMEOUT with the rank,
+ * device, frame and partition in rt_last_error().  The renderer is then
+ * unusable: later calls return RT_E_TIMEOUT, and rt_renderer_destroy releases
+ * only what does not wait on the stalled work (exit the process to reclaim the
+ * rest).  Default 0: no bound, as Go's Render (a large frame may take
+ * minutes); callers opt in (the CLI: --watchdog SECONDS).  One-rank renders
+ * have no collective and are never bounded. */
 int rt_renderer_set_watchdog(rt_renderer* r, double seconds);
 /* Test hook for the watchdog: the renderer's next multi-rank frame first
  * runs, on `rank`'s stream, one workgroup that sleeps for `ms` (0..60000)

@@ -93,25 +93,11 @@ RT_RNG_FN uint32_t rt_pcg_out(uint64_t x) {
   return (xs >> rot) | (xs << ((32u - rot) & 31u));
 }
 
-#if defined(RT_EXP_CHEAP_RNG) && defined(__HIP_DEVICE_COMPILE__)
-/* timing experiment only (scripts/build_variant.sh): a xorshift32 step in
- * place of the PCG step -- a different stream, so different images; it bounds
- * what the draws cost the kernel */
-RT_RNG_FN uint32_t rt_rng_next(rt_rng* r) {
-  uint32_t x = (uint32_t)r->x | 1u;
-  x ^= x << 13;
-  x ^= x >> 17;
-  x ^= x << 5;
-  r->x = (r->x & 0xFFFFFFFF00000000ULL) | x;
-  return x;
-}
-#else
 RT_RNG_FN uint32_t rt_rng_next(rt_rng* r) {
   const uint64_t old = r->x;
   r->x = old * RT_PCG_MULT + RT_PCG_INC;
   return rt_pcg_out(old);
 }
-#endif
 
 /* x * 2^-32, built from the bits: 1.x (x in the top 32 mantissa bits) - 1 */
 RT_RNG_FN double rt_bits_to_unit(uint32_t x) {

@@ -6,7 +6,9 @@ CPU: the harness compiles against include/rt_api.h and librtgo.so; the
 marshalled scene parses to exactly the scene the loader makes from the
 original JSON; without a GPU the sequence stops at rt_renderer_create with
 RT_E_DEVICE and a message (no CPU fallback).
-GPU: the harness's image equals the Python mirror's render bit for bit."""
+GPU: the harness's image equals the CPU oracle's render of the same
+Go-marshalled scene and settings bit for bit (the parity pin of SURVEY §8f
+row 3), and the Python mirror's render too."""
 import json
 import os
 import subprocess
@@ -71,7 +73,7 @@ def test_sequence_fails_loudly_without_a_gpu(harness, tmp_path):
     import torch
 
     if torch.cuda.is_available():
-        pytest.skip("a GPU is present: see test_sequence_renders_like_the_mirror")
+        pytest.skip("a GPU is present: see test_sequence_renders_like_the_oracle")
     p = subprocess.run([harness, MARSHALLED, "32", "24", "2", str(tmp_path / "o.rgba")], capture_output=True,
                        text=True, timeout=120)
     assert p.returncode == 3
@@ -80,7 +82,7 @@ def test_sequence_fails_loudly_without_a_gpu(harness, tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("devices", ["0", "0,0,0"], ids=["1_rank", "3_ranks_on_device_0"])
-def test_sequence_renders_like_the_mirror(harness, tmp_path, devices):
+def test_sequence_renders_like_the_oracle(harness, tmp_path, devices):
     w, h, spp = 64, 48, 3
     out = tmp_path / "o.rgba"
     p = subprocess.run([harness, MARSHALLED, str(w), str(h), str(spp), str(out), str(devices)], capture_output=True,
@@ -89,6 +91,17 @@ def test_sequence_renders_like_the_mirror(harness, tmp_path, devices):
     assert "objects 11 lights 3" in p.stdout
     assert "Created 11 hittables total" in p.stdout  # GetHittables' lines (scene.go:62-88)
     got = np.fromfile(out, np.uint8).reshape(h, w, 4)
+    # the oracle (test infrastructure: the checker) on the scene bytes the
+    # harness read and the settings it made: rt_settings_default + samples
+    # (NewParallelRenderer's defaults, settings.go:3-25; seed 1)
+    import oracle
+
+    st = rtgo.default_settings()
+    st.samples = spp
+    assert st.seed == 1
+    _, ref_rgba, _ = oracle.render(rtgo.Scene.from_json_text(open(MARSHALLED).read()), w, h, st)
+    assert ref_rgba.any()
+    assert got.tobytes() == ref_rgba.tobytes()
     r = rtgo.ParallelRenderer()
     r.settings = make_settings(rtgo, {"samples": spp}, seed=1)
     want = r.render(rtgo.Scene.from_json_text(all_materials_json()), w, h)
