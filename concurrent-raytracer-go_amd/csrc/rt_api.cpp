@@ -183,6 +183,12 @@ struct rt_context {
   // a multi-rank renderer's frame deadline (steady_now_s() clock; <= 0:
   // none), set by rt_renderer_render for the frame (context_set_deadline)
   double deadline = 0;
+  // tail helpers: control block | queue | ready flags | rows
+  // | row bits | row headers, laid out for tail_spp samples per pixel
+  char* d_tail = nullptr;
+  size_t tail_bytes = 0;
+  int32_t tail_cap = 0, tail_spp = -1;
+  uint32_t tail_epoch = 0;
 };
 
 // Events for kernel classes [first, last] of one launch sequence: ev[k] opens
@@ -311,7 +317,8 @@ int rt_context_set_tuning(rt_context* c, const rt_tuning* t) {
   }
   if (t->pilot_depth < 0 || t->split_samples < 0 || t->split_samples > 64 || t->bvh_leaf < 0 || t->bvh_leaf > 7 || t->bvh_bins < 0 || t->block_work < 0 || t->block_samples < 0 ||
       t->wf_paths < 0 || t->wf_chunk < 0 || t->wf_trav_block < 0 || t->wf_trav_block > 1024 || t->wf_trav_wgs < 0 ||
-      t->wf_list_tries < 0 || t->wf_list_tries > 64) {
+      t->wf_list_tries < 0 || t->wf_list_tries > 64 || t->tail_helpers < -1 || t->tail_helpers > 4096 ||
+      t->tail_paths < 0 || t->tail_paths > 64 || t->tail_depth < 0) {
     set_error("tuning value out of range");
     return RT_E_INVALID;
   }
@@ -443,7 +450,7 @@ void rt_context_destroy(rt_context* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (void* p : {(void*)c->d_scene, (void*)c->d_counts, (void*)c->d_blocks, (void*)c->d_pilot, c->d_acc,
                   (void*)c->d_meas, (void*)c->d_split, (void*)c->d_sched, (void*)c->d_part, c->wf_mem, c->wf_rad,
-                  (void*)c->wf_ctl})
+                  (void*)c->wf_ctl, (void*)c->d_tail})
     dev_free(p);
   host_free(c->h_stage);
   host_free(c->h_small);
@@ -637,6 +644,52 @@ static void base_params(const rt_context* c, int w, int h, const rt_settings* st
   p.stage_bytes = c->tun.stage ? c->stage_bytes : 0;
   p.stack_off = (p.stage_bytes + 15) & ~15;
   p.stack_depth = std::max(1, f.bvh_depth);
+}
+
+// Tail helpers for a megakernel launch of p: the product
+// instantiation on a staged linear-scan scene with shadow-cone masks (what
+// solo_path needs), one sample pass, no sky, not measuring.  Lays out the
+// context's queue and rows for p.spp_total samples per pixel (the control
+// block and ready flags zeroed once per layout: each launch's last helper
+// leaves the control block zeroed, and a ready flag holds its launch's epoch)
+// and sets p's tail fields; leaves them null (off) otherwise.
+static int setup_tail(rt_context* c, KParams* p, hipStream_t s) {
+  const rt_tuning& tn = c->tun;
+  p->tail = nullptr;
+  const bool masks = !p->use_bvh && p->ns <= 64 && p->nt <= 64;
+  if (tn.tail_helpers < 0 || p->stage_bytes <= 0 || !masks || p->sky || p->work_max || p->counts || p->acc_mode != 0 ||
+      p->spp_total < 1 || p->spp_total > kMaxBlockSamples || p->max_depth < 2 || !p->recursive)
+    return RT_OK;
+  const int spp = p->spp_total, bw = (spp + 31) / 32;
+  const size_t per = (size_t)spp * 24 + (size_t)bw * 4 + sizeof(TailPath) + sizeof(TailRow) + 4;
+  // one queue entry and at most one row per exported path; 64 MB at most
+  const int cap = (int)std::max<size_t>(1024, std::min<size_t>(16384, (size_t(64) << 20) / per));
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t o_q = al(sizeof(TailCtl)), o_ready = o_q + al((size_t)cap * sizeof(TailPath));
+  const size_t o_rows = o_ready + al((size_t)cap * 4), o_bits = o_rows + al((size_t)cap * spp * 24);
+  const size_t o_hdr = o_bits + al((size_t)cap * bw * 4), total = o_hdr + al((size_t)cap * sizeof(TailRow));
+  if (c->tail_spp != spp || c->tail_cap != cap) {
+    int rc = grow(c, &c->d_tail, &c->tail_bytes, total);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(c->d_tail, 0, o_rows, s));  // control block, queue, ready flags
+    c->tail_spp = spp;
+    c->tail_cap = cap;
+    c->tail_epoch = 0;
+  }
+  if (++c->tail_epoch == 0) c->tail_epoch = 1;
+  char* b = c->d_tail;
+  p->tail = (TailCtl*)b;
+  p->tail_q = (TailPath*)(b + o_q);
+  p->tail_ready = (unsigned int*)(b + o_ready);
+  p->tail_rows = (double*)(b + o_rows);
+  p->tail_bits = (uint32_t*)(b + o_bits);
+  p->tail_hdr = (TailRow*)(b + o_hdr);
+  p->tail_cap = cap;
+  p->tail_helpers = tn.tail_helpers > 0 ? tn.tail_helpers : 256;
+  p->tail_kmax = tn.tail_paths > 0 ? tn.tail_paths : 4;
+  p->tail_dmin = tn.tail_depth > 0 ? tn.tail_depth : 2;
+  p->tail_epoch = c->tail_epoch;
+  return RT_OK;
 }
 
 // The scheduler's inputs for `tiles` (host masks and costs uploaded into
@@ -1215,6 +1268,10 @@ static int render_one(rt_context* c, int32_t w, int32_t h, const rt_settings* st
       rc = render_wavefront(c, p, st, s, counts != nullptr);
       if (rc) return rc;
     } else {
+      if (npass == 1 && !counts) {
+        rc = setup_tail(c, &p, s);
+        if (rc) return rc;
+      }
       int e = launch_render(p, counts != nullptr, s);
       if (e != hipSuccess) {
         set_error(std::string("render launch failed: ") + hipGetErrorString((hipError_t)e));
@@ -1561,6 +1618,8 @@ int rt_context_render_frames_async(rt_context* c, int32_t w, int32_t h, const rt
     p.frame_rgba[f] = d_rgba ? d_rgba[f] : nullptr;
   }
   p.num_wgs = p.num_blocks * nframes;
+  rc = setup_tail(c, &p, s);
+  if (rc) return rc;
   HIP_TRY(hipEventRecord(c->ev0, s));
   const int e = launch_render(p, false, s);
   if (e != hipSuccess) {
@@ -1584,6 +1643,39 @@ int rt_context_get_stats(const rt_context* c, rt_context_stats* out) {
   *out = c->stats;
   out->blocks = c->num_blocks;
   out->split_pixels = c->nsplit;
+  out->tail_exported = out->tail_errors = 0;
+  if (c->d_tail) {
+    rt_context* m = const_cast<rt_context*>(c);
+    int rc = quiesce(m);
+    if (rc) return rc;
+    TailCtl h;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpy(&h, c->d_tail, sizeof h, hipMemcpyDeviceToHost));
+    out->tail_exported = h.exported;
+    out->tail_errors = h.err;
+  }
+  return RT_OK;
+}
+
+int rt_context_tail_debug(const rt_context* c, uint64_t out[6]) {
+  if (!c || !out) {
+    set_error("context or out is NULL");
+    return RT_E_INVALID;
+  }
+  for (int i = 0; i < 6; ++i) out[i] = 0;
+  if (!c->d_tail) return RT_OK;
+  rt_context* m = const_cast<rt_context*>(c);
+  int rc = quiesce(m);
+  if (rc) return rc;
+  TailCtl h;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpy(&h, c->d_tail, sizeof h, hipMemcpyDeviceToHost));
+  out[0] = h.exported;
+  out[1] = h.paths_done;
+  out[2] = h.solo_ticks;
+  out[3] = h.export_ticks;
+  out[4] = h.helper_ticks;
+  out[5] = h.err;
   return RT_OK;
 }
 

@@ -138,6 +138,58 @@ constexpr int kGroupSoft = 2, kGroupExtend = 3, kGroupHard = 4;
 // the scene's actual depth (10k spheres: 15 levels).
 constexpr int kStack = 40;
 
+// ---- tail helpers: a launch's long paths handed to idle waves
+// When a block's wave has started every entry of its hit list and only a
+// few paths are left (at most tail_kmax, each at least tail_dmin bounces
+// deep), it EXPORTS them: each path's state goes to a queue, and one of
+// tail_helpers extra one-wave workgroups at the end of the grid runs it to
+// its end with the whole wave (solo_path: ~5 us per bounce against ~9-17
+// us for a few paths sharing a wave).  Its radiance goes to a per-sample row
+// of its pixel (the block's own pixels: a dynamic row; split pixels: the
+// split row), and the last contributor of a pixel -- the block or a helper --
+// sums the row in sample order and writes the pixel, so the image is the
+// same bit for bit.  Main blocks never wait for a helper; helpers leave when
+// every main block is done and the queue is empty, so the launch always
+// drains.
+constexpr int kTailShards = 64;
+struct TailCtl {
+  unsigned int tail;          // queue entries reserved
+  unsigned int head;          // queue entries taken by helpers
+  unsigned int unused0;
+  unsigned int inflight;      // exported paths not yet finished
+  unsigned int rows_used;     // dynamic rows allocated
+  unsigned int helpers_live;  // helpers started and not yet gone
+  unsigned int helpers_gone;  // helpers finished (the last one zeroes this block for the next launch)
+  unsigned int err;           // a helper gave up waiting (never expected)
+  unsigned int exported;      // paths exported (statistics, since the layout)
+  // statistics since the layout (s_memrealtime ticks, 100 MHz): helpers'
+  // time running paths, exporting waves' time in the export, helper lifetimes
+  unsigned int solo_ticks, export_ticks, helper_ticks, paths_done;
+  unsigned int pad[3];
+  // main workgroups finished, sharded (block b adds to shard b % kTailShards,
+  // 128 B apart): one counter took every block's add and serialized them
+  unsigned int done[kTailShards * 32];
+};
+// one exported path (its state after `depth` bounces, renderer.go:165-227)
+struct TailPath {
+  double o[3], d[3], T[3], L[3];
+  uint64_t rng, skey;
+  int32_t depth, sample;   // bounces so far; its sample within the destination row
+  int32_t kind, row;       // kTailRow: dynamic row `row`; kTailSplit: split slot index `row`
+  int32_t nsub, frame;     // split pixel: its sub-blocks; the frame of the launch
+  int64_t oi;              // output pixel index (layout-resolved, as the epilogue writes it)
+};
+// the header of a dynamic row: its pixel's running sum over the samples
+// before k0 (summed by the block), and who still owes a sample
+struct TailRow {
+  double prefix[3];
+  int32_t counter;         // contributors still to finish: the block (1) + its exported paths
+  int32_t k0;              // first sample held by the row
+  int32_t frame, _pad;
+  int64_t oi;
+};
+constexpr int kTailRow = 1, kTailSplit = 2;
+
 struct KParams {
   const DSphere* spheres;
   const DTri* tris;
@@ -195,6 +247,17 @@ struct KParams {
   uint64_t frame_key[kMaxFrames];
   float* frame_lin[kMaxFrames];
   uint8_t* frame_rgba[kMaxFrames];
+  // tail helpers (null tail: off): the control block, the queue and its
+  // ready flags (== tail_epoch when written), the dynamic rows ([row][spp][3]
+  // radiance, [row][(spp+31)/32] hit bits, headers); tail_cap entries and rows
+  TailCtl* tail;
+  TailPath* tail_q;
+  unsigned int* tail_ready;
+  double* tail_rows;
+  uint32_t* tail_bits;
+  TailRow* tail_hdr;
+  int32_t tail_cap, tail_helpers, tail_kmax, tail_dmin;
+  uint32_t tail_epoch, _tpad;
 };
 
 // Enqueue the render kernel; returns hipError_t as int.

@@ -773,7 +773,7 @@ __shared__ unsigned long long solo_clk[16];
 // variant fault on its first parameter load -- so the kernel passes it in
 // (`karg`) and every per-bounce read launders that copy (launder()).
 #ifndef RT_SOLO_CALL
-#define RT_SOLO_CALL 1
+#define RT_SOLO_CALL 0
 #endif
 #if RT_SOLO_CALL
 #define RT_SOLO_ATTR __noinline__
@@ -1098,6 +1098,243 @@ constexpr int kRound = 128;  // list entries shaded per round (LDS radiance slot
 #endif
 constexpr int kRefill2Min = RT_REFILL2_MIN;
 
+// ---- tail helpers (TailCtl in rt_internal.h)
+// Device-scope hand-offs on MI355X (MI355X_MICROARCH.md, inter-workgroup
+// visibility): the 8 XCDs' L2 caches are not coherent with each other, and an
+// agent-scope release fence writes back the whole XCD L2's dirty lines
+// (buffer_wbl2: microseconds, and tens of them when many waves fence at
+// once).  The tail protocol hands its data over WITHOUT fences, in the
+// guide's "8-B agent atomics both sides" form: every byte a helper or a
+// block hands over (a queued path, a row's samples, bits and header) is
+// stored write-through with relaxed agent-scope atomic stores (st_wt*, sc1),
+// the storing wave drains them (s_waitcnt vmcnt(0)), and only then stores
+// the flag or adds to the counter that signals them; the consumer polls the
+// flag or takes the counter's returned value and reads every handed-over
+// byte with relaxed agent-scope atomic loads (ld_wt*, sc1).  Counters that
+// every block touches are sharded (TailCtl.done), and the export's gate
+// reads before it adds.  (Measured on the headline frame: a __threadfence
+// at every block's end, or 2 atomics per draining iteration on one line,
+// made the launch 2-3x slower.)
+__device__ __forceinline__ unsigned int ld_rlx(const unsigned int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wt_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void st_wt64(void* p, uint64_t v) {
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt32(void* p, uint32_t v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wtd(double* p, double v) { st_wt64(p, __builtin_bit_cast(uint64_t, v)); }
+__device__ __forceinline__ uint64_t ld_wt64(const void* p) {
+  return __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_wt32(const void* p) {
+  return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wtd(const double* p) { return __builtin_bit_cast(double, ld_wt64(p)); }
+// One pixel's mean, tone map (renderer.go:348-367) and write, as the epilogue
+// writes it: sum / spp (DivScalar(float64(samples))), float3 + RGBA8.
+__device__ __forceinline__ void store_pixel(KArg k, int fr, size_t oi, double sx, double sy, double sz) {
+  const double n = (double)k->spp_total;
+  const double mx = sx / n, my = sy / n, mz = sz / n;
+  float* const ol = k->frame_lin[fr];
+  uint8_t* const orgba = k->frame_rgba[fr];
+  if (ol) {
+    ol[oi * 3 + 0] = (float)mx;
+    ol[oi * 3 + 1] = (float)my;
+    ol[oi * 3 + 2] = (float)mz;
+  }
+  if (orgba) *reinterpret_cast<uint32_t*>(orgba + oi * 4) = tonemap_rgba8(mx, my, mz);
+}
+// Samples [k0, n) of a per-sample radiance row added to `a` (lanes 0..2:
+// channel `lane`) in sample order, a sample whose hit bit is clear adding +0
+// (a miss: traceRay's black, renderer.go:170-173, summed as tracePixel sums,
+// renderer.go:150-163).  The whole wave loads each chunk of kRound samples
+// into `buf` (LDS); lanes 0..2 then add it in order.
+// (kWT: the row was handed over write-through: every load of it is sc1)
+template <bool kWT>
+__device__ __forceinline__ double row_sum(double (*buf)[3], const double* row, const uint32_t* hw, int k0, int n,
+                                          double a, int lane) {
+  for (int c0 = k0; c0 < n; c0 += kRound) {
+    const int cn = min(kRound, n - c0);
+    for (int i = lane; i < cn; i += 64) {
+      const int s = c0 + i;
+      const bool hit = ((kWT ? ld_wt32(hw + (s >> 5)) : hw[s >> 5]) >> (s & 31)) & 1u;
+      buf[i][0] = hit ? (kWT ? ld_wtd(row + 3 * s + 0) : row[3 * s + 0]) : 0.0;
+      buf[i][1] = hit ? (kWT ? ld_wtd(row + 3 * s + 1) : row[3 * s + 1]) : 0.0;
+      buf[i][2] = hit ? (kWT ? ld_wtd(row + 3 * s + 2) : row[3 * s + 2]) : 0.0;
+    }
+    __syncthreads();
+    if (lane < 3)
+      for (int i = 0; i < cn; ++i) a += buf[i][lane];
+    __syncthreads();
+  }
+  return a;
+}
+
+// A tail helper: one of the one-wave workgroups past the grid's main blocks.
+// It takes exported paths off the queue and runs each to its end with the
+// whole wave (solo_path), delivers its radiance to the row of its pixel and,
+// when it is the pixel's last contributor, sums the row and writes the
+// pixel.  It leaves once every main block has finished and the queue is
+// empty (main blocks never wait for a helper, so that always comes); the last
+// helper to leave zeroes the control block for the context's next launch.
+__device__ __forceinline__ void tail_helper(KArg karg, int* stack, double (*buf)[3]) {
+  const int lane = (int)(threadIdx.x & 63);
+  const KArg k0 = launder(karg);
+  TailCtl* const ctl = k0->tail;
+  const unsigned int epoch = k0->tail_epoch, cap = (unsigned int)k0->tail_cap, main_wgs = (unsigned int)k0->num_wgs;
+  if (lane == 0) atomicAdd(&ctl->helpers_live, 1u);
+  const unsigned long long t_born = __builtin_amdgcn_s_memrealtime();
+  unsigned long long t_idle = t_born;
+#ifdef RT_WG_TIMING
+  unsigned long long dbg_first = 0, dbg_paths = 0, dbg_solo = 0;
+#endif
+  for (;;) {
+    int idx = -1;
+    if (lane == 0) {
+      for (;;) {
+        const unsigned int h = ld_rlx(&ctl->head), t = min(ld_rlx(&ctl->tail), cap);
+        if (h >= t) break;
+        if (atomicCAS(&ctl->head, h, h + 1u) == h) {
+          idx = (int)h;
+          break;
+        }
+      }
+    }
+    idx = __builtin_amdgcn_readfirstlane(idx);
+    if (idx < 0) {
+      // every main block finished (the sharded counters, one per lane)?
+      // Then nothing more can be queued: leave once the queue is empty
+      unsigned int dn = lane < kTailShards ? ld_rlx(&ctl->done[lane * 32]) : 0u;
+      for (int off = 32; off >= 1; off >>= 1) dn += __shfl_xor(dn, off);
+      if (__builtin_amdgcn_readfirstlane(dn) >= main_wgs) {
+        const unsigned int h = ld_rlx(&ctl->head), t = min(ld_rlx(&ctl->tail), cap);
+        if (__builtin_amdgcn_readfirstlane(h >= t ? 1 : 0)) break;
+        continue;
+      }
+      // (a bound that is never expected to bite: main blocks are at most a
+      // 1024-sample block each; a stuck helper must not hang the device)
+      if (__builtin_amdgcn_s_memrealtime() - t_idle > 1000000000ull) {  // 10 s at 100 MHz
+        if (lane == 0) atomicOr(&ctl->err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(16);
+      continue;
+    }
+    // the entry was reserved by a block that writes it at once
+    bool ready = true;
+    for (const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+         __hip_atomic_load(&k0->tail_ready[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch;) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // (never expected: 10 s)
+        ready = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (!__builtin_amdgcn_readfirstlane(ready ? 1 : 0)) {
+      if (lane == 0) atomicOr(&ctl->err, 2u);
+      break;
+    }
+    // the record: written through by its exporter, drained before the flag
+    const unsigned long long t_path = __builtin_amdgcn_s_memrealtime();
+    const TailPath* q = k0->tail_q + idx;
+    const d3 o = mk(ld_wtd(q->o), ld_wtd(q->o + 1), ld_wtd(q->o + 2)), d = mk(ld_wtd(q->d), ld_wtd(q->d + 1), ld_wtd(q->d + 2));
+    const d3 T = mk(ld_wtd(q->T), ld_wtd(q->T + 1), ld_wtd(q->T + 2)), L0 = mk(ld_wtd(q->L), ld_wtd(q->L + 1), ld_wtd(q->L + 2));
+    const uint64_t rx = ld_wt64(&q->rng), sk = ld_wt64(&q->skey);
+    const int depth = (int)ld_wt32(&q->depth), sample = (int)ld_wt32(&q->sample), kind = (int)ld_wt32(&q->kind),
+              row = (int)ld_wt32(&q->row), nsub = (int)ld_wt32(&q->nsub), fr = (int)ld_wt32(&q->frame);
+    const int64_t oi = (int64_t)ld_wt64(&q->oi);
+    const d3 L = solo_path<false>(karg, 0, o, d, T, L0, rx, depth, sk, stack);
+    const KArg k = launder(karg);
+#ifdef RT_WG_TIMING
+    if (!dbg_first) dbg_first = t_path;
+    dbg_paths += 1;
+    dbg_solo += __builtin_amdgcn_s_memrealtime() - t_path;
+#endif
+    const int spp = k->spp_total, bw = (spp + 31) >> 5;
+    int last = 0;
+    if (lane == 0) {
+      atomicAdd(&ctl->solo_ticks, (unsigned int)(__builtin_amdgcn_s_memrealtime() - t_path));
+      atomicAdd(&ctl->paths_done, 1u);
+      // the sample, written through and drained before the counter
+      if (kind == kTailRow) {
+        double* r = k->tail_rows + ((size_t)row * spp + sample) * 3;
+        st_wtd(r, L.x);
+        st_wtd(r + 1, L.y);
+        st_wtd(r + 2, L.z);
+        atomicOr(k->tail_bits + (size_t)row * bw + (sample >> 5), 1u << (sample & 31));
+        wt_drain();
+        last = atomicSub(&k->tail_hdr[row].counter, 1) == 1 ? 1 : 0;
+      } else {
+        double* r = k->split_rad + ((size_t)row * spp + sample) * 3;
+        st_wtd(r, L.x);
+        st_wtd(r + 1, L.y);
+        st_wtd(r + 2, L.z);
+        atomicOr(k->split_hits + (size_t)row * bw + (sample >> 5), 1u << (sample & 31));
+        wt_drain();
+        last = atomicAdd(&k->split_cnt[row], 1) == nsub - 1 ? 1 : 0;
+      }
+      atomicSub(&ctl->inflight, 1u);
+    }
+    last = __builtin_amdgcn_readfirstlane(last);
+    if (last) {
+      // the pixel's last contributor: its row in sample order, then the pixel
+      // (every byte of the row read sc1: written through or by atomics)
+      double a;
+      int pfr = fr;
+      size_t poi = (size_t)oi;
+      if (kind == kTailRow) {
+        const TailRow* hd = k->tail_hdr + row;
+        a = lane < 3 ? ld_wtd(hd->prefix + lane) : 0.0;
+        a = row_sum<true>(buf, k->tail_rows + (size_t)row * spp * 3, k->tail_bits + (size_t)row * bw,
+                          (int)ld_wt32(&hd->k0), spp, a, lane);
+        pfr = (int)ld_wt32(&hd->frame);
+        poi = (size_t)ld_wt64(&hd->oi);
+      } else {
+        uint32_t* hw = k->split_hits + (size_t)row * bw;
+        a = row_sum<true>(buf, k->split_rad + (size_t)row * spp * 3, hw, 0, spp, 0.0, lane);
+        // the slot's hit bits and counter are left zeroed for the next launch
+        for (int i = lane; i < bw; i += 64) hw[i] = 0u;
+        if (lane == 0) k->split_cnt[row] = 0;
+      }
+      const double sx = rld(a, 0), sy = rld(a, 1), sz = rld(a, 2);
+      if (lane == 0) store_pixel(k, pfr, poi, sx, sy, sz);
+    }
+    t_idle = __builtin_amdgcn_s_memrealtime();
+  }
+  int gone = 0;
+#ifdef RT_WG_TIMING
+  if (k0->dbg && lane == 0) {  // a helper's record: start, first path, end, paths, their ticks; [14] = -1
+    unsigned long long* r = k0->dbg + (size_t)blockIdx.x * kDbgStride;
+    r[0] = t_born;
+    r[1] = dbg_first;
+    r[2] = __builtin_amdgcn_s_memrealtime();
+    r[3] = dbg_solo;
+    r[7] = dbg_paths;
+    r[14] = ~0ull;
+  }
+#endif
+  if (lane == 0) {
+    atomicAdd(&ctl->helper_ticks, (unsigned int)(__builtin_amdgcn_s_memrealtime() - t_born));
+    atomicSub(&ctl->helpers_live, 1u);
+    gone = (int)atomicAdd(&ctl->helpers_gone, 1u);
+  }
+  if (__builtin_amdgcn_readfirstlane(gone) + 1 == k0->tail_helpers) {
+    // every helper and every main block is done: ready for the next launch
+    if (lane < kTailShards) ctl->done[lane * 32] = 0u;
+    if (lane == 0) {
+      ctl->tail = 0;
+      ctl->head = 0;
+      ctl->inflight = 0;
+      ctl->rows_used = 0;
+      ctl->helpers_live = 0;
+      ctl->helpers_gone = 0;
+    }
+  }
+}
+
 template <bool kCount, bool kStage, bool kPilot, bool kSky>
 __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KParams pk) {
   __shared__ uint32_t hbits[kMaxBlockSamples / 32];  // hit samples of the block
@@ -1107,9 +1344,30 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   __shared__ uint8_t lpix[64];                       // phase 1: the block's live pixels
   __shared__ uint64_t skey[64];                      // per lane: its path's soft-shadow key (rt_soft_key, spec v4)
   // dynamic LDS (dyn_lds): [staged scene prefix (kStage)][BVH stack (stack_depth x 64 ints)]
+  // tail helpers: the product instantiation exports a
+  // block's last few long paths to the helpers past its main blocks
+  constexpr bool kTail = kStage && !kCount && !kPilot && !kSky;
 
   const int lane = threadIdx.x;
   int* stack = reinterpret_cast<int*>(dyn_lds + pk.stack_off) + lane;
+  if constexpr (kTail) {
+    if ((int)blockIdx.x >= pk.num_wgs) {  // a tail helper (launch_render adds them only with pk.tail set)
+      const uint4* __restrict__ src = reinterpret_cast<const uint4*>(pk.stage_src);
+      uint4* dst = reinterpret_cast<uint4*>(dyn_lds);
+      for (int i = lane; i < pk.stage_bytes / 16; i += 64) dst[i] = src[i];
+      __syncthreads();
+      tail_helper(fresh(), stack, slot);
+      return;
+    }
+  }
+  // a row pixel (tail helpers): its dynamic row and first row sample (-1: none)
+  __shared__ int prow[kTail ? 64 : 1];
+  __shared__ short pk0[kTail ? 64 : 1];
+  __shared__ uint32_t xm[kTail ? kRound / 32 : 1];  // ring slots whose path was exported
+  if constexpr (kTail) {
+    prow[lane] = -1;
+    if (lane < kRound / 32) xm[lane] = 0u;
+  }
   const BlockLoc blk = block_loc(fresh(), block_of(fresh()));
   // a black block (up to 64 pixels x spp samples) sets no hit bits
   const int nwords = blk.black ? 0 : (blk.np * blk.ns + 31) >> 5;
@@ -1296,9 +1554,12 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       for (int e = a + lane; e < b; e += 64) {
         const int s = blk.s0 + entry_id(e);  // one pixel: id = sample - s0
         const int q = e & (kRound - 1);
-        row[3 * s + 0] = slot[q][0];
-        row[3 * s + 1] = slot[q][1];
-        row[3 * s + 2] = slot[q][2];
+        if constexpr (kTail) {
+          if ((xm[q >> 5] >> (q & 31)) & 1u) continue;  // exported: its helper writes the sample
+        }
+        st_wtd(row + 3 * s + 0, slot[q][0]);  // (written through: read sc1 by the pixel's last sub-block)
+        st_wtd(row + 3 * s + 1, slot[q][1]);
+        st_wtd(row + 3 * s + 2, slot[q][2]);
         atomicOr(hw + (s >> 5), 1u << (s & 31));
       }
     } else {
@@ -1309,7 +1570,37 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
         int e1 = (a1 >> 5) < nwords ? hoff[a1 >> 5] + __popc(hbits[a1 >> 5] & ((1u << (a1 & 31)) - 1u)) : nh;
         e0 = max(e0, a);
         e1 = min(e1, b);
-        if (e0 < e1) {
+        bool rowed = false;
+        if constexpr (kTail) rowed = prow[lane] >= 0;
+        if (rowed) {
+          // a pixel with exported paths (tail helpers): samples before its
+          // first exported one go to its running sum as below, the later
+          // ones (the exported ones aside: their helpers write them) to its
+          // row, which the pixel's last contributor sums in order
+          KArg k = fresh();
+          const int r = prow[lane], k0 = pk0[lane], bw = (k->spp_total + 31) >> 5;
+          double* row = k->tail_rows + (size_t)r * k->spp_total * 3;
+          uint32_t* hw = k->tail_bits + (size_t)r * bw;
+          double ax = psum[lane][0], ay = psum[lane][1], az = psum[lane][2];
+          for (int e = e0; e < e1; ++e) {
+            const int q = e & (kRound - 1);
+            if ((xm[q >> 5] >> (q & 31)) & 1u) continue;
+            const int sl = entry_id(e) - a0;
+            if (sl < k0) {
+              ax += slot[q][0];
+              ay += slot[q][1];
+              az += slot[q][2];
+            } else {  // (written through: the row's last contributor reads it sc1)
+              st_wtd(row + 3 * sl + 0, slot[q][0]);
+              st_wtd(row + 3 * sl + 1, slot[q][1]);
+              st_wtd(row + 3 * sl + 2, slot[q][2]);
+              atomicOr(hw + (sl >> 5), 1u << (sl & 31));
+            }
+          }
+          psum[lane][0] = ax;
+          psum[lane][1] = ay;
+          psum[lane][2] = az;
+        } else if (e0 < e1) {
           double ax = psum[lane][0], ay = psum[lane][1], az = psum[lane][2];
           for (int e = e0; e < e1; ++e) {
             const int q = e & (kRound - 1);
@@ -1423,6 +1714,107 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
             fresh()->dbg[(size_t)blockIdx.x * kDbgStride + 16 + dbg_iter / 4] = __builtin_amdgcn_s_memrealtime();
           ts0 = __builtin_amdgcn_s_memtime();
 #endif
+          if constexpr (kTail) {
+            // Tail helpers: every entry has started and at
+            // most tail_kmax paths are left, each tail_dmin bounces deep or
+            // more -- the block's drain.  Each goes to a helper wave (while
+            // one is free), which runs it alone at solo latency; its radiance
+            // reaches the pixel through the pixel's row (resolve_entries, the
+            // epilogue), the same sum in the same order.
+            if (next >= nh && fresh()->tail != nullptr) {
+              const unsigned long long am = __ballot(alive);
+              if (__popcll(am) <= fresh()->tail_kmax) {
+                for (unsigned long long em = __ballot(alive && depth >= fresh()->tail_dmin); em; em &= em - 1) {
+                  const int ow = __builtin_ctzll(em);
+                  const unsigned long long t_x = __builtin_amdgcn_s_memrealtime();
+                  KArg k = fresh();
+                  TailCtl* ctl = k->tail;
+                  int idx = -1;
+                  if (lane == 0 && ld_rlx(&ctl->inflight) < ld_rlx(&ctl->helpers_live)) {
+                    // a helper for it (inflight < live helpers: read before any add, so
+                    // draining waves do not hammer the line) and a queue entry
+                    if (atomicAdd(&ctl->inflight, 1u) < ld_rlx(&ctl->helpers_live)) {
+                      const unsigned int t = atomicAdd(&ctl->tail, 1u);
+                      if (t < (unsigned int)k->tail_cap) idx = (int)t;  // (entries past the cap are never taken)
+                    }
+                    if (idx < 0) atomicSub(&ctl->inflight, 1u);
+                  }
+                  idx = __builtin_amdgcn_readfirstlane(idx);
+                  // (all the handed-over bytes below are written through: st_wt*)
+                  if (idx < 0) break;  // (no helper free: the paths stay here)
+                  const int e = (int)rl32((uint32_t)entry, ow);
+                  const BlockLoc loc = block_loc(k, block_of(k));
+                  const int id = entry_id(e), ns = loc.ns;
+                  const int p = id / ns, sl = id - p * ns;
+                  const int tp = loc.p0 + p;
+                  const int px = loc.tx * 32 + (tp & 31), py = loc.ty * 32 + (tp >> 5);
+                  const int64_t oi = k->layout == RT_LAYOUT_IMAGE ? (int64_t)py * k->W + px
+                                                                  : (int64_t)loc.lt * 1024 + tp;
+                  int kind, row, sample;
+                  if (loc.slot >= 0) {  // a split pixel: its split row (its counter owes one more finisher)
+                    kind = kTailSplit;
+                    row = (int)split_index(k, loc.slot);
+                    sample = loc.s0 + sl;
+                    if (lane == 0) atomicSub(&k->split_cnt[row], 1);
+                  } else {
+                    kind = kTailRow;
+                    sample = sl;
+                    int r = prow[p];
+                    if (r < 0) {  // the pixel's dynamic row (one row per export at most: rows_used < cap)
+                      if (lane == 0) r = (int)atomicAdd(&ctl->rows_used, 1u);
+                      r = __builtin_amdgcn_readfirstlane(r);
+                      const int bw = (k->spp_total + 31) >> 5;
+                      for (int w = lane; w < bw; w += 64) st_wt32(k->tail_bits + (size_t)r * bw + w, 0u);
+                      if (lane == 0) {
+                        TailRow* hd = k->tail_hdr + r;
+                        st_wt32(&hd->counter, 2u);  // the block's own share (given back in its epilogue) + this path
+                        st_wt32(&hd->k0, (uint32_t)sl);
+                        st_wt32(&hd->frame, (uint32_t)frame_of(k));
+                        st_wt64(&hd->oi, (uint64_t)oi);
+                        prow[p] = r;
+                        pk0[p] = (short)sl;
+                      }
+                    } else if (lane == 0) {
+                      pk0[p] = (short)min((int)pk0[p], sl);
+                      atomicAdd(&k->tail_hdr[r].counter, 1);  // one more path owes the row a sample
+                    }
+                    row = r;
+                  }
+                  if (lane == ow) {
+                    TailPath* q = k->tail_q + idx;
+                    const int qs = e & (kRound - 1);
+                    st_wtd(q->o, o.x); st_wtd(q->o + 1, o.y); st_wtd(q->o + 2, o.z);
+                    st_wtd(q->d, d.x); st_wtd(q->d + 1, d.y); st_wtd(q->d + 2, d.z);
+                    st_wtd(q->T, T.x); st_wtd(q->T + 1, T.y); st_wtd(q->T + 2, T.z);
+                    st_wtd(q->L, slot[qs][0]); st_wtd(q->L + 1, slot[qs][1]); st_wtd(q->L + 2, slot[qs][2]);
+                    st_wt64(&q->rng, rng.x);
+                    st_wt64(&q->skey, skey[ow]);
+                    st_wt32(&q->depth, (uint32_t)depth);
+                    st_wt32(&q->sample, (uint32_t)sample);
+                    st_wt32(&q->kind, (uint32_t)kind);
+                    st_wt32(&q->row, (uint32_t)row);
+                    st_wt32(&q->nsub, (uint32_t)loc.nsub);
+                    st_wt32(&q->frame, (uint32_t)frame_of(k));
+                    st_wt64(&q->oi, (uint64_t)oi);
+                    alive = false;
+                  }
+                  if (lane == 0) {
+                    const int qs = e & (kRound - 1);
+                    xm[qs >> 5] |= 1u << (qs & 31);
+                    atomicAdd(&ctl->exported, 1u);
+                  }
+                  wt_drain();  // every lane's write-through stores, then the flag
+                  if (lane == ow) __hip_atomic_store(&k->tail_ready[idx], k->tail_epoch, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                  if (lane == 0) atomicAdd(&ctl->export_ticks, (unsigned int)(__builtin_amdgcn_s_memrealtime() - t_x));
+                }
+                if (__ballot(alive) == 0) {  // every path left went to a helper
+                  outer = 2;
+                  break;
+                }
+              }
+            }
+          }
           if constexpr (kStage && !kCount && !kPilot && RT_SOLO) {
             // one path left (no free lane found an entry to start): the whole
             // wave runs it to its end (solo_path)
@@ -1722,33 +2114,22 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   if (blk.slot >= 0) {
     // a split pixel: the last of its sub-blocks to finish sums the hit
     // samples of the slot row in sample order (misses add +0) and writes it
-    __threadfence();
+    // (its row samples were written through: drained before the counter;
+    // the last sub-block reads the row sc1 -- no L2 write-back or
+    // invalidate, see the tail helpers' hand-off notes above)
+    wt_drain();
     int old = 0;
     if (lane3 == 0) old = atomicAdd(&k->split_cnt[split_index(k, blk.slot)], 1);
     old = __builtin_amdgcn_readfirstlane(old);
     resolve = old == blk.nsub - 1;
     if (resolve) {
-      __threadfence();
       const double* row = k->split_rad + split_index(k, blk.slot) * k->spp * 3;
       uint32_t* hw = k->split_hits + split_index(k, blk.slot) * ((k->spp + 31) >> 5);
       // chunks of kRound samples: all lanes load (in parallel) into the LDS
       // slots, misses as +0, then one lane per channel adds them in order
       double a = 0;  // (a later sample pass continues the running sum)
       if ((k->acc_mode & 1) && lane3 < 3) a = k->acc[((size_t)blk.lt * 1024 + blk.p0) * 3 + lane3];
-      for (int c0 = 0; c0 < k->spp; c0 += kRound) {
-        const int cn = min(kRound, k->spp - c0);
-        for (int i = lane3; i < cn; i += 64) {
-          const int s = c0 + i;
-          const bool hit = (hw[s >> 5] >> (s & 31)) & 1u;
-          slot[i][0] = hit ? row[3 * s + 0] : 0.0;
-          slot[i][1] = hit ? row[3 * s + 1] : 0.0;
-          slot[i][2] = hit ? row[3 * s + 2] : 0.0;
-        }
-        __syncthreads();
-        if (lane3 < 3)
-          for (int i = 0; i < cn; ++i) a += slot[i][lane3];
-        __syncthreads();
-      }
+      a = row_sum<true>(slot, row, hw, 0, k->spp, a, lane3);
       if (lane3 < 3) psum[0][lane3] = a;
       // the slot's hit bits and counter are left zeroed for the next launch
       // (the host clears them only when it builds a schedule: no memset per frame)
@@ -1762,7 +2143,10 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     const int p = lane3;
     const int tp = loc.p0 + p;
     const int x = loc.tx * 32 + (tp & 31), y = loc.ty * 32 + (tp >> 5);
-    if ((k->acc_mode & 2) && p < loc.np && tp < 1024) {  // not the last sample pass: keep the running sum
+    bool rowed = false;  // (tail helpers: the pixel's row writes it, below)
+    if constexpr (kTail) rowed = prow[p] >= 0;
+    if (rowed) {
+    } else if ((k->acc_mode & 2) && p < loc.np && tp < 1024) {  // not the last sample pass: keep the running sum
       double* a = k->acc + ((size_t)loc.lt * 1024 + tp) * 3;
       a[0] = psum[p][0];
       a[1] = psum[p][1];
@@ -1781,6 +2165,32 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
       }
       if (orgba) {
         *reinterpret_cast<uint32_t*>(orgba + oi * 4) = tonemap_rgba8(mx, my, mz);
+      }
+    }
+  }
+  if constexpr (kTail) {
+    // pixels with exported paths: the block gives back its share of each
+    // row (the running sum of the samples before the row's first one), and
+    // the row's last contributor sums it and writes the pixel
+    if (k->tail != nullptr && blk.slot < 0) {
+      int last = 0;
+      if (prow[lane3] >= 0) {
+        TailRow* hd = k->tail_hdr + prow[lane3];
+        st_wtd(hd->prefix, psum[lane3][0]);
+        st_wtd(hd->prefix + 1, psum[lane3][1]);
+        st_wtd(hd->prefix + 2, psum[lane3][2]);
+        st_wt32(&hd->k0, (uint32_t)pk0[lane3]);
+      }
+      wt_drain();  // (the resolve's row samples too) before the counter
+      if (prow[lane3] >= 0) last = atomicSub(&k->tail_hdr[prow[lane3]].counter, 1) == 1 ? 1 : 0;
+      for (unsigned long long b = __ballot(last); b; b &= b - 1) {
+        const int r = prow[__builtin_ctzll(b)], spp = k->spp_total, bw = (spp + 31) >> 5;
+        const TailRow* hd = k->tail_hdr + r;
+        double a = lane3 < 3 ? ld_wtd(hd->prefix + lane3) : 0.0;
+        a = row_sum<true>(slot, k->tail_rows + (size_t)r * spp * 3, k->tail_bits + (size_t)r * bw, (int)ld_wt32(&hd->k0),
+                          spp, a, lane3);
+        const double sx = rld(a, 0), sy = rld(a, 1), sz = rld(a, 2);
+        if (lane3 == 0) store_pixel(k, (int)ld_wt32(&hd->frame), (size_t)ld_wt64(&hd->oi), sx, sy, sz);
       }
     }
   }
@@ -1820,6 +2230,13 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     r[43] = solo_clk[7];  // entries into solo_path
   }
 #endif
+  if constexpr (kTail) {
+    if (k->tail != nullptr) {
+      // this main block is done: it queues nothing more (no fence: its queue
+      // reservations were returning atomics, complete before this one)
+      if (lane3 == 0) atomicAdd(&k->tail->done[(blockIdx.x % kTailShards) * 32], 1u);
+    }
+  }
 }
 
 // Gathered shares [world][share_bytes] (each: [max_local][1024] float3, then
@@ -1944,7 +2361,11 @@ int launch_render(const KParams& pin, bool count, void* stream) {
   }
   const size_t shmem = render_shmem(p);
   const bool stage = p.stage_bytes > 0;
-  const dim3 g(p.num_wgs), b(64);
+  // tail helpers: only the product instantiation exports
+  // paths; tail_helpers one-wave workgroups follow its num_wgs main blocks
+  const bool tail = p.tail && stage && !count && !p.sky && !p.work_max && p.acc_mode == 0 && p.tail_helpers > 0;
+  if (!tail) p.tail = nullptr;
+  const dim3 g(p.num_wgs + (tail ? p.tail_helpers : 0)), b(64);
   // (the opted-in sky has instantiations of its own: its code would cost the
   // others registers; the pilot and the counting variant ignore it -- path
   // lengths and counts do not depend on what a miss returns)

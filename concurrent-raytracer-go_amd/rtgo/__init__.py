@@ -146,6 +146,10 @@ class Tuning(ctypes.Structure):
         ("split_depth", ctypes.c_int32),
         ("partition", ctypes.c_int32),
         ("wf_list_tries", ctypes.c_int32),
+        ("tail_helpers", ctypes.c_int32),
+        ("tail_paths", ctypes.c_int32),
+        ("tail_depth", ctypes.c_int32),
+        ("_tail_pad", ctypes.c_int32),
     ]
 
 
@@ -170,7 +174,8 @@ class ContextStats(ctypes.Structure):
     """rt_context_stats (rt_context_get_stats)."""
 
     _fields_ = [(n, ctypes.c_int64) for n in ("schedules_built", "measuring_frames", "frames", "launches",
-                                             "batched_launches", "blocks", "split_pixels")]
+                                             "batched_launches", "blocks", "split_pixels", "tail_exported",
+                                             "tail_errors")]
 
 
 COUNT_FIELDS = [
@@ -272,6 +277,7 @@ EXPORTED_SYMBOLS = [
     "rt_renderer_rank_seconds",
     "rt_renderer_num_ranks",
     "rt_debug_xlane_faults",
+    "rt_context_tail_debug",
     "rt_context_profile",
     "rt_context_kernel_seconds",
     "rt_context_render_frames_async",
@@ -369,6 +375,7 @@ def lib():
         "rt_renderer_rank_seconds": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int32]),
         "rt_renderer_num_ranks": (ctypes.c_int32, [vp]),
         "rt_debug_xlane_faults": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64)]),
+        "rt_context_tail_debug": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64)]),
         "rt_context_profile": (ctypes.c_int, [vp, i32]),
         "rt_context_render_frames_async": (
             ctypes.c_int,
@@ -743,6 +750,12 @@ class Context:
         n = (ctypes.c_int64 * len(WF_KERNELS))()
         _check(lib().rt_context_kernel_seconds(self._h, s, n))
         return {k: (s[i], int(n[i])) for i, k in enumerate(WF_KERNELS)}
+
+    def tail_debug(self) -> dict:
+        """rt_context_tail_debug: tail-helper counters since the layout (ticks at 100 MHz)."""
+        out = (ctypes.c_uint64 * 6)()
+        _check(lib().rt_context_tail_debug(self._h, out))
+        return dict(zip(("exported", "paths_done", "solo_ticks", "export_ticks", "helper_ticks", "err"), out))
 
     def stats(self) -> dict:
         """rt_context_get_stats: schedules built, measuring frames, frames, launches, batched launches;

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4  /* 4: rt_renderer_rank_seconds takes a capacity */
+#define RT_ABI_VERSION 5  /* 5: rt_tuning tail_* fields; 4: rt_renderer_rank_seconds takes a capacity */
 
 /* status codes */
 #define RT_OK 0
@@ -336,6 +336,13 @@ typedef struct {
                              scenes, strided for BVH scenes, whose frames have thousands of busy tiles) */
   int32_t wf_list_tries;  /* wavefront list test: rejection tries a listed cone's accepted-try mask covers
                              (1..64; 0: 64); later points continue the sequential loop (tests force it low) */
+  /* tail helpers (megakernel, staged scenes): a block's last
+   * few long paths are handed to extra one-wave workgroups at the end of the
+   * launch that run each alone, at the latency of a lone bounce */
+  int32_t tail_helpers;   /* helper workgroups per launch; 0: 256; -1: none (the paths stay in their blocks) */
+  int32_t tail_paths;     /* a block exports once at most this many paths are left; 0: 4 */
+  int32_t tail_depth;     /* ... each at least this many bounces deep; 0: 2 */
+  int32_t _tail_pad;
 } rt_tuning;
 #define RT_PARTITION_AUTO 0
 #define RT_PARTITION_STRIDED 1
@@ -384,8 +391,18 @@ int rt_context_render_frames_async(rt_context* ctx, int32_t width, int32_t heigh
 typedef struct {
   int64_t schedules_built, measuring_frames, frames, launches, batched_launches;
   int64_t blocks, split_pixels;  /* of the schedule last used: work blocks, pixels split over sub-blocks */
+  /* tail helpers (rt_tuning.tail_*): paths exported to them since the
+   * context's tail buffers were laid out, and a helper error word (0: none);
+   * reading them waits for the context's last render */
+  int64_t tail_exported, tail_errors;
 } rt_context_stats;
 int rt_context_get_stats(const rt_context* ctx, rt_context_stats* out);
+/* Debug (tail helpers), cumulative since the context's tail
+ * buffers were laid out: out[0] paths exported, [1] paths the helpers ran,
+ * [2] helpers' ticks running paths, [3] exporting waves' ticks in the export,
+ * [4] helpers' lifetime ticks, [5] error word (ticks: s_memrealtime, 100 MHz).
+ * Waits for the context's last render; all zero when no launch used helpers. */
+int rt_context_tail_debug(const rt_context* ctx, uint64_t out[6]);
 
 /* Packed share of one rank, as rt_comm_gather_tiles_async moves it:
  * [max_local_tiles * 1024 float3][max_local_tiles * 1024 RGBA8] = 16 B per

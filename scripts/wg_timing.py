@@ -52,6 +52,19 @@ WPG = int(os.environ.get("WG_WAVES", "1"))  # waves per workgroup of the kernel
 d = dbg.cpu().numpy().reshape(-1, WPG, 48)
 used = d[:, 0, 0] != 0
 d = d[used]
+# tail helpers write records of their own ([14] = -1)
+helper = d[:, 0, 14] == -1
+hd = d[helper]
+d = d[~helper]
+if len(hd):
+    t0h = d[:, :, 0].min()
+    hs = (hd[:, 0, 0] - t0h) / 100.0
+    he = (hd[:, 0, 2] - t0h) / 100.0
+    hf = np.where(hd[:, 0, 1] > 0, (hd[:, 0, 1] - t0h) / 100.0, np.nan)
+    print(f"tail helpers: {len(hd)}, start us p0/p50/p100 {hs.min():.1f}/{np.median(hs):.1f}/{hs.max():.1f}, "
+          f"end p0/p50/p100 {he.min():.1f}/{np.median(he):.1f}/{he.max():.1f}, first path p0/p50 "
+          f"{np.nanmin(hf) if np.isfinite(hf).any() else -1:.1f}/{np.nanmedian(hf) if np.isfinite(hf).any() else -1:.1f}, "
+          f"paths {int(hd[:, 0, 7].sum())}, solo us per path {hd[:, 0, 3].sum() / max(1, hd[:, 0, 7].sum()) / 100:.1f}")
 nwg = d.shape[0]
 t0 = d[:, :, 0].min()
 start = (d[:, :, 0] - t0) / 100.0  # s_memrealtime: 100 MHz -> microseconds
