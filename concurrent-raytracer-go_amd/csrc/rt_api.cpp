@@ -318,7 +318,8 @@ int rt_context_set_tuning(rt_context* c, const rt_tuning* t) {
   if (t->pilot_depth < 0 || t->split_samples < 0 || t->split_samples > 64 || t->bvh_leaf < 0 || t->bvh_leaf > 7 || t->bvh_bins < 0 || t->block_work < 0 || t->block_samples < 0 ||
       t->wf_paths < 0 || t->wf_chunk < 0 || t->wf_trav_block < 0 || t->wf_trav_block > 1024 || t->wf_trav_wgs < 0 ||
       t->wf_list_tries < 0 || t->wf_list_tries > 64 || t->tail_helpers < -1 || t->tail_helpers > 4096 ||
-      t->tail_paths < 0 || t->tail_paths > 64 || t->tail_depth < 0) {
+      t->tail_paths < 0 || t->tail_paths > 64 || t->tail_depth < 0 || t->tail_every < 0 || t->tail_every > 64 ||
+      t->tail_at < 0 || t->tail_at > 100) {
     set_error("tuning value out of range");
     return RT_E_INVALID;
   }
@@ -685,9 +686,14 @@ static int setup_tail(rt_context* c, KParams* p, hipStream_t s) {
   p->tail_bits = (uint32_t*)(b + o_bits);
   p->tail_hdr = (TailRow*)(b + o_hdr);
   p->tail_cap = cap;
-  p->tail_helpers = tn.tail_helpers > 0 ? tn.tail_helpers : 256;
+  p->tail_helpers = tn.tail_helpers > 0 ? tn.tail_helpers : 64;
   p->tail_kmax = tn.tail_paths > 0 ? tn.tail_paths : 4;
   p->tail_dmin = tn.tail_depth > 0 ? tn.tail_depth : 2;
+  int every = tn.tail_every > 0 ? tn.tail_every : 4, pow2 = 1;
+  while (pow2 < every && pow2 < 64) pow2 <<= 1;
+  p->tail_every_mask = pow2 - 1;
+  const int at = tn.tail_at > 0 ? std::min(tn.tail_at, 100) : 100;
+  p->tail_pos = (int32_t)((int64_t)p->num_wgs * at / 100);
   p->tail_epoch = c->tail_epoch;
   return RT_OK;
 }

@@ -515,12 +515,18 @@ __device__ __forceinline__ KArg fresh() {
   return k;
 }
 
+// This main workgroup's index: the grid's, less the tail helpers placed
+// before it (KParams.tail_pos; launch_render)
+__device__ __forceinline__ unsigned main_wg(KArg k) {
+  const unsigned b = blockIdx.x;
+  return (k->tail != nullptr && b >= (unsigned)k->tail_pos) ? b - (unsigned)k->tail_helpers : b;
+}
 // The launch's frame and block of this workgroup (KParams.nframes)
 __device__ __forceinline__ int frame_of(KArg k) {
-  return k->nframes > 1 ? (int)(blockIdx.x % (unsigned)k->nframes) : 0;
+  return k->nframes > 1 ? (int)(main_wg(k) % (unsigned)k->nframes) : 0;
 }
 __device__ __forceinline__ int block_of(KArg k) {
-  return k->nframes > 1 ? (int)(blockIdx.x / (unsigned)k->nframes) : (int)blockIdx.x;
+  return k->nframes > 1 ? (int)(main_wg(k) / (unsigned)k->nframes) : (int)main_wg(k);
 }
 // a split pixel's radiance row / hit-bit words / sub-block counter in this frame's copy
 __device__ __forceinline__ size_t split_index(KArg k, int slot) {
@@ -790,7 +796,7 @@ __device__ __forceinline__ KArg launder(KArg k) {
 }
 template <bool kSky>
 __device__ RT_SOLO_ATTR d3 solo_path(KArg karg, int ow, d3 o, d3 d, d3 T, d3 L, uint64_t rx, int depth,
-                                     uint64_t skey, int* stack) {
+                                     uint64_t skey, int* stack, int* dep_out = nullptr) {
   const int lane = (int)(threadIdx.x & 63);
   o = rl3(o, ow);
   d = rl3(d, ow);
@@ -820,7 +826,10 @@ __device__ RT_SOLO_ATTR d3 solo_path(KArg karg, int ow, d3 o, d3 d, d3 T, d3 L, 
   for (;;) {
     const Hot h = hot<true>(launder(karg));
     const Geo& g = h.g;
-    if (depth >= h.max_depth) return L;  // traceRay depth cut-off: contributes 0
+    if (depth >= h.max_depth) {  // traceRay depth cut-off: contributes 0
+      if (dep_out) *dep_out = depth;
+      return L;
+    }
 #ifdef RT_WG_TIMING
     solo_clk[6] += 1;
 #endif
@@ -830,6 +839,7 @@ __device__ RT_SOLO_ATTR d3 solo_path(KArg karg, int ow, d3 o, d3 d, d3 T, d3 L, 
     SOLO_T(0);
     if (!found) {  // miss -> black (or the opted-in sky)
       if constexpr (kSky) L = L + mul(T, sky_color(launder(karg)->sky, d));
+      if (dep_out) *dep_out = depth + 1;
       return L;
     }
     d3 P, N;
@@ -1056,9 +1066,15 @@ __device__ RT_SOLO_ATTR d3 solo_path(KArg karg, int ow, d3 o, d3 d, d3 T, d3 L, 
     const d3 E = ld3(m->emit);
     const Scat sc = scatter<false>(m, d, N, front, rng, c);
     SOLO_T(5);
-    if (!sc.ok) return L + mul(T, E + D);
+    if (!sc.ok) {
+      if (dep_out) *dep_out = depth + 1;
+      return L + mul(T, E + D);
+    }
     L = L + mul(T, E + muls(D, m->dw));
-    if (!h.recursive || depth + 1 >= h.max_depth) return L;
+    if (!h.recursive || depth + 1 >= h.max_depth) {
+      if (dep_out) *dep_out = depth + 1;
+      return L;
+    }
     T = mul(T, muls(sc.A, m->rw));
     o = P;
     d = sc.nd;
@@ -1185,19 +1201,21 @@ __device__ __forceinline__ void tail_helper(KArg karg, int* stack, double (*buf)
   const KArg k0 = launder(karg);
   TailCtl* const ctl = k0->tail;
   const unsigned int epoch = k0->tail_epoch, cap = (unsigned int)k0->tail_cap, main_wgs = (unsigned int)k0->num_wgs;
-  if (lane == 0) atomicAdd(&ctl->helpers_live, 1u);
+  if (lane == 0) atomicAdd(ctl->gate, 1ull << 32);  // one more helper
   const unsigned long long t_born = __builtin_amdgcn_s_memrealtime();
   unsigned long long t_idle = t_born;
+  int polls = 0;
 #ifdef RT_WG_TIMING
-  unsigned long long dbg_first = 0, dbg_paths = 0, dbg_solo = 0;
+  unsigned long long dbg_first = 0, dbg_paths = 0, dbg_solo = 0, dbg_last = 0, dbg_last_d0 = 0, dbg_last_d1 = 0,
+                     dbg_bounces = 0;
 #endif
   for (;;) {
     int idx = -1;
     if (lane == 0) {
       for (;;) {
-        const unsigned int h = ld_rlx(&ctl->head), t = min(ld_rlx(&ctl->tail), cap);
+        const unsigned int t = min(ld_rlx(ctl->tail), cap), h = ld_rlx(ctl->head);
         if (h >= t) break;
-        if (atomicCAS(&ctl->head, h, h + 1u) == h) {
+        if (atomicCAS(ctl->head, h, h + 1u) == h) {
           idx = (int)h;
           break;
         }
@@ -1205,14 +1223,17 @@ __device__ __forceinline__ void tail_helper(KArg karg, int* stack, double (*buf)
     }
     idx = __builtin_amdgcn_readfirstlane(idx);
     if (idx < 0) {
-      // every main block finished (the sharded counters, one per lane)?
-      // Then nothing more can be queued: leave once the queue is empty
-      unsigned int dn = lane < kTailShards ? ld_rlx(&ctl->done[lane * 32]) : 0u;
-      for (int off = 32; off >= 1; off >>= 1) dn += __shfl_xor(dn, off);
-      if (__builtin_amdgcn_readfirstlane(dn) >= main_wgs) {
-        const unsigned int h = ld_rlx(&ctl->head), t = min(ld_rlx(&ctl->tail), cap);
-        if (__builtin_amdgcn_readfirstlane(h >= t ? 1 : 0)) break;
-        continue;
+      // every main block finished (the sharded counters, one per lane; read
+      // every 32nd idle poll)?  Then nothing more can be queued: leave once
+      // the queue is empty
+      if ((++polls & 31) == 0) {
+        unsigned int dn = lane < kTailShards ? ld_rlx(&ctl->done[lane * 32]) : 0u;
+        for (int off = 32; off >= 1; off >>= 1) dn += __shfl_xor(dn, off);
+        if (__builtin_amdgcn_readfirstlane(dn) >= main_wgs) {
+          const unsigned int h = ld_rlx(ctl->head), t = min(ld_rlx(ctl->tail), cap);
+          if (__builtin_amdgcn_readfirstlane(h >= t ? 1 : 0)) break;
+          continue;
+        }
       }
       // (a bound that is never expected to bite: main blocks are at most a
       // 1024-sample block each; a stuck helper must not hang the device)
@@ -1220,7 +1241,7 @@ __device__ __forceinline__ void tail_helper(KArg karg, int* stack, double (*buf)
         if (lane == 0) atomicOr(&ctl->err, 1u);
         break;
       }
-      __builtin_amdgcn_s_sleep(16);
+      __builtin_amdgcn_s_sleep(96);  // (~2.6 us between polls: idle helpers must not crowd the lines they poll)
       continue;
     }
     // the entry was reserved by a block that writes it at once
@@ -1246,12 +1267,17 @@ __device__ __forceinline__ void tail_helper(KArg karg, int* stack, double (*buf)
     const int depth = (int)ld_wt32(&q->depth), sample = (int)ld_wt32(&q->sample), kind = (int)ld_wt32(&q->kind),
               row = (int)ld_wt32(&q->row), nsub = (int)ld_wt32(&q->nsub), fr = (int)ld_wt32(&q->frame);
     const int64_t oi = (int64_t)ld_wt64(&q->oi);
-    const d3 L = solo_path<false>(karg, 0, o, d, T, L0, rx, depth, sk, stack);
+    int dep_end = depth;
+    const d3 L = solo_path<false>(karg, 0, o, d, T, L0, rx, depth, sk, stack, &dep_end);
     const KArg k = launder(karg);
 #ifdef RT_WG_TIMING
     if (!dbg_first) dbg_first = t_path;
     dbg_paths += 1;
     dbg_solo += __builtin_amdgcn_s_memrealtime() - t_path;
+    dbg_last = t_path;
+    dbg_last_d0 = (unsigned long long)depth;
+    dbg_last_d1 = (unsigned long long)dep_end;
+    dbg_bounces += (unsigned long long)(dep_end - depth);
 #endif
     const int spp = k->spp_total, bw = (spp + 31) >> 5;
     int last = 0;
@@ -1276,7 +1302,7 @@ __device__ __forceinline__ void tail_helper(KArg karg, int* stack, double (*buf)
         wt_drain();
         last = atomicAdd(&k->split_cnt[row], 1) == nsub - 1 ? 1 : 0;
       }
-      atomicSub(&ctl->inflight, 1u);
+      atomicAdd(ctl->gate, ~0ull);  // one exported path fewer in flight (-1 on the low half)
     }
     last = __builtin_amdgcn_readfirstlane(last);
     if (last) {
@@ -1312,25 +1338,28 @@ __device__ __forceinline__ void tail_helper(KArg karg, int* stack, double (*buf)
     r[1] = dbg_first;
     r[2] = __builtin_amdgcn_s_memrealtime();
     r[3] = dbg_solo;
+    r[4] = dbg_last;     // the last path's start,
+    r[5] = dbg_last_d0;  // its depth when exported,
+    r[6] = dbg_last_d1;  // and at its end
     r[7] = dbg_paths;
+    r[8] = dbg_bounces;
     r[14] = ~0ull;
   }
 #endif
   if (lane == 0) {
     atomicAdd(&ctl->helper_ticks, (unsigned int)(__builtin_amdgcn_s_memrealtime() - t_born));
-    atomicSub(&ctl->helpers_live, 1u);
-    gone = (int)atomicAdd(&ctl->helpers_gone, 1u);
+    atomicAdd(ctl->gate, ~0ull << 32);  // one helper fewer (-2^32)
+    gone = (int)atomicAdd(ctl->helpers_gone, 1u);
   }
   if (__builtin_amdgcn_readfirstlane(gone) + 1 == k0->tail_helpers) {
     // every helper and every main block is done: ready for the next launch
     if (lane < kTailShards) ctl->done[lane * 32] = 0u;
     if (lane == 0) {
-      ctl->tail = 0;
-      ctl->head = 0;
-      ctl->inflight = 0;
-      ctl->rows_used = 0;
-      ctl->helpers_live = 0;
-      ctl->helpers_gone = 0;
+      ctl->tail[0] = 0;
+      ctl->head[0] = 0;
+      ctl->gate[0] = 0;
+      ctl->rows_used[0] = 0;
+      ctl->helpers_gone[0] = 0;
     }
   }
 }
@@ -1351,7 +1380,8 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   const int lane = threadIdx.x;
   int* stack = reinterpret_cast<int*>(dyn_lds + pk.stack_off) + lane;
   if constexpr (kTail) {
-    if ((int)blockIdx.x >= pk.num_wgs) {  // a tail helper (launch_render adds them only with pk.tail set)
+    if (pk.tail != nullptr && blockIdx.x - (unsigned)pk.tail_pos < (unsigned)pk.tail_helpers) {
+      // a tail helper (launch_render adds them only with pk.tail set)
       const uint4* __restrict__ src = reinterpret_cast<const uint4*>(pk.stage_src);
       uint4* dst = reinterpret_cast<uint4*>(dyn_lds);
       for (int i = lane; i < pk.stage_bytes / 16; i += 64) dst[i] = src[i];
@@ -1621,6 +1651,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     int depth = 0, entry = 0;
     bool alive = false;
     int next = 0, resolved = 0;  // wave-uniform: next entry to start; entries [0, resolved) summed
+    int drain_it = 0;            // (tail helpers) iterations since every entry started
     // The path's radiance L lives in its entry's ring slot (the slot is the
     // path's own until it finishes, and resolve_entries reads it only then):
     // read and written once per bounce, in VGPRs it held 6 registers through
@@ -1671,6 +1702,17 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
             __syncthreads();
             resolve_entries(resolved, lo);
             __syncthreads();
+            if constexpr (kTail) {
+              // the resolved entries' ring slots take new entries now: their
+              // exported marks go (slot s is in [resolved, lo) mod kRound iff
+              // (s - resolved) mod kRound < lo - resolved)
+              if (lane < kRound / 32) {
+                uint32_t m = 0;
+                for (int j = 0; j < 32; ++j)
+                  m |= (uint32_t)(((32 * lane + j - resolved) & (kRound - 1)) < lo - resolved) << j;
+                xm[lane] &= ~m;
+              }
+            }
             resolved = lo;
             limit = min(nh, resolved + kRound);
           }
@@ -1721,7 +1763,16 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
             // one is free), which runs it alone at solo latency; its radiance
             // reaches the pixel through the pixel's row (resolve_entries, the
             // epilogue), the same sum in the same order.
-            if (next >= nh && fresh()->tail != nullptr) {
+            // (every tail_every-th iteration of the drain, 4 by default: the gate read is a memory round
+            // trip on the lone paths' chain, and a drain shorter than that
+            // gains nothing from a helper)
+            // The block's drain: every entry has started.  (Exporting at ring
+            // stalls too -- the ring full behind a long path, whose export lets
+            // the lanes take new entries -- measured slower: one frame 0.555 ->
+            // 0.620 ms at 64 helpers; more, shorter paths queue for the helpers
+            // ahead of the long ones.  The resolve below supports it: rows are
+            // filled mid-loop and exported ring slots are unmarked on reuse.)
+            if (next >= nh && (++drain_it & fresh()->tail_every_mask) == 0 && fresh()->tail != nullptr) {
               const unsigned long long am = __ballot(alive);
               if (__popcll(am) <= fresh()->tail_kmax) {
                 for (unsigned long long em = __ballot(alive && depth >= fresh()->tail_dmin); em; em &= em - 1) {
@@ -1730,14 +1781,19 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
                   KArg k = fresh();
                   TailCtl* ctl = k->tail;
                   int idx = -1;
-                  if (lane == 0 && ld_rlx(&ctl->inflight) < ld_rlx(&ctl->helpers_live)) {
-                    // a helper for it (inflight < live helpers: read before any add, so
-                    // draining waves do not hammer the line) and a queue entry
-                    if (atomicAdd(&ctl->inflight, 1u) < ld_rlx(&ctl->helpers_live)) {
-                      const unsigned int t = atomicAdd(&ctl->tail, 1u);
-                      if (t < (unsigned int)k->tail_cap) idx = (int)t;  // (entries past the cap are never taken)
+                  // a helper for it (paths in flight < live helpers: the gate word is
+                  // read first, so draining waves do not add to it in vain) and a
+                  // queue entry
+                  if (lane == 0) {
+                    const unsigned long long g0 = __hip_atomic_load(ctl->gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((uint32_t)g0 < (uint32_t)(g0 >> 32)) {
+                      const unsigned long long g = atomicAdd(ctl->gate, 1ull);
+                      if ((uint32_t)g < (uint32_t)(g >> 32)) {
+                        const unsigned int t = atomicAdd(ctl->tail, 1u);
+                        if (t < (unsigned int)k->tail_cap) idx = (int)t;  // (entries past the cap are never taken)
+                      }
+                      if (idx < 0) atomicAdd(ctl->gate, ~0ull);
                     }
-                    if (idx < 0) atomicSub(&ctl->inflight, 1u);
                   }
                   idx = __builtin_amdgcn_readfirstlane(idx);
                   // (all the handed-over bytes below are written through: st_wt*)
@@ -1761,7 +1817,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
                     sample = sl;
                     int r = prow[p];
                     if (r < 0) {  // the pixel's dynamic row (one row per export at most: rows_used < cap)
-                      if (lane == 0) r = (int)atomicAdd(&ctl->rows_used, 1u);
+                      if (lane == 0) r = (int)atomicAdd(ctl->rows_used, 1u);
                       r = __builtin_amdgcn_readfirstlane(r);
                       const int bw = (k->spp_total + 31) >> 5;
                       for (int w = lane; w < bw; w += 64) st_wt32(k->tail_bits + (size_t)r * bw + w, 0u);
@@ -1809,7 +1865,7 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
                   if (lane == 0) atomicAdd(&ctl->export_ticks, (unsigned int)(__builtin_amdgcn_s_memrealtime() - t_x));
                 }
                 if (__ballot(alive) == 0) {  // every path left went to a helper
-                  outer = 2;
+                  outer = next >= nh ? 2 : 1;  // done / the ring moves on: resolve, then refill
                   break;
                 }
               }

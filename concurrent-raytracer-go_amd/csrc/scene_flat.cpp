@@ -303,8 +303,9 @@ void rt_tuning_default(rt_tuning* t) {
   // the chains of the longest paths, not the block sizes (C2 0.80 pilot-only
   // vs 0.84 ms measured, C3 0.59 vs 0.56; scripts/tuning_sweep.py)
   t->measure = 0;
-  // tail helpers: off until measured faster
-  t->tail_helpers = -1;
+  // tail helpers: 64 at the end of the launch; drains
+  // checked every 4th iteration, paths of >= 2 bounces, <= 4 left (the 0s)
+  t->tail_helpers = 64;
 }
 
 int32_t rt_num_tiles(int32_t w, int32_t h) {

@@ -149,6 +149,8 @@ class Tuning(ctypes.Structure):
         ("tail_helpers", ctypes.c_int32),
         ("tail_paths", ctypes.c_int32),
         ("tail_depth", ctypes.c_int32),
+        ("tail_every", ctypes.c_int32),
+        ("tail_at", ctypes.c_int32),
         ("_tail_pad", ctypes.c_int32),
     ]
 

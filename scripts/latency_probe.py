@@ -37,8 +37,13 @@ def scene(inner=True, lights=2):
     return rtgo.Scene.from_json_text(json.dumps(s))
 
 
+TUN = {k: int(v) for k, v in (kv.split("=") for kv in filter(None, os.environ.get("PROBE_TUNING", "").split(",")))}
+
+
 def time_depth(sc, depth, soft=1, reps=9):
     ctx = rtgo.Context(0)
+    if TUN:  # e.g. PROBE_TUNING=tail_helpers=1,tail_depth=1,tail_every=1: the path runs in a tail helper
+        ctx.set_tuning(rtgo.default_tuning(**TUN))
     ctx.set_scene(sc)
     st = rtgo.default_settings()
     st.samples = 1

@@ -64,7 +64,11 @@ if len(hd):
     print(f"tail helpers: {len(hd)}, start us p0/p50/p100 {hs.min():.1f}/{np.median(hs):.1f}/{hs.max():.1f}, "
           f"end p0/p50/p100 {he.min():.1f}/{np.median(he):.1f}/{he.max():.1f}, first path p0/p50 "
           f"{np.nanmin(hf) if np.isfinite(hf).any() else -1:.1f}/{np.nanmedian(hf) if np.isfinite(hf).any() else -1:.1f}, "
-          f"paths {int(hd[:, 0, 7].sum())}, solo us per path {hd[:, 0, 3].sum() / max(1, hd[:, 0, 7].sum()) / 100:.1f}")
+          f"paths {int(hd[:, 0, 7].sum())}, solo us per path {hd[:, 0, 3].sum() / max(1, hd[:, 0, 7].sum()) / 100:.1f}, "
+          f"bounces {int(hd[:, 0, 8].sum())}, us per bounce {hd[:, 0, 3].sum() / max(1, hd[:, 0, 8].sum()) / 100:.2f}")
+    late = np.argsort(-he)[:8]
+    print("  latest helpers (end us, last path start us, depth at export -> end): " + ", ".join(
+        f"({he[i]:.0f}, {(hd[i, 0, 4] - t0h) / 100.0:.0f}, {int(hd[i, 0, 5])}->{int(hd[i, 0, 6])})" for i in late))
 nwg = d.shape[0]
 t0 = d[:, :, 0].min()
 start = (d[:, :, 0] - t0) / 100.0  # s_memrealtime: 100 MHz -> microseconds

@@ -18,7 +18,8 @@ from scene_cases import load_case, make_settings
 
 pytestmark = pytest.mark.gpu
 
-FORCED = {"tail_helpers": 256, "tail_paths": 64, "tail_depth": 1}  # every path of a draining block, from its first bounce
+# every path of a draining block, from its first bounce, checked every iteration
+FORCED = {"tail_helpers": 256, "tail_paths": 64, "tail_depth": 1, "tail_every": 1}
 ON = {"tail_helpers": 256}
 
 
