@@ -367,6 +367,52 @@ __device__ __forceinline__ void descend(glb_node* __restrict__ qb, lds_node* __r
   }
 }
 
+// The closest-hit descent with an early exit (wf_extend): the lanes that
+// have reached a leaf idle in `descend` until the deepest-descending lane
+// of the wave gets there (C4: 14.6 % of the lanes active per VALU
+// instruction).  Here the descent stops for every lane once at most
+// 1/kDescendFrac of the lanes that entered it are still descending; those
+// keep their node and stack and go on in the next round, while the others
+// test their leaves now.  (The node order and the tests are the same: only
+// when each lane's steps run changes, not which.)
+// (C4 per frame, scripts/c4_tuning_probe.py, one MI355X, two frames each,
+// profiles/r06_c4_descend.jsonl: closest hit 102.5-102.9 ms without the exit,
+// 103.9-104.3 at 1/2, 98.0-98.4 at 1/4, 98.6-99.0 at 1/8; frame 373.8-374.2 ->
+// 369.1-369.2 ms at 1/4; the image checksum unchanged)
+#ifndef RT_DESCEND_FRAC
+#define RT_DESCEND_FRAC 4
+#endif
+constexpr int kDescendFrac = RT_DESCEND_FRAC;
+template <bool kCount, bool kFull>
+__device__ __forceinline__ void descend_x(glb_node* __restrict__ qb, lds_node* __restrict__ lt, int nlds,
+                                          const RayQ& r, float tminf, float tmaxf, int& cur, int& sp, int* stack,
+                                          Counters& c) {
+  if constexpr (kDescendFrac <= 0) {
+    descend<kCount, kFull>(qb, lt, nlds, r, tminf, tmaxf, cur, sp, stack, c);
+  } else {
+    const int entered = __popcll(__ballot(true));
+    while ((cur & 7) == 0) {
+      uint4 L, R;
+      load_pair<kFull>(qb, lt, nlds, cur >> 3, L, R);
+      cnt<kCount>(c, C_BOX, 2);
+      float tl, tr;
+      const bool hl = box_q(L, r, tminf, tmaxf, tl), hr = box_q(R, r, tminf, tmaxf, tr);
+      if (hl || hr) {
+        const bool lfirst = hl && (!hr || tl <= tr);
+        if (hl && hr) {
+          stack[sp * 64] = lfirst ? (int)R.w : (int)L.w;
+          ++sp;
+        }
+        cur = lfirst ? (int)L.w : (int)R.w;
+      } else {
+        cur = sp == 0 ? -1 : stack[--sp * 64];
+      }
+      // (the lanes still in this loop are the active ones: the ballot counts them)
+      if (__popcll(__ballot((cur & 7) == 0)) * kDescendFrac <= entered) break;
+    }
+  }
+}
+
 // The any-hit descent over the 4-wide tree (bvh.cpp qbvh4: groups of 2..4
 // child boxes): a group's boxes are tested at once, the first hit child in
 // slot order is entered and the other hit children are pushed.  Half the
@@ -374,9 +420,14 @@ __device__ __forceinline__ void descend(glb_node* __restrict__ qb, lds_node* __r
 // occlusion query ends at any hit, and sorting the children (full sort, or
 // the nearest first) measured slower, as did the 4-wide tree for closest hit
 // (DESIGN.md §4.2).  The order does not change which rays are blocked.
+// (the same early exit as descend_x, 1/RT_OCC_FRAC; 0: none)
+#ifndef RT_OCC_FRAC
+#define RT_OCC_FRAC 4
+#endif
 template <bool kCount>
 __device__ __forceinline__ void descend4(lds_node* __restrict__ lt, const RayQ& r, float tminf, float tmaxf, int& cur,
                                          int& sp, int* stack, Counters& c) {
+  const int entered = RT_OCC_FRAC > 0 ? __popcll(__ballot(true)) : 0;
   while ((cur & 7) == 0) {
     const int base = cur >> 5, nk = ((cur >> 3) & 3) + 1;  // the group's first slot and size (bvh.cpp)
     const uint4 n0 = as_uint4(lt[base]), n1 = as_uint4(lt[base + 1]), n2 = as_uint4(lt[base + 2]),
@@ -395,6 +446,7 @@ __device__ __forceinline__ void descend4(lds_node* __restrict__ lt, const RayQ& 
         taken = true;
       }
     if (!taken) cur = sp == 0 ? -1 : stack[--sp * 64];
+    if (RT_OCC_FRAC > 0 && __popcll(__ballot((cur & 7) == 0)) * RT_OCC_FRAC <= entered) break;
   }
 }
 
@@ -523,8 +575,8 @@ __global__ RT_TRAV_ATTR void wf_extend(const WfParams p) {
       continue;
     }
     if (busy) {
-      descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, t_hi32(closest), cur, sp, stack, c);
-      if (cur != -1) {  // a leaf: the exact Sphere.Hit tests, in hittable order
+      descend_x<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, t_hi32(closest), cur, sp, stack, c);
+      if (cur != -1 && (cur & 7) != 0) {  // a leaf: the exact Sphere.Hit tests, in hittable order
         const int first = cur >> 3, count = cur & 7;
         DSphere ls[kLeafBatch];
         load_leaf(p.g.spheres, first, count, ls);
@@ -717,7 +769,7 @@ __device__ __forceinline__ void occlude_body(const WfParams& p) {
       else
         descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, r32, tminf, tmaxf, cur, sp, stack, c);
       bool blocked = false;
-      if (cur != -1) {
+      if (cur != -1 && (cur & 7) != 0) {  // (a leaf; an internal node: the descent paused, descend4)
         const int first = cur >> 3, count = cur & 7;
         DSphere ls[kLeafBatch];
         load_leaf(p.g.spheres, first, count, ls);
@@ -870,8 +922,12 @@ __device__ __forceinline__ void cone_descend(glb_node* __restrict__ qb, lds_node
 // The same walk over the 4-wide tree (descend4's order: the first hit child
 // entered, the other hit children pushed)
 template <bool kCount>
+#ifndef RT_CONE_FRAC
+#define RT_CONE_FRAC 4
+#endif
 __device__ __forceinline__ void cone_descend4(lds_node* __restrict__ lt, const ConeQ& k, int& cur, int& sp, int* stack,
                                               Counters& c) {
+  const int entered = RT_CONE_FRAC > 0 ? __popcll(__ballot(true)) : 0;
   while ((cur & 7) == 0) {
     const int base = cur >> 5, nk = ((cur >> 3) & 3) + 1;  // the group's first slot and size (bvh.cpp)
     const uint4 n0 = as_uint4(lt[base]), n1 = as_uint4(lt[base + 1]), n2 = as_uint4(lt[base + 2]),
@@ -888,6 +944,7 @@ __device__ __forceinline__ void cone_descend4(lds_node* __restrict__ lt, const C
         taken = true;
       }
     if (!taken) cur = sp == 0 ? -1 : stack[--sp * 64];
+    if (RT_CONE_FRAC > 0 && __popcll(__ballot((cur & 7) == 0)) * RT_CONE_FRAC <= entered) break;
   }
 }
 
@@ -999,7 +1056,7 @@ __device__ __forceinline__ void cone_body(const WfParams& p) {
         cone_descend4<kCount>(lt, k, cur, sp, stack, c);
       else
         cone_descend<kCount, kFull>((glb_node*)p.qbvh, lt, p.lds_nodes, k, cur, sp, stack, c);
-      if (cur != -1) {
+      if (cur != -1 && (cur & 7) != 0) {  // (a leaf; an internal node: the walk paused, cone_descend4)
         const int first = cur >> 3, count = cur & 7;
         DSphere ls[kLeafBatch];
         load_leaf(p.g.spheres, first, count, ls);

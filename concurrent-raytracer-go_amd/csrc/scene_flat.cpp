@@ -305,7 +305,7 @@ void rt_tuning_default(rt_tuning* t) {
   t->measure = 0;
   // tail helpers: 64 at the end of the launch; drains
   // checked every 4th iteration, paths of >= 2 bounces, <= 4 left (the 0s)
-  t->tail_helpers = 64;
+  t->tail_helpers = -1;  // measured a net loss on the headline frame
 }
 
 int32_t rt_num_tiles(int32_t w, int32_t h) {

@@ -339,7 +339,8 @@ typedef struct {
   /* tail helpers (megakernel, staged scenes): a block's last
    * few long paths are handed to extra one-wave workgroups at the end of the
    * launch that run each alone, at the latency of a lone bounce */
-  int32_t tail_helpers;   /* helper workgroups per launch (rt_tuning_default: 64); 0: 64; -1: none (the paths stay in their blocks) */
+  int32_t tail_helpers;   /* helper workgroups per launch; 0: 64; -1: none, the paths stay in their blocks
+                             (rt_tuning_default: -1; DESIGN.md §4.6 measures 64 as a net loss) */
   int32_t tail_paths;     /* a block exports once at most this many paths are left; 0: 4 */
   int32_t tail_depth;     /* ... each at least this many bounces deep; 0: 2 */
   int32_t tail_every;     /* ... checked every this many iterations of the block's drain (rounded up to a power of 2, at most 64); 0: 4 */
