@@ -95,10 +95,10 @@ TRAV_RAY_SETUP_FLOPS = 21
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) peak: 256 CU x 2.4 GHz x 128 FLOP/clk
 PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-PMC_FILE = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r06_pmc_traffic.json")
 # the driver's own command under rocprofv3 --kernel-trace: its timed launches
 # (scripts/batched_trace.py, scripts/profile.sh "driver")
-TRACE_FILE = os.path.join(ROOT, "profiles", "r05_driver_batched_trace.json")
+TRACE_FILE = os.path.join(ROOT, "profiles", "r06_driver_batched_trace.json")
 
 CONFIGS = {
     # name: (scene, W, H, spp, label, default steps, default frames in flight at one GPU)
@@ -745,7 +745,7 @@ def cpu_baseline_bvh(args, rtgo, scene, W, H, st):
 
 def pmc_traffic(workload):
     """HBM bytes per launch of the dominant kernel from the committed
-    rocprofv3 PMC passes (profiles/r05_pmc_traffic.json, scripts/pmc_traffic.py,
+    rocprofv3 PMC passes (profiles/r06_pmc_traffic.json, scripts/pmc_traffic.py,
     with the gfx950 corrections of MI355X_MICROARCH.md §HBM), if it holds this
     workload."""
     try:
@@ -1159,11 +1159,11 @@ def main():
                         "(HIP events on the render stream; for c4/c5 the soft-shadow traversal kernel's time per "
                         "frame from rt_context_profile's events in the timed frames); frac_in_flight: the frame's flops over "
                         "ms_per_step (the throughput line's time per frame).  traffic = HBM bytes per "
-                        "launch from rocprofv3 FETCH_SIZE + WRITE_SIZE passes (profiles/r05_pmc_traffic.json; "
+                        "launch from rocprofv3 FETCH_SIZE + WRITE_SIZE passes (profiles/r06_pmc_traffic.json; "
                         "traffic_batched_per_frame: the same passes over launches of several frames, per frame).  "
                         "busy_ms_per_frame / frac_busy: the timed launches' HIP-event spans (their union: launches in "
                         "flight overlap) over the frames; trace_batched: the same from the committed rocprofv3 "
-                        "kernel trace of this exact command (profiles/r05_driver_batched_trace.json).",
+                        "kernel trace of this exact command (profiles/r06_driver_batched_trace.json).",
             },
             "roofline_frame": whole,
             "roofline_hbm": {

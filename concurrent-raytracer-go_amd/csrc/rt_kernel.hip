@@ -1364,8 +1364,8 @@ __device__ __forceinline__ void tail_helper(KArg karg, int* stack, double (*buf)
   }
 }
 
-template <bool kCount, bool kStage, bool kPilot, bool kSky>
-__global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KParams pk) {
+template <bool kCount, bool kStage, bool kPilot, bool kSky, bool kTailT>
+__device__ __forceinline__ void render_body(const KParams& pk) {
   __shared__ uint32_t hbits[kMaxBlockSamples / 32];  // hit samples of the block
   __shared__ int hoff[kMaxBlockSamples / 32 + 1];    // list offset of each bit word; [words] = #hits
   __shared__ double slot[kRound][3];                 // radiance of the round's entries
@@ -1373,9 +1373,11 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
   __shared__ uint8_t lpix[64];                       // phase 1: the block's live pixels
   __shared__ uint64_t skey[64];                      // per lane: its path's soft-shadow key (rt_soft_key, spec v4)
   // dynamic LDS (dyn_lds): [staged scene prefix (kStage)][BVH stack (stack_depth x 64 ints)]
-  // tail helpers: the product instantiation exports a
-  // block's last few long paths to the helpers past its main blocks
-  constexpr bool kTail = kStage && !kCount && !kPilot && !kSky;
+  // tail helpers: render_kernel_tail exports a block's last
+  // few long paths to the helpers past its main blocks.  The product kernel
+  // has none of that code (compiled in but unused it cost 2-3 % one frame,
+  // 1.5 % batched: r06 A/B)
+  constexpr bool kTail = kTailT && kStage && !kCount && !kPilot && !kSky;
 
   const int lane = threadIdx.x;
   int* stack = reinterpret_cast<int*>(dyn_lds + pk.stack_off) + lane;
@@ -2294,6 +2296,14 @@ __global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KPa
     }
   }
 }
+template <bool kCount, bool kStage, bool kPilot, bool kSky>
+__global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel(const KParams pk) {
+  render_body<kCount, kStage, kPilot, kSky, false>(pk);
+}
+// the staged product render with tail helpers (rt_tuning.tail_helpers > 0)
+__global__ __launch_bounds__(64, RT_WAVES_PER_SIMD) void render_kernel_tail(const KParams pk) {
+  render_body<false, true, false, false, true>(pk);
+}
 
 // Gathered shares [world][share_bytes] (each: [max_local][1024] float3, then
 // [max_local][1024] RGBA8 at rgba_off) -> W*H images.  One thread per image
@@ -2455,6 +2465,8 @@ int launch_render(const KParams& pin, bool count, void* stream) {
     hipLaunchKernelGGL((render_kernel<false, true, false, true>), g, b, shmem, st, p);
   } else if (p.sky) {
     hipLaunchKernelGGL((render_kernel<false, false, false, true>), g, b, shmem, st, p);
+  } else if (stage && tail) {
+    hipLaunchKernelGGL(render_kernel_tail, g, b, shmem, st, p);
   } else if (stage) {
     hipLaunchKernelGGL((render_kernel<false, true, false, false>), g, b, shmem, st, p);
   } else {
