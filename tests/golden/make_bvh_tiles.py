@@ -21,6 +21,10 @@ Run once (a few CPU-minutes per tile; tiles run in parallel threads):
     python tests/golden/make_bvh_tiles.py survey c4 4
     python tests/golden/make_bvh_tiles.py survey c5 64 0 7    (ranks 0 and 7 of 8)
     python tests/golden/make_bvh_tiles.py render c4 <tile> <tile> ...
+The wider sample (r06; tests/test_gpu_bvh_tiles.py checks both):
+    SUFFIX=_more python tests/golden/make_bvh_tiles.py render c4 <12 tiles of survey_c4.json, spread over its ranking>
+    SUFFIX=_more python tests/golden/make_bvh_tiles.py survey c5 64 19 45    (ranks 3 and 5 of 8)
+    SUFFIX=_more python tests/golden/make_bvh_tiles.py render c5 <2 tiles of rank 3, 2 of rank 5>
 """
 import json
 import os
@@ -38,6 +42,9 @@ import oracle  # noqa: E402
 import rtgo  # noqa: E402
 from scene_cases import make_settings, spheres10k_scene  # noqa: E402
 
+# SUFFIX=_more: write survey_<cfg>_more.json / oracle_<cfg>_tiles_more.npz (the
+# second, wider sample of tiles) instead of the first files
+SUFFIX = os.environ.get("SUFFIX", "")
 # (width, height, spp) of each config; depth 50, soft shadows, recursion (defaults)
 CONFIGS = {"c4": (1920, 1080, 64), "c5": (3840, 2160, 256)}
 
@@ -61,7 +68,7 @@ def survey(cfg, stride, offsets, workers):
     with ThreadPoolExecutor(workers) as ex:
         res = list(ex.map(lambda t: render_tile(scene, w, h, st, t)[2], tiles))
     out = {str(t): c for t, c in zip(tiles, res)}
-    path = os.path.join(HERE, f"survey_{cfg}.json")
+    path = os.path.join(HERE, f"survey_{cfg}{SUFFIX}.json")
     with open(path, "w") as f:
         json.dump(out, f)
     top = sorted(tiles, key=lambda t: -out[str(t)]["bounce_rays"])[:12]
@@ -81,7 +88,7 @@ def render(cfg, tiles, workers):
     rgba = np.stack([r[1] for r in res])
     counts = np.array([[r[2][k] for k in rtgo.COUNT_FIELDS] for r in res], np.uint64)
     assert not np.isnan(lin).any()
-    path = os.path.join(HERE, f"oracle_{cfg}_tiles.npz")
+    path = os.path.join(HERE, f"oracle_{cfg}_tiles{SUFFIX}.npz")
     np.savez_compressed(path, tiles=np.array(tiles, np.int32), linear=lin, rgba=rgba, counts=counts,
                         config=np.array([w, h, spp, 50, 1], np.int32))
     print(f"{path}: tiles {tiles} at {w}x{h}x{spp} in {time.time() - t0:.0f} s, {os.path.getsize(path)} B")
