@@ -1589,9 +1589,15 @@ __device__ __forceinline__ void render_body(const KParams& pk) {
         if constexpr (kTail) {
           if ((xm[q >> 5] >> (q & 31)) & 1u) continue;  // exported: its helper writes the sample
         }
-        st_wtd(row + 3 * s + 0, slot[q][0]);  // (written through: read sc1 by the pixel's last sub-block)
-        st_wtd(row + 3 * s + 1, slot[q][1]);
-        st_wtd(row + 3 * s + 2, slot[q][2]);
+        if constexpr (kTail) {  // (written through: read sc1 by the pixel's last contributor, maybe a helper)
+          st_wtd(row + 3 * s + 0, slot[q][0]);
+          st_wtd(row + 3 * s + 1, slot[q][1]);
+          st_wtd(row + 3 * s + 2, slot[q][2]);
+        } else {  // (combined in L2, written back by the release fence below)
+          row[3 * s + 0] = slot[q][0];
+          row[3 * s + 1] = slot[q][1];
+          row[3 * s + 2] = slot[q][2];
+        }
         atomicOr(hw + (s >> 5), 1u << (s & 31));
       }
     } else {
@@ -2172,22 +2178,29 @@ __device__ __forceinline__ void render_body(const KParams& pk) {
   if (blk.slot >= 0) {
     // a split pixel: the last of its sub-blocks to finish sums the hit
     // samples of the slot row in sample order (misses add +0) and writes it
-    // (its row samples were written through: drained before the counter;
-    // the last sub-block reads the row sc1 -- no L2 write-back or
-    // invalidate, see the tail helpers' hand-off notes above)
-    wt_drain();
+    // Tail kernel: its row samples were written through, drained before the
+    // counter, and the last contributor reads the row sc1 (the tail
+    // helpers' hand-off, above).  Product kernel: plain stores, a release
+    // fence before the counter and an acquire fence after it (the same
+    // time, r06 A/B, and the row's samples reach HBM as whole lines: the
+    // write-through form wrote 3.8 MB more per headline frame)
+    if constexpr (kTail)
+      wt_drain();
+    else
+      __threadfence();
     int old = 0;
     if (lane3 == 0) old = atomicAdd(&k->split_cnt[split_index(k, blk.slot)], 1);
     old = __builtin_amdgcn_readfirstlane(old);
     resolve = old == blk.nsub - 1;
     if (resolve) {
+      if constexpr (!kTail) __threadfence();
       const double* row = k->split_rad + split_index(k, blk.slot) * k->spp * 3;
       uint32_t* hw = k->split_hits + split_index(k, blk.slot) * ((k->spp + 31) >> 5);
       // chunks of kRound samples: all lanes load (in parallel) into the LDS
       // slots, misses as +0, then one lane per channel adds them in order
       double a = 0;  // (a later sample pass continues the running sum)
       if ((k->acc_mode & 1) && lane3 < 3) a = k->acc[((size_t)blk.lt * 1024 + blk.p0) * 3 + lane3];
-      a = row_sum<true>(slot, row, hw, 0, k->spp, a, lane3);
+      a = row_sum<kTail>(slot, row, hw, 0, k->spp, a, lane3);
       if (lane3 < 3) psum[0][lane3] = a;
       // the slot's hit bits and counter are left zeroed for the next launch
       // (the host clears them only when it builds a schedule: no memset per frame)
