@@ -77,7 +77,8 @@ def run(scene, tun):
 def main():
     specs = sys.argv[1:] or ["off:tail_helpers=-1", "default:", "d4:tail_depth=4", "d8:tail_depth=8",
                              "k1:tail_paths=1", "k2d4:tail_paths=2,tail_depth=4", "h64:tail_helpers=64"]
-    scene = rtgo.Scene.load_from_file(os.path.join(ROOT, "scenes", "sphere_reflections_light_facing.json"))
+    name = os.environ.get("TAIL_SCENE", "sphere_reflections_light_facing.json")  # (W, H: the headline's)
+    scene = rtgo.Scene.load_from_file(os.path.join(ROOT, "scenes", name))
     for spec in specs:
         name, tun = parse(spec)
         print(json.dumps({"name": name, "tuning": tun, **run(scene, tun)}), flush=True)
