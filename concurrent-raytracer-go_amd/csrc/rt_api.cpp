@@ -795,15 +795,15 @@ static int run_pilot(const rt_context* c, const KParams& p, SchedParams* sp, cha
 // grow: the driver's 20 frames as 2 launches of 10, C2 1024 -> 212.5 k, 1536
 // 223.7 k, 2048 215.0 k, 3072 212.6 k, 4096 208.6 k; 100 frames as 4 of 25:
 // 247.8 k, 251.6 k, 251.0 k, 249.6 k, 248.3 k; scripts/k20_tuning.sh)
-// (r06, one frame per launch, sphere scenes: 384 -> 512 bounce-samples per
-// block, 0.575-0.589 -> 0.565-0.575 ms, median of 40 frames, three
-// alternating runs, scripts/tail_probe.py; 448 0.575-0.583, 576 0.571-0.579,
-// 768 0.725, 256 0.60-0.62)
+// (r06, one frame per launch, sphere scenes, scripts/tail_probe.py, median
+// of 40 frames: 384 and 512 bounce-samples per block equal when the order of
+// the settings is balanced, 0.571-0.583 vs 0.574-0.586 ms -- a first sweep
+// that always ran 384 first had put 512 2 % ahead; 768 0.725, 256 0.60-0.62)
 static double default_block_work(const rt_context* c, int frames = 1) {
   const FlatScene& f = c->flat;
   double block_work = !f.bvh.empty() ? 8192.0
                       : frames > 1    ? (f.tris.empty() ? 1536.0 : 2048.0)
-                                      : (f.tris.empty() ? 512.0 : 256.0);
+                                      : (f.tris.empty() ? 384.0 : 256.0);
   if (c->tun.block_work > 0) block_work = std::max(1.0, c->tun.block_work);
   return block_work;
 }
