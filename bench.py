@@ -212,7 +212,9 @@ def launch_ranks(args, argv, grace_s=30.0):
     """Start args.gpus rank processes of this script, forward rank 0's stdout,
     return the job's exit status (0 only if every rank exited 0).  When a rank
     fails, the others get `grace_s` seconds to end on their own (their
-    watchdogs), then are terminated by PID."""
+    watchdogs), then are terminated by PID.  If the launcher is itself
+    stopped (SIGTERM / SIGINT / SIGHUP) it ends its ranks first, and a rank
+    whose launcher dies anyway gets SIGTERM from the kernel (PDEATHSIG)."""
     import signal
     import subprocess
     import threading
@@ -220,10 +222,38 @@ def launch_ranks(args, argv, grace_s=30.0):
     n = args.gpus
     port = int(os.environ.get("MASTER_PORT", "0")) or free_port()
     procs = []
+
+    def die_with_parent():  # (in the child, before exec: PR_SET_PDEATHSIG = 1)
+        import ctypes
+
+        ctypes.CDLL(None).prctl(1, signal.SIGTERM)
+
+    def stop_all(signum, _frame):
+        # the launcher itself is being stopped (a driver's time limit): its
+        # ranks live in sessions of their own, so end them here, by PID
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except OSError:
+                    pass
+        t_end = time.monotonic() + 10
+        while time.monotonic() < t_end and any(p.poll() is None for p in procs):
+            time.sleep(0.1)
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except OSError:
+                    pass
+        os._exit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, stop_all)
     for r, env in enumerate(rank_envs(n, port)):
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env,
                                       stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
-                                      stderr=None, start_new_session=True))
+                                      stderr=None, start_new_session=True, preexec_fn=die_with_parent))
 
     def pump(p):
         for line in iter(p.stdout.readline, b""):

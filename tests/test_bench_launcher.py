@@ -63,3 +63,48 @@ def test_one_gpu_does_not_launch():
     assert p.returncode == 0, p.stderr
     d = json.loads(p.stdout.strip())
     assert d["rank"] == 0 and d["env"]["WORLD_SIZE"] is None
+
+
+def _alive(pid):
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    with open(f"/proc/{pid}/stat") as f:  # (a zombie is gone for our purpose)
+        return f.read().split(") ")[1][0] != "Z"
+
+
+def _start_with_hung_rank():
+    """The launcher with rank 1 hung (rank 0 done): returns (launcher, rank 1 pid)."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.Popen([sys.executable, BENCH, "--gpus", "2", "--launch-dry-run", "--dry-run-hang-rank", "1"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+    for line in p.stderr:
+        if line.startswith("{"):
+            d = json.loads(line)
+            if d["rank"] == 1:
+                return p, d["pid"]
+    raise AssertionError("rank 1 never reported")
+
+
+@pytest.mark.parametrize("sig", ["SIGTERM", "SIGKILL"])
+def test_a_stopped_launcher_takes_its_ranks_along(sig):
+    """A driver's time limit stops the launcher: SIGTERM -> it ends its ranks
+    itself; SIGKILL (no handler runs) -> the kernel's parent-death signal."""
+    import signal
+
+    p, pid1 = _start_with_hung_rank()
+    try:
+        assert _alive(pid1)
+        p.send_signal(getattr(signal, sig))
+        p.wait(timeout=30)
+        t_end = time.monotonic() + 20
+        while _alive(pid1) and time.monotonic() < t_end:
+            time.sleep(0.1)
+        assert not _alive(pid1), f"rank 1 (pid {pid1}) outlived its launcher"
+    finally:
+        if p.poll() is None:
+            p.kill()
+        if _alive(pid1):
+            os.kill(pid1, 9)
