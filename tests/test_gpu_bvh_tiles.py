@@ -14,6 +14,11 @@ and rendered them: tests/golden/oracle_c4_tiles.npz, oracle_c5_tiles.npz.
 - C5 (configs[4], 3840x2160x256 over 8 GPUs): the packed shares of ranks 0
   and 7 of 8 (exactly what those GPUs render); their 2 heaviest surveyed
   tiles each equal the oracle's bit for bit.
+- (r06) A wider sample, tests/golden/oracle_c4_tiles_more.npz and
+  oracle_c5_tiles_more.npz: 12 more C4 tiles spread over the survey's
+  ranking (heavy to light, all over the frame), checked in the same frame
+  and for path counts; 2 tiles each of C5 ranks 3 and 5, in those ranks'
+  shares.
 Tolerance (north star): per-channel RMSE < 1e-4; asserted: max |diff| == 0.
 """
 import os
@@ -31,10 +36,18 @@ pytestmark = pytest.mark.gpu
 PATH_KEYS = ("camera_rays", "bounce_rays", "shadow_rays", "shade_events", "light_evals", "rng_draws")
 
 
-def _fixture(name):
-    g = np.load(os.path.join(GOLDEN, f"oracle_{name}_tiles.npz"))
+def _fixture(name, suffix=""):
+    g = np.load(os.path.join(GOLDEN, f"oracle_{name}_tiles{suffix}.npz"))
     w, h, spp, depth, seed = (int(v) for v in g["config"])
     return g, w, h, make_settings(rtgo, {"samples": spp, "max_depth": depth}, seed=seed)
+
+
+def _c4_fixtures():
+    """(tiles, linear, rgba, counts) of both C4 samples, concatenated."""
+    g, w, h, st = _fixture("c4")
+    m = _fixture("c4", "_more")[0]
+    assert tuple(m["config"]) == tuple(g["config"])
+    return ({k: np.concatenate([g[k], m[k]]) for k in ("tiles", "linear", "rgba", "counts")}, w, h, st)
 
 
 def _tile_of_image(img, w, t):
@@ -44,7 +57,7 @@ def _tile_of_image(img, w, t):
 
 
 def test_c4_full_frame_tiles_match_oracle():
-    g, w, h, st = _fixture("c4")
+    g, w, h, st = _c4_fixtures()
     scene = spheres10k_scene(rtgo)
     lin, rgba, _, _ = render_dev(scene, w, h, st)
     lin, rgba = lin.reshape(h, w, 3), rgba.reshape(h, w, 4)
@@ -62,7 +75,7 @@ def test_c4_tile_path_counts_match_oracle():
     """Each fixture tile alone (rank t of world = #tiles): the wavefront
     path's path counts equal the oracle's (camera, bounce and shadow rays,
     shading events, light evaluations, RNG draws)."""
-    g, w, h, st = _fixture("c4")
+    g, w, h, st = _c4_fixtures()
     scene = spheres10k_scene(rtgo)
     n = rtgo.num_tiles(w, h)
     for i, t in enumerate(g["tiles"]):
@@ -71,9 +84,9 @@ def test_c4_tile_path_counts_match_oracle():
         assert {k: c[k] for k in PATH_KEYS} == {k: want[k] for k in PATH_KEYS}, f"tile {t}"
 
 
-@pytest.mark.parametrize("rank", [0, 7])
-def test_c5_rank_shares_match_oracle(rank):
-    g, w, h, st = _fixture("c5")
+@pytest.mark.parametrize("rank,suffix", [(0, ""), (7, ""), (3, "_more"), (5, "_more")])
+def test_c5_rank_shares_match_oracle(rank, suffix):
+    g, w, h, st = _fixture("c5", suffix)
     world = 8
     scene = spheres10k_scene(rtgo)
     lin, rgba, _, _ = render_dev(scene, w, h, st, rank=rank, world=world)
