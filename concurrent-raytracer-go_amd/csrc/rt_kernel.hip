@@ -74,8 +74,8 @@ constexpr int kSqTries = RT_SQ_TRIES;
 #ifndef RT_SOLO
 #define RT_SOLO 0
 #endif
-#ifndef RT_CONE_WIDE
-#define RT_CONE_WIDE 1
+#ifndef RT_CONE_HELPERS  // (not RT_CONE_WIDE: rt_internal.h's candidate-list width)
+#define RT_CONE_HELPERS 1
 #endif
 
 namespace rtgo {
@@ -2014,7 +2014,7 @@ __device__ __forceinline__ void render_body(const KParams& pk) {
           const bool hard = shade && lit && (kCount || !dark);
           bool wide_c = false;
           if constexpr (kStage) {  // few lit hit points: the cone tests with helpers
-            if (masks && gg.nt == 0 && RT_CONE_WIDE) {
+            if (masks && gg.nt == 0 && RT_CONE_HELPERS) {
               const unsigned long long cq = __ballot(hard);
               const int ncq = __popcll(cq);
               if (ncq > 0 && ncq <= 16) {
