@@ -647,8 +647,8 @@ static void base_params(const rt_context* c, int w, int h, const rt_settings* st
   p.stack_depth = std::max(1, f.bvh_depth);
 }
 
-// Tail helpers for a megakernel launch of p: the product
-// instantiation on a staged linear-scan scene with shadow-cone masks (what
+// Tail helpers for a megakernel launch of p: render_kernel_tail
+// (the staged product body) on a linear-scan scene with shadow-cone masks (what
 // solo_path needs), one sample pass, no sky, not measuring.  Lays out the
 // context's queue and rows for p.spp_total samples per pixel (the control
 // block and ready flags zeroed once per layout: each launch's last helper

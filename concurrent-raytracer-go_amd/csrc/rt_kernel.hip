@@ -2440,8 +2440,8 @@ int launch_render(const KParams& pin, bool count, void* stream) {
   }
   const size_t shmem = render_shmem(p);
   const bool stage = p.stage_bytes > 0;
-  // tail helpers: only the product instantiation exports
-  // paths; tail_helpers one-wave workgroups follow its num_wgs main blocks
+  // tail helpers: render_kernel_tail exports paths;
+  // tail_helpers one-wave workgroups follow its num_wgs main blocks
   const bool tail = p.tail && stage && !count && !p.sky && !p.work_max && p.acc_mode == 0 && p.tail_helpers > 0;
   if (!tail) p.tail = nullptr;
   const dim3 g(p.num_wgs + (tail ? p.tail_helpers : 0)), b(64);
